@@ -1,0 +1,206 @@
+/*
+ * pebble_amd.h — C-ABI of the MI355X-native Pebble SSTable data-block decoder.
+ *
+ * This is the drop-in boundary described in SURVEY.md §8(b).  A thin cgo shim
+ * behind Pebble's `sstable/blockiter.Data` interface (or the Python host layer
+ * in pebble_amd/) calls these entry points once per BATCH of data blocks; the
+ * per-KV work runs in hand-written gfx950 HIP kernels.
+ *
+ * Reference interfaces replaced (paths relative to cockroachdb/pebble):
+ *   pbl_decode_batch      rowblk.Iter.Init/First/Next  sstable/rowblk/rowblk_iter.go:241-276,1061-1087,1145-1201
+ *                         colblk.DataBlockDecoder.Init sstable/colblk/data_block.go:1096-1109
+ *                         colblk.DataBlockIter.Next    sstable/colblk/data_block.go:1662-1708
+ *                         (driven by singleLevelIterator.loadDataBlock, sstable/reader_iter_single_lvl.go:485-547)
+ *   pbl_rowblk_writer_*   rowblk.Writer                sstable/rowblk/rowblk_writer.go:48-320 (format producer)
+ *   PBL_STATUS_*          base.CorruptionErrorf sites  sstable/rowblk/rowblk_iter.go:249-251,471-476;
+ *                                                      sstable/colblk/data_block.go:1005-1009
+ *
+ * Conventions
+ *   - Every pointer in pbl_block_batch / pbl_decode_out is a DEVICE pointer unless
+ *     the field says otherwise.  The caller owns every buffer; the library never
+ *     allocates or frees caller memory (mirrors block.BufferHandle ownership,
+ *     sstable/blockiter/block_iter.go:76-81).
+ *   - `stream` is a hipStream_t passed as void* (0 = legacy default stream).  All
+ *     device entry points are stream-ordered and asynchronous; they never
+ *     synchronise and are safe to capture into a hipGraph.
+ *   - The library holds no global mutable state; it is reentrant across
+ *     streams and devices.
+ */
+#ifndef PEBBLE_AMD_H
+#define PEBBLE_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PBL_ABI_VERSION 1
+
+/* ---- status codes (per block, and OR-ed as bit masks into totals) ---------- */
+enum {
+  PBL_OK = 0,
+  PBL_CORRUPT_NO_RESTARTS = 1,   /* rowblk_iter.go:249-251 */
+  PBL_CORRUPT_FIRST_KEY = 2,     /* rowblk_iter.go:429-434,471-476 */
+  PBL_CORRUPT_BOUNDS = 3,        /* entry/column extends past the block */
+  PBL_CORRUPT_COLBLK_HEADER = 4, /* data_block.go:1005-1009 (panic -> corruption) */
+  PBL_UNSUPPORTED = 5,           /* legal but outside this build's limits */
+  PBL_OVERFLOW = 6,              /* an output capacity was too small: nothing written */
+  PBL_INVALID_ARG = 7,
+  PBL_DEVICE_ERROR = 8,
+  PBL_TIMEOUT = 9                /* in-kernel look-back spin bound hit (never expected) */
+};
+
+/* ---- block formats ---------------------------------------------------------- */
+enum {
+  PBL_FMT_ROW = 0,          /* sstable/rowblk data block                          */
+  PBL_FMT_COL_DEFAULT = 1,  /* colblk data block, colblk.DefaultKeySchema          */
+  PBL_FMT_COL_CRDB1 = 2     /* colblk data block, cockroachkvs.KeySchema ("crdb1") */
+};
+
+/* batch flags */
+#define PBL_ROW_VALUE_PREFIX 0x1u /* TableFormat >= Pebblev3: SET values carry a
+                                     1-byte block.ValuePrefix (rowblk_iter.go:298-300) */
+#define PBL_ROW_NO_VALUER 0x2u    /* iterator has no lazy valuer: strip the prefix
+                                     byte even for handles (rowblk_iter.go:1195)   */
+#define PBL_ROW_RAW_KEYS 0x4u     /* rowblk.RawIter semantics (rowblk_iter.go:1743-1794):
+                                     keys are emitted whole, no trailer split, no
+                                     first-key check; trailer[] = 0              */
+
+/* per-KV flag byte (kv_flags[]) */
+#define PBL_KV_RESTART 0x01u       /* entry offset is a restart point            */
+#define PBL_KV_RESTART_SAMEPFX 0x02u /* restart word bit 31 (setHasSameKeyPrefix) */
+#define PBL_KV_OBSOLETE 0x04u      /* trailer had InternalKeyKindSSTableInternalObsoleteBit */
+#define PBL_KV_INVALID_KEY 0x08u   /* key < 8 bytes: kind Invalid, nil user key   */
+#define PBL_KV_VALBLK_HANDLE 0x10u /* value bytes are prefix+valblk.Handle        */
+#define PBL_KV_BLOB_HANDLE 0x20u   /* value bytes are prefix+blob handle / colblk external */
+#define PBL_KV_PREFIX_CHANGED 0x40u /* colblk prefixChanged bit                   */
+
+/* ---- batch descriptor ------------------------------------------------------- */
+typedef struct pbl_block_batch {
+  const uint8_t* blocks;     /* concatenated, already-decompressed block bytes (no 5 B
+                                physical trailer).  Must be readable up to the next
+                                16-byte boundary after every block.                 */
+  const uint64_t* block_off; /* [n_blocks] byte offset of each block in `blocks`    */
+  const uint32_t* block_len; /* [n_blocks] byte length of each block                */
+  uint32_t n_blocks;
+  uint32_t format;           /* PBL_FMT_* for every block of the batch              */
+  uint32_t flags;            /* PBL_ROW_* flags                                     */
+  uint32_t reserved;
+} pbl_block_batch;
+
+/* ---- batch totals (device struct, written by the decode kernel) -------------- */
+typedef struct pbl_totals {
+  uint64_t n_kv;        /* KVs decoded over all blocks                         */
+  uint64_t key_bytes;   /* user-key bytes                                      */
+  uint64_t val_bytes;   /* value bytes                                         */
+  uint64_t n_restarts;  /* restart words (row format)                          */
+  uint32_t status_mask; /* OR of (1u << status) over blocks                    */
+  uint32_t n_bad_blocks;/* blocks whose status != PBL_OK                       */
+  uint32_t n_slow_blocks;/* blocks decoded by the general (non-LDS) path      */
+  uint32_t pad;
+} pbl_totals;
+
+/*
+ * Output arrays (all caller-allocated, device).  Indexing for block b, KV j:
+ *   kv  = blk_kv_base[b] + j                (per-KV arrays)
+ *   o   = blk_kv_base[b] + b + j, j<=nkv_b  (per-block N+1 offset arrays)
+ * key j of block b  = key_bytes[blk_key_base[b] + key_off[o] .. + key_off[o+1])
+ * value j of block b= val_bytes[blk_val_base[b] + val_off[o] .. + val_off[o+1])
+ * restart r of b    = restarts[blk_rst_base[b] + r]  (raw LE32 word, bit 31 kept)
+ * Optional arrays may be NULL.  The blk_*_base arrays have n_blocks+1 entries; the
+ * last entry holds the batch total.  When a capacity is exceeded the kernel still
+ * computes every size (totals, blk_*_base) but writes no bytes, and reports
+ * PBL_OVERFLOW: re-run with larger buffers.
+ */
+typedef struct pbl_decode_out {
+  uint64_t* trailer;      /* [kv_cap] base.InternalKeyTrailer (obsolete bit cleared) */
+  uint8_t* kv_flags;      /* [kv_cap] PBL_KV_* (optional)                        */
+  uint32_t* entry_off;    /* [kv_cap] KVEncoding.Offset of each row entry (optional) */
+  uint32_t* key_off;      /* [kv_cap + n_blocks] block-relative key offsets       */
+  uint32_t* val_off;      /* [kv_cap + n_blocks] block-relative value offsets     */
+  uint8_t* key_bytes;     /* [key_cap]                                            */
+  uint8_t* val_bytes;     /* [val_cap]                                            */
+  uint32_t* restarts;     /* [rst_cap] raw restart words (optional, row format)   */
+  uint64_t* blk_kv_base;  /* [n_blocks+1]                                         */
+  uint64_t* blk_key_base; /* [n_blocks+1]                                         */
+  uint64_t* blk_val_base; /* [n_blocks+1]                                         */
+  uint64_t* blk_rst_base; /* [n_blocks+1] (optional)                              */
+  uint32_t* blk_status;   /* [n_blocks] PBL_* status per block                    */
+  pbl_totals* totals;     /* [1]                                                  */
+  uint64_t kv_cap, key_cap, val_cap, rst_cap;
+  void* workspace;        /* device scratch of pbl_workspace_bytes(n_blocks) bytes */
+  uint64_t workspace_bytes;
+} pbl_decode_out;
+
+/* ABI version of the loaded library (== PBL_ABI_VERSION). */
+int pbl_abi_version(void);
+
+/* Device scratch the decode needs for a batch of n_blocks (look-back state). */
+uint64_t pbl_workspace_bytes(uint32_t n_blocks);
+
+/*
+ * Decode every block of `batch` into `out` on `stream`: one stream-ordered
+ * single-pass launch (plus a memset of the workspace).  Returns PBL_OK or
+ * PBL_INVALID_ARG / PBL_DEVICE_ERROR for launch problems; per-block corruption is
+ * reported in out->blk_status and out->totals (read them after the stream syncs).
+ */
+int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stream);
+
+/*
+ * Offset concat for a sharded batch: add this rank's global
+ * bases (exclusive prefix over lower ranks of n_kv / key_bytes / val_bytes /
+ * n_restarts, all-gathered over RCCL) to the n_blocks+1 entries of each
+ * blk_*_base array.  Per-KV offsets are block-relative and never need rebasing.
+ */
+int pbl_rebase_blocks(pbl_decode_out* out, uint32_t n_blocks, uint64_t kv_base,
+                      uint64_t key_base, uint64_t val_base, uint64_t rst_base,
+                      void* stream);
+
+
+/*
+ * Same offset concat, fully stream-ordered: `rank_totals` is the DEVICE array of
+ * world*4 u64 {n_kv, key_bytes, val_bytes, n_restarts} per rank exactly as an
+ * RCCL all-gather of each rank's pbl_totals prefix leaves it; the kernel forms
+ * this rank's exclusive prefix itself (no host round trip).
+ */
+int pbl_offset_concat(pbl_decode_out* out, uint32_t n_blocks, const uint64_t* rank_totals,
+                      uint32_t rank, void* stream);
+
+/* ---- rowblk.Writer (format producer; host memory) ---------------------------- */
+typedef struct pbl_rowblk_writer pbl_rowblk_writer;
+pbl_rowblk_writer* pbl_rowblk_writer_new(int restart_interval);
+void pbl_rowblk_writer_free(pbl_rowblk_writer* w);
+void pbl_rowblk_writer_reset(pbl_rowblk_writer* w, int restart_interval);
+/* rowblk_writer.go:263-286.  `trailer` is base.InternalKeyTrailer. */
+int pbl_rowblk_writer_add(pbl_rowblk_writer* w, const uint8_t* user_key, size_t user_key_len,
+                          uint64_t trailer, int is_obsolete, const uint8_t* value,
+                          size_t value_len, int64_t max_shared_key_len, int add_value_prefix,
+                          uint8_t value_prefix, int set_has_same_key_prefix);
+/* rowblk_writer.go:323-334 (raw key, no trailer). */
+int pbl_rowblk_writer_add_raw(pbl_rowblk_writer* w, const uint8_t* key, size_t key_len,
+                              const uint8_t* value, size_t value_len);
+size_t pbl_rowblk_writer_estimated_size(const pbl_rowblk_writer* w);
+size_t pbl_rowblk_writer_entry_count(const pbl_rowblk_writer* w);
+/* Finish; copies the block into `dst` if dst_cap suffices; returns the block size. */
+size_t pbl_rowblk_writer_finish(pbl_rowblk_writer* w, uint8_t* dst, size_t dst_cap);
+
+/*
+ * Synthetic batch generator (host memory, multithreaded), SURVEY.md §8(d):
+ * key of row r = BE64(r) || BE64(splitmix64(seed ^ r)) (key_len 16; longer keys
+ * append splitmix bytes), row r = (block << 20) + k, trailer MakeTrailer(r, SET),
+ * value bytes from splitmix64(seed + r).  Each block is filled while
+ * EstimatedSize()+entry <= block_size and is placed at a fixed `block_size`
+ * stride in `dst` (dst must hold n_blocks*block_size bytes).  Fills
+ * block_off/block_len (host arrays) and returns total KVs.
+ */
+uint64_t pbl_gen_row_blocks(uint64_t seed, uint32_t n_blocks, uint32_t block_size,
+                            int restart_interval, uint32_t key_len, uint32_t val_len,
+                            int value_prefix, uint8_t* dst, uint64_t* block_off,
+                            uint32_t* block_len, int n_threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PEBBLE_AMD_H */

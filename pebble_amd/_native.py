@@ -1,0 +1,131 @@
+"""ctypes binding of the C-ABI in include/pebble_amd.h (libpebble_amd.so).
+
+The shared library is built in-tree by pebble_amd.build (hipcc, gfx950) and is
+the only implementation of the decode path: there is no CPU fallback.  Loading
+fails loudly when the library is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpebble_amd.so")
+
+# status codes (include/pebble_amd.h)
+PBL_OK = 0
+PBL_CORRUPT_NO_RESTARTS = 1
+PBL_CORRUPT_FIRST_KEY = 2
+PBL_CORRUPT_BOUNDS = 3
+PBL_CORRUPT_COLBLK_HEADER = 4
+PBL_UNSUPPORTED = 5
+PBL_OVERFLOW = 6
+PBL_INVALID_ARG = 7
+PBL_DEVICE_ERROR = 8
+PBL_TIMEOUT = 9
+STATUS_NAMES = {
+    0: "OK", 1: "CORRUPT_NO_RESTARTS", 2: "CORRUPT_FIRST_KEY", 3: "CORRUPT_BOUNDS",
+    4: "CORRUPT_COLBLK_HEADER", 5: "UNSUPPORTED", 6: "OVERFLOW", 7: "INVALID_ARG",
+    8: "DEVICE_ERROR", 9: "TIMEOUT",
+}
+
+PBL_FMT_ROW = 0
+PBL_FMT_COL_DEFAULT = 1
+PBL_FMT_COL_CRDB1 = 2
+
+PBL_ROW_VALUE_PREFIX = 0x1
+PBL_ROW_NO_VALUER = 0x2
+PBL_ROW_RAW_KEYS = 0x4
+
+PBL_KV_RESTART = 0x01
+PBL_KV_RESTART_SAMEPFX = 0x02
+PBL_KV_OBSOLETE = 0x04
+PBL_KV_INVALID_KEY = 0x08
+PBL_KV_VALBLK_HANDLE = 0x10
+PBL_KV_BLOB_HANDLE = 0x20
+PBL_KV_PREFIX_CHANGED = 0x40
+
+_vp = ctypes.c_void_p
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+class BlockBatchC(ctypes.Structure):
+    _fields_ = [
+        ("blocks", _vp), ("block_off", _vp), ("block_len", _vp),
+        ("n_blocks", ctypes.c_uint32), ("format", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+    ]
+
+
+class TotalsC(ctypes.Structure):
+    _fields_ = [
+        ("n_kv", ctypes.c_uint64), ("key_bytes", ctypes.c_uint64),
+        ("val_bytes", ctypes.c_uint64), ("n_restarts", ctypes.c_uint64),
+        ("status_mask", ctypes.c_uint32), ("n_bad_blocks", ctypes.c_uint32),
+        ("n_slow_blocks", ctypes.c_uint32), ("pad", ctypes.c_uint32),
+    ]
+
+
+class DecodeOutC(ctypes.Structure):
+    _fields_ = [
+        ("trailer", _vp), ("kv_flags", _vp), ("entry_off", _vp),
+        ("key_off", _vp), ("val_off", _vp), ("key_bytes", _vp), ("val_bytes", _vp),
+        ("restarts", _vp), ("blk_kv_base", _vp), ("blk_key_base", _vp),
+        ("blk_val_base", _vp), ("blk_rst_base", _vp), ("blk_status", _vp),
+        ("totals", _vp),
+        ("kv_cap", ctypes.c_uint64), ("key_cap", ctypes.c_uint64),
+        ("val_cap", ctypes.c_uint64), ("rst_cap", ctypes.c_uint64),
+        ("workspace", _vp), ("workspace_bytes", ctypes.c_uint64),
+    ]
+
+
+# Every symbol include/pebble_amd.h declares, with its ctypes signature.
+SIGNATURES = {
+    "pbl_abi_version": (ctypes.c_int, []),
+    "pbl_workspace_bytes": (ctypes.c_uint64, [ctypes.c_uint32]),
+    "pbl_decode_batch": (ctypes.c_int, [ctypes.POINTER(BlockBatchC), ctypes.POINTER(DecodeOutC), _vp]),
+    "pbl_rebase_blocks": (ctypes.c_int, [ctypes.POINTER(DecodeOutC), ctypes.c_uint32, ctypes.c_uint64,
+                                         ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _vp]),
+    "pbl_offset_concat": (ctypes.c_int, [ctypes.POINTER(DecodeOutC), ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]),
+    "pbl_rowblk_writer_new": (_vp, [ctypes.c_int]),
+    "pbl_rowblk_writer_free": (None, [_vp]),
+    "pbl_rowblk_writer_reset": (None, [_vp, ctypes.c_int]),
+    "pbl_rowblk_writer_add": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64,
+                                             ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t,
+                                             ctypes.c_int64, ctypes.c_int, ctypes.c_uint8, ctypes.c_int]),
+    "pbl_rowblk_writer_add_raw": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_size_t,
+                                                 ctypes.c_char_p, ctypes.c_size_t]),
+    "pbl_rowblk_writer_estimated_size": (ctypes.c_size_t, [_vp]),
+    "pbl_rowblk_writer_entry_count": (ctypes.c_size_t, [_vp]),
+    "pbl_rowblk_writer_finish": (ctypes.c_size_t, [_vp, _vp, ctypes.c_size_t]),
+    "pbl_gen_row_blocks": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                             ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                             _vp, _vp, _vp, ctypes.c_int]),
+}
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libpebble_amd.so (torch is imported first so that the HIP runtime it
+    bundles is the one the library binds to: same SONAME, one runtime)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950).  There is no CPU fallback for the decode path.")
+    try:
+        import torch  # noqa: F401  (binds libamdhip64.so.7 first)
+    except Exception:  # pragma: no cover - torch is always present in this image
+        pass
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    if L.pbl_abi_version() != 1:
+        raise RuntimeError("libpebble_amd.so ABI mismatch")
+    _lib = L
+    return L

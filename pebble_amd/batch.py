@@ -1,0 +1,231 @@
+"""Device-resident block batches and the batch decode (host side of the C-ABI).
+
+A `BlockBatch` holds raw, already-decompressed data blocks in HBM; `decode()`
+runs the single-pass HIP decoder over it and returns a `DecodedBatch` whose
+arrays follow include/pebble_amd.h exactly.  torch is only plumbing here
+(device memory, streams); the work is done by libpebble_amd.so.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+
+def _dp(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream_handle(stream: Optional[torch.cuda.Stream]) -> ctypes.c_void_p:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class DecodeError(RuntimeError):
+    pass
+
+
+@dataclass
+class BlockBatch:
+    """Raw data blocks resident on one device (concatenated, 16-B readable slack)."""
+    blocks: torch.Tensor        # uint8 [bytes (+16 pad)]
+    block_off: torch.Tensor     # int64 [n]  (uint64 in the ABI)
+    block_len: torch.Tensor     # int32 [n]  (uint32 in the ABI)
+    format: int = N.PBL_FMT_ROW
+    flags: int = 0
+
+    @property
+    def n_blocks(self) -> int:
+        return int(self.block_off.numel())
+
+    @property
+    def device(self) -> torch.device:
+        return self.blocks.device
+
+    @classmethod
+    def from_host(cls, blocks: np.ndarray, off: np.ndarray, lens: np.ndarray, device="cuda",
+                  fmt: int = N.PBL_FMT_ROW, flags: int = 0, non_blocking: bool = False) -> "BlockBatch":
+        blocks = np.ascontiguousarray(blocks, dtype=np.uint8)
+        pad = np.zeros(len(blocks) + 16, np.uint8)
+        pad[: len(blocks)] = blocks
+        b = torch.from_numpy(pad).to(device, non_blocking=non_blocking)
+        o = torch.from_numpy(np.ascontiguousarray(off, dtype=np.uint64).view(np.int64)).to(device)
+        l = torch.from_numpy(np.ascontiguousarray(lens, dtype=np.uint32).view(np.int32)).to(device)
+        return cls(b, o, l, fmt, flags)
+
+    @classmethod
+    def from_blocks(cls, blocks: list, device="cuda", fmt: int = N.PBL_FMT_ROW, flags: int = 0,
+                    align: int = 8) -> "BlockBatch":
+        """Pack a list of block byte strings (each start `align`-aligned)."""
+        offs, lens, pos = [], [], 0
+        for bk in blocks:
+            pos = (pos + align - 1) // align * align
+            offs.append(pos)
+            lens.append(len(bk))
+            pos += len(bk)
+        buf = np.zeros(max(pos, 1), np.uint8)
+        for o, bk in zip(offs, blocks):
+            buf[o:o + len(bk)] = np.frombuffer(bk, np.uint8)
+        return cls.from_host(buf, np.array(offs, np.uint64), np.array(lens, np.uint32), device, fmt, flags)
+
+    def c_struct(self) -> N.BlockBatchC:
+        return N.BlockBatchC(self.blocks.data_ptr(), self.block_off.data_ptr(), self.block_len.data_ptr(),
+                             self.n_blocks, self.format, self.flags, 0)
+
+    def input_bytes(self) -> int:
+        return int(self.block_len.to(torch.int64).sum().item()) if self.n_blocks else 0
+
+
+@dataclass
+class Capacity:
+    kv: int
+    key: int
+    val: int
+    rst: int
+
+    @classmethod
+    def estimate(cls, batch: BlockBatch) -> "Capacity":
+        tot = max(batch.input_bytes(), 1)
+        nb = batch.n_blocks
+        # values never exceed the input; keys and KV counts are heuristics that
+        # are corrected by one re-run when the kernel reports PBL_OVERFLOW.
+        return cls(kv=tot // 24 + 64 * nb + 64, key=tot // 2 + 64, val=tot + 64, rst=tot // 16 + 16 * nb + 16)
+
+
+@dataclass
+class DecodedBatch:
+    n_blocks: int
+    trailer: torch.Tensor
+    kv_flags: torch.Tensor
+    entry_off: Optional[torch.Tensor]
+    key_off: torch.Tensor
+    val_off: torch.Tensor
+    key_bytes: torch.Tensor
+    val_bytes: torch.Tensor
+    restarts: Optional[torch.Tensor]
+    blk_kv_base: torch.Tensor
+    blk_key_base: torch.Tensor
+    blk_val_base: torch.Tensor
+    blk_rst_base: torch.Tensor
+    blk_status: torch.Tensor
+    totals: torch.Tensor          # uint8 view of pbl_totals
+    workspace: torch.Tensor
+    cap: Capacity
+    _host_totals: Optional[N.TotalsC] = field(default=None, repr=False)
+
+    @classmethod
+    def allocate(cls, n_blocks: int, cap: Capacity, device, entry_off: bool = True,
+                 restarts: bool = True) -> "DecodedBatch":
+        d = torch.device(device)
+        u = lambda n, dt: torch.empty(max(int(n), 1), dtype=dt, device=d)  # noqa: E731
+        lib = N.lib()
+        ws = int(lib.pbl_workspace_bytes(n_blocks))
+        return cls(
+            n_blocks=n_blocks,
+            trailer=u(cap.kv, torch.int64), kv_flags=u(cap.kv, torch.uint8),
+            entry_off=u(cap.kv, torch.int32) if entry_off else None,
+            key_off=u(cap.kv + n_blocks, torch.int32), val_off=u(cap.kv + n_blocks, torch.int32),
+            key_bytes=u(cap.key + 16, torch.uint8), val_bytes=u(cap.val + 16, torch.uint8),
+            restarts=u(cap.rst, torch.int32) if restarts else None,
+            blk_kv_base=u(n_blocks + 1, torch.int64), blk_key_base=u(n_blocks + 1, torch.int64),
+            blk_val_base=u(n_blocks + 1, torch.int64), blk_rst_base=u(n_blocks + 1, torch.int64),
+            blk_status=u(n_blocks, torch.int32),
+            totals=torch.zeros(ctypes.sizeof(N.TotalsC), dtype=torch.uint8, device=d),
+            workspace=u(ws, torch.uint8), cap=cap,
+        )
+
+    def c_struct(self) -> N.DecodeOutC:
+        c = self.cap
+        return N.DecodeOutC(
+            self.trailer.data_ptr(), self.kv_flags.data_ptr(),
+            self.entry_off.data_ptr() if self.entry_off is not None else None,
+            self.key_off.data_ptr(), self.val_off.data_ptr(), self.key_bytes.data_ptr(),
+            self.val_bytes.data_ptr(), self.restarts.data_ptr() if self.restarts is not None else None,
+            self.blk_kv_base.data_ptr(), self.blk_key_base.data_ptr(), self.blk_val_base.data_ptr(),
+            self.blk_rst_base.data_ptr(), self.blk_status.data_ptr(), self.totals.data_ptr(),
+            c.kv, c.key, c.val, c.rst if self.restarts is not None else 0,
+            self.workspace.data_ptr(), self.workspace.numel(),
+        )
+
+    # ---- host readouts ------------------------------------------------------------
+    def read_totals(self) -> N.TotalsC:
+        raw = self.totals.cpu().numpy().tobytes()
+        t = N.TotalsC.from_buffer_copy(raw)
+        self._host_totals = t
+        return t
+
+    def to_host(self) -> dict:
+        """Copy every array back (sized by the totals) as numpy, oracle layout."""
+        t = self.read_totals()
+        nb, n = self.n_blocks, int(t.n_kv)
+        g = lambda x, k, dt: x[:k].cpu().numpy().view(dt) if k else np.zeros(0, dt)  # noqa: E731
+        r = {
+            "trailer": g(self.trailer, n, np.uint64), "kv_flags": g(self.kv_flags, n, np.uint8),
+            "entry_off": g(self.entry_off, n, np.uint32) if self.entry_off is not None else None,
+            "key_off": g(self.key_off, n + nb, np.uint32), "val_off": g(self.val_off, n + nb, np.uint32),
+            "key_bytes": g(self.key_bytes, int(t.key_bytes), np.uint8),
+            "val_bytes": g(self.val_bytes, int(t.val_bytes), np.uint8),
+            "restarts": g(self.restarts, int(t.n_restarts), np.uint32) if self.restarts is not None else None,
+            "blk_kv_base": g(self.blk_kv_base, nb + 1, np.uint64),
+            "blk_key_base": g(self.blk_key_base, nb + 1, np.uint64),
+            "blk_val_base": g(self.blk_val_base, nb + 1, np.uint64),
+            "blk_rst_base": g(self.blk_rst_base, nb + 1, np.uint64),
+            "blk_status": g(self.blk_status, nb, np.uint32),
+            "n_kv": n, "key_bytes_total": int(t.key_bytes), "val_bytes_total": int(t.val_bytes),
+            "n_restarts": int(t.n_restarts), "status_mask": int(t.status_mask),
+            "n_bad_blocks": int(t.n_bad_blocks), "n_slow_blocks": int(t.n_slow_blocks),
+        }
+        return r
+
+
+def decode_into(batch: BlockBatch, out: DecodedBatch, stream=None) -> None:
+    """Launch the decode of `batch` into preallocated `out` (asynchronous)."""
+    lib = N.lib()
+    b = batch.c_struct()
+    o = out.c_struct()
+    rc = lib.pbl_decode_batch(ctypes.byref(b), ctypes.byref(o), _stream_handle(stream))
+    if rc != N.PBL_OK:
+        raise DecodeError(f"pbl_decode_batch failed: {N.STATUS_NAMES.get(rc, rc)}")
+
+
+def decode(batch: BlockBatch, cap: Optional[Capacity] = None, stream=None, entry_off: bool = True,
+           restarts: bool = True) -> DecodedBatch:
+    """Decode a batch; re-runs once with exact capacities on PBL_OVERFLOW."""
+    cap = cap or Capacity.estimate(batch)
+    out = DecodedBatch.allocate(batch.n_blocks, cap, batch.device, entry_off, restarts)
+    decode_into(batch, out, stream)
+    torch.cuda.current_stream().synchronize() if stream is None else stream.synchronize()
+    t = out.read_totals()
+    if t.status_mask & (1 << N.PBL_OVERFLOW):
+        cap = Capacity(kv=int(t.n_kv) + 1, key=int(t.key_bytes) + 1, val=int(t.val_bytes) + 1,
+                       rst=int(t.n_restarts) + 1)
+        out = DecodedBatch.allocate(batch.n_blocks, cap, batch.device, entry_off, restarts)
+        decode_into(batch, out, stream)
+        torch.cuda.current_stream().synchronize() if stream is None else stream.synchronize()
+        out.read_totals()
+    return out
+
+
+def rebase(out: DecodedBatch, kv: int, key: int, val: int, rst: int, stream=None) -> None:
+    """Offset concat for a sharded batch: add this rank's global bases."""
+    lib = N.lib()
+    o = out.c_struct()
+    rc = lib.pbl_rebase_blocks(ctypes.byref(o), out.n_blocks, kv, key, val, rst, _stream_handle(stream))
+    if rc != N.PBL_OK:
+        raise DecodeError(f"pbl_rebase_blocks failed: {N.STATUS_NAMES.get(rc, rc)}")
+
+
+def offset_concat(out: DecodedBatch, rank_totals: torch.Tensor, rank: int, stream=None) -> None:
+    """Device-side offset concat: `rank_totals` is the int64 [world*4] tensor an
+    RCCL all-gather of every rank's totals prefix produced."""
+    lib = N.lib()
+    o = out.c_struct()
+    rc = lib.pbl_offset_concat(ctypes.byref(o), out.n_blocks, ctypes.c_void_p(rank_totals.data_ptr()), rank,
+                               _stream_handle(stream))
+    if rc != N.PBL_OK:
+        raise DecodeError(f"pbl_offset_concat failed: {N.STATUS_NAMES.get(rc, rc)}")

@@ -1,0 +1,136 @@
+// common.hip.h — shared device helpers for the gfx950 block decoders:
+// wave/block scans, LDS byte access, the decoupled look-back that places every
+// block's outputs in ONE pass (no separate size pass), and granule-aligned
+// byte-range stores.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pebble_amd.h"
+
+namespace pbl {
+
+constexpr int kTPB = 256;   // threads per workgroup (4 waves); one workgroup per block
+constexpr int kWave = 64;
+constexpr int kNumComp = 4; // look-back components: n_kv, key bytes, value bytes, restarts
+
+// ---- workspace layout ------------------------------------------------------
+// [0,256): ticket counter (+ pad).  Then kNumComp arrays of n_blocks u64
+// granules {state:2 | value:62} written and read with agent-scope relaxed
+// atomics (8-byte sc1 accesses: the data IS the flag, no fences needed —
+// MI355X_MICROARCH.md "Valid forms", R2 granules).
+constexpr uint64_t kWsHeader = 256;
+constexpr uint64_t kStateAgg = 1ull << 62;
+constexpr uint64_t kStatePfx = 2ull << 62;
+constexpr uint64_t kValMask = (1ull << 62) - 1;
+
+__host__ __device__ inline uint64_t ws_bytes(uint32_t n_blocks) {
+  return kWsHeader + uint64_t(kNumComp) * n_blocks * 8ull;
+}
+
+__device__ inline uint64_t ld_agent(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void st_agent(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ inline int lane_id() { return threadIdx.x & (kWave - 1); }
+__device__ inline int wave_id() { return threadIdx.x >> 6; }
+
+// In-wave ordering of LDS traffic between lanes (no workgroup barrier).
+__device__ inline void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <typename T>
+__device__ inline T wave_incl_scan(T v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    T o = __shfl_up(v, d, kWave);
+    if (l >= d) v += o;
+  }
+  return v;
+}
+template <typename T>
+__device__ inline T wave_sum(T v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, kWave);
+  return v;
+}
+
+// Block-wide exclusive scan of two u32 sequences held 2 items per thread.
+// `scratch` must hold 2*(kTPB/kWave) u32.  Returns the exclusive prefix of this
+// thread's first item; totals via *tot0/*tot1.  Caller must __syncthreads()
+// before reusing scratch.
+__device__ inline void block_excl_scan2(uint32_t a, uint32_t b, uint32_t* ea, uint32_t* eb,
+                                        uint32_t* scratch, uint32_t* tot_a, uint32_t* tot_b) {
+  uint32_t ia = wave_incl_scan(a), ib = wave_incl_scan(b);
+  const int w = wave_id(), l = lane_id();
+  if (l == kWave - 1) { scratch[w] = ia; scratch[4 + w] = ib; }
+  __syncthreads();
+  uint32_t pa = 0, pb = 0, ta = 0, tb = 0;
+#pragma unroll
+  for (int i = 0; i < kTPB / kWave; i++) {
+    uint32_t sa = scratch[i], sb = scratch[4 + i];
+    if (i < w) { pa += sa; pb += sb; }
+    ta += sa; tb += sb;
+  }
+  *ea = pa + ia - a;
+  *eb = pb + ib - b;
+  *tot_a = ta;
+  *tot_b = tb;
+}
+
+// Decoupled look-back (single-pass scan across blocks).  Executed by wave 0 of
+// the workgroup that owns virtual block `v` (tickets are handed out in launch
+// order, so every predecessor is already resident and publishes its aggregate
+// before it waits: no deadlock for any residency).  Returns exclusive prefixes.
+__device__ inline void lookback(uint64_t* st, uint32_t n_blocks, uint32_t v,
+                                const uint64_t agg[kNumComp], uint64_t excl[kNumComp],
+                                uint32_t* timeout_flag) {
+  const int l = lane_id();
+  // publish aggregates (block 0 publishes its inclusive prefix directly)
+  if (l < kNumComp) {
+    uint64_t a = l == 0 ? agg[0] : l == 1 ? agg[1] : l == 2 ? agg[2] : agg[3];
+    st_agent(st + uint64_t(l) * n_blocks + v, (v == 0 ? kStatePfx : kStateAgg) | (a & kValMask));
+  }
+#pragma unroll
+  for (int c = 0; c < kNumComp; c++) {
+    uint64_t acc = 0;
+    if (v > 0) {
+      int64_t top = int64_t(v) - 1;
+      uint32_t spins = 0;
+      const uint64_t* sc = st + uint64_t(c) * n_blocks;
+      for (;;) {
+        int64_t idx = top - l;
+        uint64_t g = idx >= 0 ? ld_agent(sc + idx) : kStatePfx;
+        uint64_t state = g >> 62;
+        uint64_t pfx = __ballot(state == 2);
+        uint64_t notready = __ballot(state == 0);
+        int first = pfx ? __builtin_ctzll(pfx) : 64;
+        uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
+        if (notready & need) {
+          if (++spins > (1u << 24)) { if (l == 0) atomicOr(timeout_flag, 1u << PBL_TIMEOUT); break; }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        uint64_t val = (l <= first) ? (g & kValMask) : 0;
+        acc += wave_sum(val);
+        if (first < 64) break;
+        top -= kWave;
+      }
+    }
+    excl[c] = acc;
+  }
+  if (l < kNumComp) {
+    uint64_t e = l == 0 ? excl[0] : l == 1 ? excl[1] : l == 2 ? excl[2] : excl[3];
+    uint64_t a = l == 0 ? agg[0] : l == 1 ? agg[1] : l == 2 ? agg[2] : agg[3];
+    if (v > 0) st_agent(st + uint64_t(l) * n_blocks + v, kStatePfx | ((e + a) & kValMask));
+  }
+}
+
+}  // namespace pbl

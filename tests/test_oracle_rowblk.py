@@ -1,0 +1,185 @@
+"""Pin the CPU oracle (oracle/rowblk_oracle.c) and the native rowblk writer to
+the reference's golden vectors.  CPU only."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from ddutil import parse_ikeys, run_iter_cmds
+from pebble_amd import _native as N
+from pebble_amd.rowblk import InternalKV, Iter, Transforms, Writer, gen_row_blocks, make_trailer
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def uvarint_encode(v: int) -> bytes:
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def test_decode_varint_kat(golden):
+    # sstable/rowblk/unsafe_test.go:19-42
+    for v in golden["varint_kat"]:
+        got, n = oracle.decode_varint(uvarint_encode(v) + b"\x00" * 4)
+        assert got == v and n == len(uvarint_encode(v))
+
+
+def test_decode_varint_5th_byte_truncation():
+    # rowblk_iter.go:2034-2036: uint32(e)<<28 keeps only the low 4 bits of e
+    got, n = oracle.decode_varint(b"\xff\xff\xff\xff\x7f")
+    assert n == 5 and got == 0xFFFFFFFF
+    got, n = oracle.decode_varint(b"\x80\x80\x80\x80\x7f")
+    assert got == (0x7F << 28) & 0xFFFFFFFF
+
+
+def test_writer_golden_bytes(golden):
+    # TestBlockWriter, rowblk_writer_test.go:44-59
+    g = golden["writer_basic"]
+    w = Writer(g["restart_interval"])
+    for k, v in g["raw_kvs"]:
+        w.add_raw(k.encode(), v.encode())
+    assert w.finish().hex() == g["block_hex"]
+
+
+def test_writer_with_prefix_golden_bytes(golden):
+    # TestBlockWriterWithPrefix, rowblk_writer_test.go:61-118
+    g = golden["writer_with_prefix"]
+    w = Writer(g["restart_interval"])
+    for k, v, addp, vp, same in g["adds"]:
+        w.add_with_optional_value_prefix(k.encode(), 0, False, v.encode(), len(k), addp, vp, same)
+    assert w.finish().hex() == g["block_hex"]
+
+
+def test_oracle_raw_iter_on_writer_block(golden):
+    blk = bytes.fromhex(golden["writer_basic"]["block_hex"])
+    # Iter.Init rejects it: first key "apple" is shorter than a trailer (rowblk_iter.go:471-476)
+    st, kvs, _ = oracle.rowblk_decode_block(blk)
+    assert st == N.PBL_CORRUPT_FIRST_KEY and kvs == []
+    # RawIter sees the raw keys (rowblk_iter.go:1784-1794)
+    st, kvs, rs = oracle.rowblk_decode_block(blk, N.PBL_ROW_RAW_KEYS)
+    assert st == 0
+    assert [k for k, *_ in kvs] == [b"apple", b"apricot", b"banana"]
+    assert rs == [0]
+
+
+def test_oracle_with_prefix_block(golden):
+    blk = bytes.fromhex(golden["writer_with_prefix"]["block_hex"])
+    for flags in (0, N.PBL_ROW_VALUE_PREFIX):
+        st, kvs, rs = oracle.rowblk_decode_block(blk, flags)
+        assert st == 0
+        # kind DELETE (zero trailer): values come back verbatim, prefix byte included
+        assert [(k, t, v) for k, t, v, _f, _o in kvs] == [
+            (b"apple", 0, b"red"), (b"apricot", 0, b"\xfforange"), (b"banana", 0, b"\x00yellow"),
+            (b"cherry", 0, b"red"), (b"mango", 0, b"juicy")]
+        assert rs == [0x0, 0x2A, 0x80000056]
+        fl = [f for *_x, f, _o in kvs]
+        assert fl == [N.PBL_KV_RESTART, 0, N.PBL_KV_RESTART, 0, N.PBL_KV_RESTART | N.PBL_KV_RESTART_SAMEPFX]
+        assert [o for *_x, o in kvs] == [0, 19, 0x2A, 66, 0x56]
+
+
+def test_oracle_value_prefix_set_kind():
+    w = Writer(16)
+    w.add_with_optional_value_prefix(b"a", make_trailer(5, 1), False, b"inplace", 1, True, 0x00, False)
+    w.add_with_optional_value_prefix(b"b", make_trailer(4, 1), False, b"HANDLE", 1, True, 0x81, False)
+    w.add_with_optional_value_prefix(b"c", make_trailer(3, 1), False, b"BLOB", 1, True, 0x42, False)
+    w.add_with_optional_value_prefix(b"d", make_trailer(2, 0), True, b"del", 1, False, 0, False)
+    blk = w.finish()
+    st, kvs, _ = oracle.rowblk_decode_block(blk, N.PBL_ROW_VALUE_PREFIX)
+    assert st == 0
+    assert [(k, v, f & 0x3C) for k, _t, v, f, _o in kvs] == [
+        (b"a", b"inplace", 0), (b"b", b"\x81HANDLE", N.PBL_KV_VALBLK_HANDLE),
+        (b"c", b"\x42BLOB", N.PBL_KV_BLOB_HANDLE), (b"d", b"del", N.PBL_KV_OBSOLETE)]
+    assert kvs[3][1] == make_trailer(2, 0)  # obsolete bit cleared (TrailerObsoleteMask)
+    st, kvs, _ = oracle.rowblk_decode_block(blk, N.PBL_ROW_VALUE_PREFIX | N.PBL_ROW_NO_VALUER)
+    assert [v for _k, _t, v, _f, _o in kvs][:3] == [b"inplace", b"HANDLE", b"BLOB"]
+
+
+def _hamlet_batch(golden):
+    g = golden["h_no_compression"]
+    blob = np.fromfile(os.path.join(GOLDEN, "h_no_compression_blocks.bin"), np.uint8)
+    return blob, np.array(g["block_off"], np.uint64), np.array(g["block_len"], np.uint32)
+
+
+def test_oracle_hamlet_sst_against_h_txt(golden):
+    # sstable/testdata/h-no-compression-sst/000012.sst vs sstable/testdata/h.txt
+    blob, off, lens = _hamlet_batch(golden)
+    got = []
+    for o, ln in zip(off, lens):
+        st, kvs, rs = oracle.rowblk_decode_block(blob[int(o):int(o) + int(ln)].tobytes())
+        assert st == 0 and len(rs) >= 1
+        got += [(k.decode(), v.decode(), t) for k, t, v, _f, _o in kvs]
+    assert len(got) == 1710
+    assert [(k, v) for k, v, _t in got] == [tuple(x) for x in golden["hamlet_kvs"]]
+    assert all(t == make_trailer(0, 1) for *_x, t in got)
+
+
+def test_oracle_batch_layout_matches_block_decode(golden):
+    blob, off, lens = _hamlet_batch(golden)
+    r = oracle.rowblk_decode_batch(blob, off, lens)
+    assert r["n_kv"] == 1710 and r["status_mask"] == 1
+    for b in range(len(off)):
+        st, kvs, rs = oracle.rowblk_decode_block(blob[int(off[b]):int(off[b]) + int(lens[b])].tobytes())
+        kv0 = int(r["blk_kv_base"][b])
+        for j, (k, t, v, f, eo) in enumerate(kvs):
+            o = kv0 + b + j
+            kb, vb = int(r["blk_key_base"][b]), int(r["blk_val_base"][b])
+            assert r["key_bytes"][kb + r["key_off"][o]: kb + r["key_off"][o + 1]].tobytes() == k
+            assert r["val_bytes"][vb + r["val_off"][o]: vb + r["val_off"][o + 1]].tobytes() == v
+            assert int(r["trailer"][kv0 + j]) == t and int(r["entry_off"][kv0 + j]) == eo
+
+
+@pytest.mark.parametrize("ri", [1, 2, 3, 4])
+def test_rowblk_iter_datadriven_on_oracle(golden, ri):
+    # TestBlockIter2 (rowblk_iter_test.go:123-161) over sstable/rowblk/testdata/rowblk_iter
+    blk = None
+    for case in golden["rowblk_iter_datadriven"]:
+        cmd = case["cmd"].split()
+        if cmd[0] == "build":
+            w = Writer(ri)
+            for k, s in parse_ikeys(case["input"]):
+                w.add(k, make_trailer(s, 1), b"")
+            blk = w.finish()
+        elif cmd[0] == "iter":
+            gsn = 0
+            for a in cmd[1:]:
+                if a.startswith("globalSeqNum="):
+                    gsn = int(a.split("=")[1])
+            st, kvs, _ = oracle.rowblk_decode_block(blk)
+            assert st == 0
+            it = Iter([InternalKV(k, t, v, f) for k, t, v, f, _o in kvs], transforms=Transforms(gsn))
+            assert run_iter_cmds(it, case["input"]) == case["expected"], case
+
+
+def test_oracle_corruption_statuses():
+    w = Writer(16)
+    w.add(b"key00001", make_trailer(1, 1), b"v")
+    good = w.finish()
+    assert oracle.rowblk_decode_block(good)[0] == 0
+    assert oracle.rowblk_decode_block(b"\x00\x00\x00\x00")[0] == N.PBL_CORRUPT_NO_RESTARTS   # :249-251
+    assert oracle.rowblk_decode_block(b"\x01\x00")[0] == N.PBL_CORRUPT_BOUNDS
+    bad_first = b"\x01" + good[1:]
+    assert oracle.rowblk_decode_block(bad_first)[0] == N.PBL_CORRUPT_FIRST_KEY            # :429-434
+    w = Writer(16)
+    w.add_raw(b"short", b"")
+    assert oracle.rowblk_decode_block(w.finish())[0] == N.PBL_CORRUPT_FIRST_KEY             # :471-476
+    trunc = bytearray(good)
+    trunc[2] = 0x7F  # unshared length runs past the block
+    assert oracle.rowblk_decode_block(bytes(trunc))[0] == N.PBL_CORRUPT_BOUNDS
+    empty = Writer(16).finish()
+    assert oracle.rowblk_decode_block(empty) == (0, [], [0])
+
+
+def test_generator_blocks_decode_on_oracle():
+    buf, off, lens, n_kv = gen_row_blocks(7, 8, 32768, 16, 16, 100)
+    assert (lens <= 32768).all() and (lens > 32000).all()
+    r = oracle.rowblk_decode_batch(buf, off, lens)
+    assert r["n_kv"] == n_kv and r["status_mask"] == 1
+    # ~271 KVs / 17 restarts per 32 KiB block
+    per = np.diff(r["blk_kv_base"].astype(np.int64))
+    assert 250 <= per.min() and per.max() <= 290
+    assert (np.diff(r["blk_rst_base"].astype(np.int64)) >= 16).all()
