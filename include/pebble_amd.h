@@ -96,7 +96,7 @@ typedef struct pbl_totals {
   uint64_t key_bytes;   /* user-key bytes                                      */
   uint64_t val_bytes;   /* value bytes                                         */
   uint64_t n_restarts;  /* restart words (row format)                          */
-  uint32_t status_mask; /* OR of (1u << status) over blocks                    */
+  uint32_t status_mask; /* OR of (1u << status) over blocks with status != OK  */
   uint32_t n_bad_blocks;/* blocks whose status != PBL_OK                       */
   uint32_t n_slow_blocks;/* blocks decoded by the general (non-LDS) path      */
   uint32_t pad;

@@ -257,8 +257,10 @@ int orc_rowblk_decode_batch(const uint8_t* blocks, const uint64_t* off, const ui
       bo->blk_val_base[b] = vb;
       if (bo->blk_rst_base) bo->blk_rst_base[b] = rb;
     }
-    bo->status_mask |= 1u << st;
-    if (st != OK) bo->n_bad_blocks++;
+    if (st != OK) {
+      bo->status_mask |= 1u << st;
+      bo->n_bad_blocks++;
+    }
     kvb += o.n_kv;
     kb += o.key_bytes;
     vb += o.val_bytes;

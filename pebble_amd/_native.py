@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpebble_amd.so")
+# PBL_LIB selects the diagnostic (phase-stamp) build for scripts/phase_stamps.py
+LIB_PATH = os.environ.get("PBL_LIB") or os.path.join(_HERE, "libpebble_amd.so")
 
 # status codes (include/pebble_amd.h)
 PBL_OK = 0

@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libpebble_amd.so")
 SOURCES = ["rowblk_decode.hip", "colblk_decode.hip", "rowblk_writer.cpp"]
-HEADERS = ["common.hip.h", os.path.join("..", "..", "include", "pebble_amd.h")]
+HEADERS = ["common.hip.h", "rowblk_general.hip.h", os.path.join("..", "..", "include", "pebble_amd.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-pthread"]
 
@@ -28,16 +28,23 @@ def _stale() -> bool:
     return False
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+DIAG_OUT = os.path.join(HERE, "libpebble_amd_diag.so")
+
+
+def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str:
+    """Build libpebble_amd.so; `diag` builds the phase-stamp diagnostic variant
+    (libpebble_amd_diag.so, -DPBL_STAMPS) used only by scripts/phase_stamps.py."""
+    out = DIAG_OUT if diag else OUT
+    if not force and not diag and not _stale():
         return OUT
-    cmd = [HIPCC, *FLAGS, *[os.path.join(CSRC, s) for s in SOURCES], "-o", OUT + ".tmp"]
+    cmd = [HIPCC, *FLAGS, *(["-DPBL_STAMPS"] if diag else []), *[os.path.join(CSRC, s) for s in SOURCES],
+           "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, diag="--diag" in sys.argv))

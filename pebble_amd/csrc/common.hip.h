@@ -1,7 +1,6 @@
 // common.hip.h — shared device helpers for the gfx950 block decoders:
-// wave/block scans, LDS byte access, the decoupled look-back that places every
-// block's outputs in ONE pass (no separate size pass), and granule-aligned
-// byte-range stores.
+// wave/block scans and the decoupled look-back that places every block's
+// outputs in ONE pass (no separate size pass).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -13,6 +12,7 @@ namespace pbl {
 constexpr int kTPB = 256;   // threads per workgroup (4 waves); one workgroup per block
 constexpr int kWave = 64;
 constexpr int kNumComp = 4; // look-back components: n_kv, key bytes, value bytes, restarts
+constexpr int kLbWin = 4;   // look-back windows (of 64 predecessors) loaded per round trip
 
 // ---- workspace layout ------------------------------------------------------
 // [0,256): ticket counter (+ pad).  Then kNumComp arrays of n_blocks u64
@@ -26,6 +26,14 @@ constexpr uint64_t kValMask = (1ull << 62) - 1;
 
 __host__ __device__ inline uint64_t ws_bytes(uint32_t n_blocks) {
   return kWsHeader + uint64_t(kNumComp) * n_blocks * 8ull;
+}
+#ifdef PBL_STAMPS
+constexpr uint64_t kStampWords = 16;  // diagnostic build: per-block phase stamps
+#else
+constexpr uint64_t kStampWords = 0;
+#endif
+__host__ __device__ inline uint64_t ws_alloc_bytes(uint32_t n_blocks) {
+  return ws_bytes(n_blocks) + kStampWords * 8ull * n_blocks;
 }
 
 __device__ inline uint64_t ld_agent(const uint64_t* p) {
@@ -62,10 +70,9 @@ __device__ inline T wave_sum(T v) {
   return v;
 }
 
-// Block-wide exclusive scan of two u32 sequences held 2 items per thread.
-// `scratch` must hold 2*(kTPB/kWave) u32.  Returns the exclusive prefix of this
-// thread's first item; totals via *tot0/*tot1.  Caller must __syncthreads()
-// before reusing scratch.
+// Block-wide exclusive scan of two u32 sequences (one value each per thread).
+// `scratch` must hold 2*(kTPB/kWave) u32.  Caller must __syncthreads() before
+// reusing scratch.
 __device__ inline void block_excl_scan2(uint32_t a, uint32_t b, uint32_t* ea, uint32_t* eb,
                                         uint32_t* scratch, uint32_t* tot_a, uint32_t* tot_b) {
   uint32_t ia = wave_incl_scan(a), ib = wave_incl_scan(b);
@@ -88,48 +95,64 @@ __device__ inline void block_excl_scan2(uint32_t a, uint32_t b, uint32_t* ea, ui
 // Decoupled look-back (single-pass scan across blocks).  Executed by wave 0 of
 // the workgroup that owns virtual block `v` (tickets are handed out in launch
 // order, so every predecessor is already resident and publishes its aggregate
-// before it waits: no deadlock for any residency).  Returns exclusive prefixes.
+// before it waits: no deadlock for any residency).  All components are walked
+// back together, kLbWin windows of 64 predecessors per round trip.  Returns
+// exclusive prefixes.
 __device__ inline void lookback(uint64_t* st, uint32_t n_blocks, uint32_t v,
                                 const uint64_t agg[kNumComp], uint64_t excl[kNumComp],
                                 uint32_t* timeout_flag) {
   const int l = lane_id();
-  // publish aggregates (block 0 publishes its inclusive prefix directly)
   if (l < kNumComp) {
     uint64_t a = l == 0 ? agg[0] : l == 1 ? agg[1] : l == 2 ? agg[2] : agg[3];
     st_agent(st + uint64_t(l) * n_blocks + v, (v == 0 ? kStatePfx : kStateAgg) | (a & kValMask));
   }
+  uint64_t acc[kNumComp];
+  int64_t top[kNumComp];
+  bool done[kNumComp];
 #pragma unroll
-  for (int c = 0; c < kNumComp; c++) {
-    uint64_t acc = 0;
-    if (v > 0) {
-      int64_t top = int64_t(v) - 1;
-      uint32_t spins = 0;
-      const uint64_t* sc = st + uint64_t(c) * n_blocks;
-      for (;;) {
-        int64_t idx = top - l;
-        uint64_t g = idx >= 0 ? ld_agent(sc + idx) : kStatePfx;
-        uint64_t state = g >> 62;
+  for (int c = 0; c < kNumComp; c++) { acc[c] = 0; top[c] = int64_t(v) - 1; done[c] = v == 0; }
+  uint32_t spins = 0;
+  while (!(done[0] && done[1] && done[2] && done[3])) {
+    uint64_t g[kNumComp][kLbWin];
+#pragma unroll
+    for (int c = 0; c < kNumComp; c++)
+#pragma unroll
+      for (int k = 0; k < kLbWin; k++) {
+        int64_t idx = top[c] - kWave * k - l;
+        g[c][k] = (!done[c] && idx >= 0) ? ld_agent(st + uint64_t(c) * n_blocks + idx) : kStatePfx;
+      }
+    bool waited = false;
+#pragma unroll
+    for (int c = 0; c < kNumComp; c++) {
+      bool stop = done[c];
+#pragma unroll
+      for (int k = 0; k < kLbWin; k++) {
+        if (stop) continue;
+        uint64_t state = g[c][k] >> 62;
         uint64_t pfx = __ballot(state == 2);
         uint64_t notready = __ballot(state == 0);
         int first = pfx ? __builtin_ctzll(pfx) : 64;
         uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
-        if (notready & need) {
-          if (++spins > (1u << 24)) { if (l == 0) atomicOr(timeout_flag, 1u << PBL_TIMEOUT); break; }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        uint64_t val = (l <= first) ? (g & kValMask) : 0;
-        acc += wave_sum(val);
-        if (first < 64) break;
-        top -= kWave;
+        if (notready & need) { waited = true; stop = true; continue; }
+        acc[c] += wave_sum((l <= first) ? (g[c][k] & kValMask) : 0ull);
+        if (first < 64) { done[c] = true; stop = true; }
+        else top[c] -= kWave;
       }
     }
-    excl[c] = acc;
+    if (waited) {
+      if (++spins > (1u << 24)) {
+        if (l == 0) atomicOr(timeout_flag, 1u << PBL_TIMEOUT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
   }
-  if (l < kNumComp) {
+#pragma unroll
+  for (int c = 0; c < kNumComp; c++) excl[c] = acc[c];
+  if (l < kNumComp && v > 0) {
     uint64_t e = l == 0 ? excl[0] : l == 1 ? excl[1] : l == 2 ? excl[2] : excl[3];
     uint64_t a = l == 0 ? agg[0] : l == 1 ? agg[1] : l == 2 ? agg[2] : agg[3];
-    if (v > 0) st_agent(st + uint64_t(l) * n_blocks + v, kStatePfx | ((e + a) & kValMask));
+    st_agent(st + uint64_t(l) * n_blocks + v, kStatePfx | ((e + a) & kValMask));
   }
 }
 

@@ -1,69 +1,129 @@
 // rowblk_decode.hip — gfx950 decoder for Pebble row-oriented data blocks.
 //
 // One 256-thread workgroup per block (block id = an atomic ticket, so the
-// decoupled look-back always waits on resident predecessors).  The block is
-// staged HBM -> LDS once with 16-byte coalesced loads; the varint headers are
-// parsed out of LDS one lane per restart run (restart points cut the prefix
-// chain, rowblk_writer.go:147-155); per-KV sizes are block-scanned; a
-// decoupled look-back over the batch turns the per-block totals into output
-// bases (single pass, no size pass); then every thread writes 16-byte granules
-// of the key and value regions, gathering bytes out of LDS.
+// decoupled look-back always waits on resident predecessors).
+//
+//   stage   the block HBM -> LDS once, 16-byte coalesced loads
+//   P1      one lane per restart run walks its entries (restart points cut the
+//           prefix chain, rowblk_writer.go:147-155), parking each entry offset
+//           and its in-run key/value output prefix in a slot; a block scan of
+//           the per-run sums gives the block's totals
+//   look-back  wave 0 publishes the totals and resolves the batch-wide output
+//           bases (decoupled look-back: single pass, no size pass) WHILE waves
+//           1-3 expand the slots into per-KV arrays (P2)
+//   write   per-KV arrays; key and value bytes as 16-byte granules, each the
+//           merge of a few LDS segment gathers (a key's bytes are the segments
+//           of its prefix chain), one dwordx4 store per full granule
 //
 // Semantics follow cockroachdb/pebble sstable/rowblk/rowblk_iter.go:
 //   Init :241-276 (numRestarts, restarts offset), readFirstKey :418-485,
 //   readEntry :333-416 (3 uint32 varints, fullKey = fullKey[:shared]+unshared),
 //   decodeInternalKey :487-504 (LE64 trailer & TrailerObsoleteMask, <8 B =>
 //   InternalKeyKindInvalid), value prefix :1192-1199 (block/kv.go:14-41),
-//   decodeRestart :1092-1096.
+//   decodeRestart :1092-1096, RawIter.readEntry :1784-1794 (PBL_ROW_RAW_KEYS).
 // Blocks whose restart table is inconsistent with a per-run walk, or that do
-// not fit the LDS limits, take the general path: a wave-serial restatement of
-// Iter.First/Next (bit-identical by construction, slower).
+// not fit the LDS limits, take the general path (rowblk_general.hip.h): a
+// wave-serial restatement of Iter.First/Next, bit-identical by construction.
 #include "common.hip.h"
 
 namespace pbl {
 namespace row {
 
-constexpr int kLdsBlkBytes = 32768 + 32;  // block staging (any 16-B phase of a <=32 KiB block)
+constexpr int kPad = 16;                  // LDS front pad: segment gathers may start up to 15 B early
+constexpr int kLdsBlkBytes = kPad + 32768 + 32;  // block staging (any 16-B phase of a <=32 KiB block)
+constexpr uint32_t kMaxFastLen = 32768;   // blocks up to this length take the LDS path
 constexpr int kKvCap = 512;               // KVs per block on the LDS path
 constexpr int kRunCap = kKvCap;           // restart runs per block on the LDS path
+constexpr uint32_t kMaxFastKeyBytes = 65535;  // user-key bytes per block on the LDS path (u16 offsets)
+constexpr int kBkt = 256;                 // bytes per output bucket of the granule -> KV index
 constexpr uint32_t kRestartMask = 0x7fffffffu;
 constexpr uint64_t kTrailerObsoleteMask = ((((uint64_t)1 << 56) - 1) << 8) | 191u;
 constexpr uint64_t kKindInvalid = 191u;
-constexpr uint16_t kRunStart = 0x8000u;   // top bit of sh[] marks the first entry of a run
+
+// aux (u16) area: run-walk slots, per-run prefixes, output buckets
+constexpr int kSlotPos = 0;                          // [kKvCap] entry offset of slot q
+constexpr int kSlotCk = kSlotPos + kKvCap;           // [kKvCap] in-run user-key prefix of slot q
+constexpr int kSlotCv = kSlotCk + kKvCap;            // [kKvCap] in-run value prefix of slot q
+constexpr int kRunKv0 = kSlotCv + kKvCap;            // [kRunCap+1] first KV of run r
+constexpr int kRunKb0 = kRunKv0 + kRunCap + 1;       // [kRunCap+1] key-byte offset of run r
+constexpr int kRunVb0 = kRunKb0 + kRunCap + 1;       // [kRunCap+1] value-byte offset of run r
+constexpr int kKBkt = kRunVb0 + kRunCap + 1;         // [65536/kBkt+1] KV holding key byte b*kBkt
+constexpr int kVBkt = kKBkt + 65536 / kBkt + 1;      // [32768/kBkt+1] KV holding value byte b*kBkt
+constexpr int kAuxWords = (kVBkt + 32768 / kBkt + 1 + 7) & ~7;
 
 struct Lds {
-  uint4 blk4[kLdsBlkBytes / 16];          // block bytes, block byte i at blk[shift+i]
-  uint16_t eoff[kKvCap];                  // entry offset
-  uint16_t ksrc[kKvCap];                  // offset of the unshared key bytes
-  uint16_t sh[kKvCap];                    // shared length (| kRunStart)
-  uint16_t klen[kKvCap];                  // internal key length
-  uint16_t vsrc[kKvCap];                  // value offset (after prefix stripping)
-  uint16_t vlen[kKvCap];                  // value length (after prefix stripping)
-  uint32_t kout[kKvCap + 1];              // user-key output offsets (block relative)
-  uint32_t vout[kKvCap + 1];              // value output offsets; first reused as run kv0
-  uint8_t kvf[kKvCap];                    // PBL_KV_* flags
+  uint4 blk4[kLdsBlkBytes / 16];  // block byte i at byte kPad+shift+i
+  uint16_t eoff[kKvCap];          // entry offset
+  uint16_t ksrc[kKvCap];          // offset of the unshared key bytes
+  uint16_t sh[kKvCap];            // shared length
+  uint16_t klen[kKvCap];          // internal key length
+  uint16_t vsrc[kKvCap];          // value offset (after prefix stripping)
+  uint16_t vlen[kKvCap];          // value length (after prefix stripping)
+  uint32_t kout[kKvCap + 1];      // user-key output offsets (block relative)
+  uint32_t vout[kKvCap + 1];      // value output offsets (block relative)
+  uint8_t kvf[kKvCap];            // PBL_KV_* flags
+  uint16_t par[kKvCap];           // prefix parent: max{i < j in run : shared_i < shared_j}
+  uint16_t aux[kAuxWords];
   uint32_t scratch[16];
   uint64_t bases[kNumComp];
-  uint32_t ticket, status, slow, nkv, nrun, nres, shift;
-  int32_t restarts_off;
-  uint32_t tot_kb, tot_vb;
+  uint32_t ticket, status, slow, nkv, nres, S, shift, tot_kb, tot_vb;
+  int32_t roff;
 };
 
-__device__ inline uint8_t lb(const Lds& s, uint32_t i) {
-  return reinterpret_cast<const uint8_t*>(s.blk4)[s.shift + i];
+// 16 bytes at LDS byte address a (any alignment): five dword reads + alignbyte
+__device__ inline uint4 lds_gather16(const uint32_t* W, uint32_t a) {
+  uint32_t q = a >> 2, r = a & 3;
+  uint32_t x0 = W[q], x1 = W[q + 1], x2 = W[q + 2], x3 = W[q + 3], x4 = W[q + 4];
+  return make_uint4(__builtin_amdgcn_alignbyte(x1, x0, r), __builtin_amdgcn_alignbyte(x2, x1, r),
+                    __builtin_amdgcn_alignbyte(x3, x2, r), __builtin_amdgcn_alignbyte(x4, x3, r));
 }
-__device__ inline uint32_t lds_le32(const Lds& s, uint32_t i) {
-  return uint32_t(lb(s, i)) | uint32_t(lb(s, i + 1)) << 8 | uint32_t(lb(s, i + 2)) << 16 |
-         uint32_t(lb(s, i + 3)) << 24;
+
+// Read-only view of the staged block: its base offset lives in a register.
+struct View {
+  const uint8_t* B;   // LDS bytes (array start)
+  const uint32_t* W;  // LDS words (array start)
+  uint32_t base;      // byte index of block byte 0 (kPad + shift)
+  __device__ inline uint32_t byte(uint32_t i) const { return B[base + i]; }
+  // 8 block bytes [i, i+8) as a little-endian u64 (three aligned LDS dword reads)
+  __device__ inline uint64_t ld8(uint32_t i) const {
+    uint32_t a = base + i, q = a >> 2, r = a & 3;
+    uint32_t x0 = W[q], x1 = W[q + 1], x2 = W[q + 2];
+    uint32_t lo = __builtin_amdgcn_alignbyte(x1, x0, r);
+    uint32_t hi = __builtin_amdgcn_alignbyte(x2, x1, r);
+    return uint64_t(hi) << 32 | lo;
+  }
+  __device__ inline uint32_t le32(uint32_t i) const {
+    uint32_t a = base + i, q = a >> 2, r = a & 3;
+    return __builtin_amdgcn_alignbyte(W[q + 1], W[q], r);
+  }
+  // 16 block bytes starting at block offset i (i may be up to 15 below 0)
+  __device__ inline uint4 ld16(int32_t i) const { return lds_gather16(W, uint32_t(int32_t(base) + i)); }
+};
+
+// mask of the low n bytes of a word, n clamped to [0, 4]
+__device__ inline uint32_t low_bytes(int n) {
+  n = n < 0 ? 0 : n;
+  return n >= 4 ? 0xffffffffu : (1u << (8 * n)) - 1u;
+}
+// byte mask of bytes [a, b) within the 4-byte word k of a 16-byte granule
+__device__ inline uint32_t word_mask(int k, uint32_t a, uint32_t b) {
+  return low_bytes(int(b) - 4 * k) & ~low_bytes(int(a) - 4 * k);
+}
+__device__ inline void merge16(uint4& w, const uint4& v, uint32_t a, uint32_t b) {
+  uint32_t m;
+  m = word_mask(0, a, b); w.x = (w.x & ~m) | (v.x & m);
+  m = word_mask(1, a, b); w.y = (w.y & ~m) | (v.y & m);
+  m = word_mask(2, a, b); w.z = (w.z & ~m) | (v.z & m);
+  m = word_mask(3, a, b); w.w = (w.w & ~m) | (v.w & m);
 }
 
 // varint from LDS (rowblk_iter.go:2020-2038); returns bytes used, 0 if it runs past `end`
-__device__ inline int lds_varint(const Lds& s, uint32_t p, uint32_t end, uint32_t* v) {
+__device__ inline uint32_t lds_varint(const View& V, uint32_t p, uint32_t end, uint32_t* v) {
   uint32_t r = 0;
 #pragma unroll
   for (int i = 0; i < 5; i++) {
     if (p + i >= end) return 0;
-    uint32_t b = lb(s, p + i);
+    uint32_t b = V.byte(p + i);
     if (i == 4) { *v = r | (b << 28); return 5; }
     if (b < 128) { *v = r | (b << (7 * i)); return i + 1; }
     r |= (b & 0x7f) << (7 * i);
@@ -71,66 +131,84 @@ __device__ inline int lds_varint(const Lds& s, uint32_t p, uint32_t end, uint32_
   return 0;
 }
 
-// byte p of the internal key of entry j (resolve the prefix chain backwards;
-// a run's first entry has shared == 0 so the walk stays inside the run)
-__device__ inline uint8_t key_byte(const Lds& s, int j, uint32_t p) {
-  while (p < uint32_t(s.sh[j] & 0x7fff)) j--;
-  return lb(s, s.ksrc[j] + p - (s.sh[j] & 0x7fff));
-}
-
-// 16-byte gather of block bytes [src, src+16) out of LDS (any alignment)
-__device__ inline uint4 lds_gather16(const Lds& s, uint32_t src) {
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(s.blk4);
-  uint32_t a = s.shift + src, q = a >> 2, sh = (a & 3) * 8;
-  uint32_t x0 = w[q], x1 = w[q + 1], x2 = w[q + 2], x3 = w[q + 3], x4 = w[q + 4];
-  uint4 r;
-  if (sh == 0) { r.x = x0; r.y = x1; r.z = x2; r.w = x3; return r; }
-  r.x = (x0 >> sh) | (x1 << (32 - sh));
-  r.y = (x1 >> sh) | (x2 << (32 - sh));
-  r.z = (x2 >> sh) | (x3 << (32 - sh));
-  r.w = (x3 >> sh) | (x4 << (32 - sh));
-  return r;
-}
-
-__device__ inline void put_byte(uint4& g, int i, uint32_t b) {
-  uint32_t* w = reinterpret_cast<uint32_t*>(&g);
-  // i is small and the loop is unrolled by callers
-  w[i >> 2] |= b << ((i & 3) * 8);
-}
-
-// Store granule g covering global bytes [gaddr, gaddr+16) of which only
-// [lo, hi) (absolute byte addresses) belong to this block.
-__device__ inline void store_granule(uint8_t* base, uint64_t gaddr, uint64_t lo, uint64_t hi,
-                                     const uint4& g) {
-  if (gaddr >= lo && gaddr + 16 <= hi) {
-    *reinterpret_cast<uint4*>(base + gaddr) = g;
-  } else {
-    const uint8_t* gb = reinterpret_cast<const uint8_t*>(&g);
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      uint64_t a = gaddr + i;
-      if (a >= lo && a < hi) base[a] = gb[i];
-    }
+// Decode the 3 varints of the entry at `pos` (fast path: all three 1 byte).
+__device__ inline uint32_t entry_header(const View& V, uint32_t pos, uint32_t end, uint32_t* sh,
+                                        uint32_t* un, uint32_t* vl) {
+  uint64_t w = V.ld8(pos);
+  if (pos + 3 <= end && (w & 0x808080ull) == 0) {
+    *sh = uint32_t(w) & 0xff;
+    *un = uint32_t(w >> 8) & 0xff;
+    *vl = uint32_t(w >> 16) & 0xff;
+    return 3;
   }
+  uint32_t x = lds_varint(V, pos, end, sh);
+  uint32_t y = x ? lds_varint(V, pos + x, end, un) : 0;
+  uint32_t z = y ? lds_varint(V, pos + x + y, end, vl) : 0;
+  return z ? x + y + z : 0;
+}
+
+// byte p of the internal key of entry j: source entry = max{i <= j : shared_i <= p}
+// (a run's first entry has shared == 0 so the walk stays inside the run)
+__device__ inline uint32_t key_byte(const Lds& s, const View& V, int j, uint32_t p) {
+  while (p < uint32_t(s.sh[j])) j--;
+  return V.byte(s.ksrc[j] + p - s.sh[j]);
 }
 
 // trailer + flags of entry j (LDS path)
-__device__ inline uint64_t entry_trailer(const Lds& s, int j, uint8_t* fl, uint32_t flags) {
-  uint32_t kl = s.klen[j];
+__device__ inline uint64_t entry_trailer(const Lds& s, const View& V, int j, uint8_t* fl, uint32_t flags) {
   if (flags & PBL_ROW_RAW_KEYS) return 0;
+  uint32_t kl = s.klen[j];
   if (kl < 8) { *fl |= PBL_KV_INVALID_KEY; return kKindInvalid; }
-  uint64_t raw = 0;
-  uint32_t sh = s.sh[j] & 0x7fff;
+  uint32_t sh = s.sh[j];
+  uint64_t raw;
   if (kl - 8 >= sh) {  // all 8 trailer bytes are in this entry's unshared part
-    uint32_t src = s.ksrc[j] + (kl - 8 - sh);
-#pragma unroll
-    for (int i = 0; i < 8; i++) raw |= uint64_t(lb(s, src + i)) << (8 * i);
+    raw = V.ld8(s.ksrc[j] + (kl - 8 - sh));
   } else {
+    raw = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) raw |= uint64_t(key_byte(s, j, kl - 8 + i)) << (8 * i);
+    for (int i = 0; i < 8; i++) raw |= uint64_t(key_byte(s, V, j, kl - 8 + i)) << (8 * i);
   }
   if (raw & 64u) *fl |= PBL_KV_OBSOLETE;
   return raw & kTrailerObsoleteMask;
+}
+
+// Store 16 bytes (w) covering global bytes [ga, ga+16) of which only [lo, hi)
+// belong to this block: one dwordx4 store when whole, byte stores at the edges.
+__device__ inline void store16(uint8_t* base, uint64_t ga, uint64_t lo, uint64_t hi, uint4 w) {
+  if (ga >= lo && ga + 16 <= hi) {
+    *reinterpret_cast<uint4*>(base + ga) = w;
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    uint32_t word = i < 4 ? w.x : i < 8 ? w.y : i < 12 ? w.z : w.w;
+    if (ga + i >= lo && ga + i < hi) base[ga + i] = uint8_t(word >> (8 * (i & 3)));
+  }
+}
+
+// Block-wide exclusive scan of three u32 sequences (one value each per thread).
+__device__ inline void block_excl_scan3(uint32_t a, uint32_t b, uint32_t c, uint32_t* e, uint32_t* tot,
+                                        uint32_t* scratch) {
+  uint32_t ia = wave_incl_scan(a), ib = wave_incl_scan(b), ic = wave_incl_scan(c);
+  const int w = wave_id(), l = lane_id();
+  if (l == kWave - 1) { scratch[w] = ia; scratch[4 + w] = ib; scratch[8 + w] = ic; }
+  __syncthreads();
+  uint32_t p[3] = {0, 0, 0}, tt[3] = {0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < kTPB / kWave; i++) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      uint32_t v = scratch[4 * k + i];
+      if (i < w) p[k] += v;
+      tt[k] += v;
+    }
+  }
+  e[0] = p[0] + ia - a;
+  e[1] = p[1] + ib - b;
+  e[2] = p[2] + ic - c;
+  tot[0] = tt[0];
+  tot[1] = tt[1];
+  tot[2] = tt[2];
 }
 
 struct Args {
@@ -138,124 +216,158 @@ struct Args {
   pbl_decode_out out;
 };
 
-// ---------------------------------------------------------------------------
-// General path: a wave-serial restatement of Iter.First/Next, block bytes read
-// from global memory, current key in LDS.  Executed by wave 0 only.
-// ---------------------------------------------------------------------------
-struct SlowState {
-  uint64_t nkv, kb, vb, nr;
-  uint32_t status;
-};
+#ifdef PBL_STAMPS
+// diagnostic build only: per-block phase timestamps (s_memtime) written past
+// the look-back state in the workspace; never part of an output
+#define STAMPT(i, tid)                                                                    \
+  do {                                                                                    \
+    if (threadIdx.x == (tid))                                                             \
+      reinterpret_cast<uint64_t*>(ws + ws_bytes(nb))[uint64_t(b) * 16 + (i)] =           \
+          __builtin_amdgcn_s_memtime();                                                   \
+  } while (0)
+#define STAMP(i) STAMPT(i, 0)
+#else
+#define STAMPT(i, tid) do {} while (0)
+#define STAMP(i) do {} while (0)
+#endif
 
-__device__ inline uint32_t g_varint(const uint8_t* p, const uint8_t* end, uint32_t* v) {
-  uint32_t r = 0;
-  for (int i = 0; i < 5; i++) {
-    if (p + i >= end) return 0;
-    uint32_t b = p[i];
-    if (i == 4) { *v = r | (b << 28); return 5; }
-    if (b < 128) { *v = r | (b << (7 * i)); return i + 1; }
-    r |= (b & 0x7f) << (7 * i);
-  }
-  return 0;
-}
+#include "rowblk_general.hip.h"
 
-__device__ inline uint32_t g_le32(const uint8_t* p) {
-  return uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 | uint32_t(p[3]) << 24;
-}
-
-// pass 0 counts; pass 1 writes outputs at the given bases.
-__device__ void slow_walk(const uint8_t* blk, uint64_t len, uint32_t flags, uint8_t* keybuf,
-                          uint32_t keycap, int pass, const Args& A, uint32_t b,
-                          const uint64_t* bases, SlowState* st) {
-  const int l = lane_id();
-  const uint8_t* end = blk + len;
-  int32_t nr = int32_t(g_le32(blk + len - 4));
-  int64_t restarts = int64_t(len) - 4 * (1 + int64_t(nr));
-  const uint8_t* rtab = blk + restarts;
-  uint64_t nkv = 0, kb = 0, vb = 0, full_len = 0;
-  int64_t offset = 0;
-  uint32_t ri = 0;
-  uint32_t status = PBL_OK;
-  const pbl_decode_out& O = A.out;
-  while (offset >= 0 && offset < restarts) {
-    const uint8_t* p = blk + offset;
-    uint32_t shared, unshared, vlen;
-    uint32_t a = g_varint(p, end, &shared);
-    uint32_t bb = a ? g_varint(p + a, end, &unshared) : 0;
-    uint32_t c = bb ? g_varint(p + a + bb, end, &vlen) : 0;
-    if (!c) { status = PBL_CORRUPT_BOUNDS; break; }
-    const uint8_t* kp = p + a + bb + c;
-    if (uint64_t(end - kp) < unshared) { status = PBL_CORRUPT_BOUNDS; break; }
-    const uint8_t* vp = kp + unshared;
-    if (uint64_t(end - vp) < vlen) { status = PBL_CORRUPT_BOUNDS; break; }
-    if (shared > full_len) { status = PBL_CORRUPT_BOUNDS; break; }
-    uint64_t klen = uint64_t(shared) + unshared;
-    if (klen > keycap) { status = PBL_UNSUPPORTED; break; }
-    wave_sync();
-    for (uint32_t i = l; i < unshared; i += kWave) keybuf[shared + i] = kp[i];
-    wave_sync();
-    full_len = klen;
-    uint64_t trailer, ukl;
-    uint8_t fl = 0;
-    if (flags & PBL_ROW_RAW_KEYS) {
-      trailer = 0;
-      ukl = klen;
-    } else if (klen >= 8) {
-      uint64_t raw = 0;
-      for (int i = 0; i < 8; i++) raw |= uint64_t(keybuf[klen - 8 + i]) << (8 * i);
-      if (raw & 64u) fl |= PBL_KV_OBSOLETE;
-      trailer = raw & kTrailerObsoleteMask;
-      ukl = klen - 8;
-    } else {
-      trailer = kKindInvalid;
-      ukl = 0;
-      fl |= PBL_KV_INVALID_KEY;
-    }
-    const uint8_t* v = vp;
-    uint64_t vl = vlen;
-    if ((flags & PBL_ROW_VALUE_PREFIX) && !(flags & PBL_ROW_RAW_KEYS) && (trailer & 0xff) == 1) {
-      if (vl == 0) { status = PBL_CORRUPT_BOUNDS; break; }
-      uint8_t pre = v[0];
-      if ((pre & 0xC0) == 0 || (flags & PBL_ROW_NO_VALUER)) { v++; vl--; }
-      else if ((pre & 0xC0) == 0x80) fl |= PBL_KV_VALBLK_HANDLE;
-      else fl |= PBL_KV_BLOB_HANDLE;
-    }
-    while (ri < uint32_t(nr) && int64_t(g_le32(rtab + 4 * ri) & kRestartMask) < offset) ri++;
-    if (ri < uint32_t(nr) && int64_t(g_le32(rtab + 4 * ri) & kRestartMask) == offset) {
-      fl |= PBL_KV_RESTART;
-      if (g_le32(rtab + 4 * ri) & 0x80000000u) fl |= PBL_KV_RESTART_SAMEPFX;
-    }
-    if (pass == 1) {
-      uint64_t kv = bases[0] + nkv, o = bases[0] + b + nkv;
-      if (l == 0) {
-        O.trailer[kv] = trailer;
-        if (O.kv_flags) O.kv_flags[kv] = fl;
-        if (O.entry_off) O.entry_off[kv] = uint32_t(offset);
-        O.key_off[o] = uint32_t(kb);
-        O.val_off[o] = uint32_t(vb);
-      }
-      uint8_t* kd = O.key_bytes + bases[1] + kb;
-      for (uint64_t i = l; i < ukl; i += kWave) kd[i] = keybuf[i];
-      uint8_t* vd = O.val_bytes + bases[2] + vb;
-      for (uint64_t i = l; i < vl; i += kWave) vd[i] = v[i];
-    }
-    nkv++;
-    kb += ukl;
+// P1 for run r: walk entries, park offsets and in-run output prefixes in the
+// slots of run r, return (count, user-key bytes, value bytes).  `ok` clears when
+// the run does not end exactly at the next restart (general path).
+__device__ inline void walk_run(Lds& s, const View& V, uint32_t r, uint32_t nres, uint32_t roff, uint32_t S,
+                                uint32_t flags, uint32_t* cnt_o, uint32_t* kb_o, uint32_t* vb_o) {
+  uint32_t st = roff + 4 * r;
+  uint32_t s0 = V.le32(st) & kRestartMask;
+  uint32_t e0 = (r + 1 < nres) ? (V.le32(st + 4) & kRestartMask) : roff;
+  uint32_t cnt = 0, kb = 0, vb = 0, prev_kl = 0;
+  bool ok = (r != 0 || s0 == 0) && s0 < e0 && e0 <= roff;
+  uint32_t pos = s0;
+  while (ok && pos < e0) {
+    uint32_t sh, un, vl;
+    uint32_t h = entry_header(V, pos, e0, &sh, &un, &vl);
+    if (!h || (cnt == 0 && sh != 0) || cnt >= S) { ok = false; break; }
+    uint64_t np = uint64_t(pos) + h + un + vl;
+    if (np > e0) { ok = false; break; }
+    // fullKey[:shared] needs shared <= len(previous key) (rowblk_iter.go:403)
+    if (sh > prev_kl && cnt > 0) atomicMax(&s.status, uint32_t(PBL_CORRUPT_BOUNDS));
+    uint32_t q = r * S + cnt;
+    s.aux[kSlotPos + q] = uint16_t(pos);
+    s.aux[kSlotCk + q] = uint16_t(kb);
+    s.aux[kSlotCv + q] = uint16_t(vb);
+    uint32_t kl = sh + un;
+    kb += (flags & PBL_ROW_RAW_KEYS) ? kl : (kl >= 8 ? kl - 8 : 0);
     vb += vl;
-    offset = int64_t(vp - blk) + vlen;
+    prev_kl = kl;
+    pos = uint32_t(np);
+    cnt++;
   }
-  if (status == PBL_OK && (kb >> 32 || vb >> 32)) status = PBL_UNSUPPORTED;
-  if (pass == 1 && status == PBL_OK) {
-    uint64_t o = bases[0] + b + nkv;
-    if (l == 0) { O.key_off[o] = uint32_t(kb); O.val_off[o] = uint32_t(vb); }
-    if (O.restarts)
-      for (int32_t r = l; r < nr; r += kWave) O.restarts[bases[3] + r] = g_le32(rtab + 4 * r);
+  if (!ok) atomicOr(&s.slow, 1u);
+  *cnt_o = cnt;
+  *kb_o = kb;
+  *vb_o = vb;
+}
+
+// P2 for slot q: expand into KV arrays at its final index; mark output buckets.
+__device__ inline void expand_slot(Lds& s, const View& V, uint32_t q, uint32_t S, uint32_t roff,
+                                   uint32_t flags) {
+  uint32_t r = q / S, k = q - r * S;
+  uint32_t kv0 = s.aux[kRunKv0 + r], kv1 = s.aux[kRunKv0 + r + 1];
+  if (kv0 + k >= kv1) return;
+  uint32_t j = kv0 + k;
+  uint32_t pos = s.aux[kSlotPos + q], sh, un, vl;
+  uint32_t h = entry_header(V, pos, roff, &sh, &un, &vl);
+  uint32_t kl = sh + un;
+  uint32_t ukl = (flags & PBL_ROW_RAW_KEYS) ? kl : (kl >= 8 ? kl - 8 : 0);
+  uint32_t ko = uint32_t(s.aux[kRunKb0 + r]) + s.aux[kSlotCk + q];
+  uint32_t vo = uint32_t(s.aux[kRunVb0 + r]) + s.aux[kSlotCv + q];
+  s.eoff[j] = uint16_t(pos);
+  s.ksrc[j] = uint16_t(pos + h);
+  s.sh[j] = uint16_t(sh);
+  s.klen[j] = uint16_t(kl);
+  s.vsrc[j] = uint16_t(pos + h + un);
+  s.vlen[j] = uint16_t(vl);
+  s.kout[j] = ko;
+  s.vout[j] = vo;
+  uint8_t fl = (!(flags & PBL_ROW_RAW_KEYS) && kl < 8) ? uint8_t(PBL_KV_INVALID_KEY) : uint8_t(0);
+  if (k == 0) fl |= uint8_t(PBL_KV_RESTART | ((V.le32(roff + 4 * r) >> 31) ? PBL_KV_RESTART_SAMEPFX : 0));
+  s.kvf[j] = fl;
+  // prefix parent: the nearest earlier entry of the run whose own bytes start
+  // below shared_j (entries in between contribute nothing to key j's prefix).
+  // Scanned through the run's parked slots, so no other thread's output is read.
+  {
+    uint32_t pj = j;
+    if (sh != 0) {
+      for (int kk = int(k) - 1; kk >= 0; kk--) {
+        uint32_t pq = r * S + uint32_t(kk);
+        uint32_t ppos = s.aux[kSlotPos + pq], psh;
+        // shared length of the parked entry: its first varint
+        uint32_t b0 = V.byte(ppos);
+        if (b0 < 128) psh = b0;
+        else { uint32_t un2, vl2; entry_header(V, ppos, roff, &psh, &un2, &vl2); }
+        if (psh < sh) { pj = kv0 + uint32_t(kk); break; }
+      }
+    }
+    s.par[j] = uint16_t(pj);
   }
-  st->status = status;
-  st->nkv = nkv;
-  st->kb = kb;
-  st->vb = vb;
-  st->nr = uint64_t(nr);
+  // bucket b (bytes [b*kBkt, ...)) belongs to the KV that holds its first byte
+  for (uint32_t bk = (ko + kBkt - 1) / kBkt; bk * kBkt < ko + ukl; bk++) s.aux[kKBkt + bk] = uint16_t(j);
+  for (uint32_t bk = (vo + kBkt - 1) / kBkt; bk * kBkt < vo + vl; bk++) s.aux[kVBkt + bk] = uint16_t(j);
+}
+
+// One 16-byte key granule: user-key bytes [o, o1) (block relative) land at
+// granule bytes [q, ...).  Each key is the concatenation of its prefix-chain
+// segments: [shared_i, cur) of entry i, walking i = j, j-1, ... (rowblk_iter.go:403
+// unrolled backwards); every segment is one LDS gather merged under a mask.
+__device__ inline uint4 key_granule(const Lds& s, const View& V, uint32_t o, uint32_t o1, uint32_t q,
+                                    uint32_t nkv) {
+  int j = s.aux[kKBkt + o / kBkt];
+  uint4 w = make_uint4(0, 0, 0, 0);
+  while (o < o1) {
+    while (s.kout[j + 1] <= o) j++;
+    uint32_t k0 = s.kout[j], k1 = s.kout[j + 1];
+    uint32_t p_lo = o - k0, p_hi = (o1 < k1 ? o1 : k1) - k0;
+    uint32_t cur = k1 - k0;  // user-key length
+    int i = j;
+    // contributing entries only: j, then prefix parents (par[] skips entries
+    // whose own bytes start at or above the current prefix length)
+    while (cur > p_lo) {
+      uint32_t shi = s.sh[i];
+      uint32_t lo_i = shi < cur ? shi : cur;
+      uint32_t a = lo_i > p_lo ? lo_i : p_lo, z = cur < p_hi ? cur : p_hi;
+      if (a < z) {
+        uint32_t gq = q + (a - p_lo);
+        int32_t src = int32_t(s.ksrc[i]) - int32_t(shi) + int32_t(a);  // block offset of key byte a
+        uint4 v = V.ld16(src - int32_t(gq));
+        if (gq == 0 && z - a == 16) w = v;
+        else merge16(w, v, gq, gq + (z - a));
+      }
+      cur = lo_i;
+      i = s.par[i];
+    }
+    q += p_hi - p_lo;
+    o += p_hi - p_lo;
+  }
+  (void)nkv;
+  return w;
+}
+
+// One 16-byte value granule: value bytes [o, o1) land at granule bytes [q, ...).
+__device__ inline uint4 val_granule(const Lds& s, const View& V, uint32_t o, uint32_t o1, uint32_t q) {
+  int j = s.aux[kVBkt + o / kBkt];
+  uint4 w = make_uint4(0, 0, 0, 0);
+  while (o < o1) {
+    while (s.vout[j + 1] <= o) j++;
+    uint32_t e = o1 < s.vout[j + 1] ? o1 : s.vout[j + 1];
+    int32_t src = int32_t(s.vsrc[j] + (o - s.vout[j]));
+    uint4 v = V.ld16(src - int32_t(q));
+    if (q == 0 && e - o == 16) w = v;
+    else merge16(w, v, q, q + (e - o));
+    q += e - o;
+    o = e;
+  }
+  return w;
 }
 
 // ---------------------------------------------------------------------------
@@ -267,6 +379,7 @@ __global__ void __launch_bounds__(kTPB) rowblk_decode_kernel(Args A) {
   const pbl_decode_out& O = A.out;
   const uint32_t nb = A.in.n_blocks;
   const uint32_t flags = A.in.flags;
+  const bool vprefix = (flags & PBL_ROW_VALUE_PREFIX) && !(flags & PBL_ROW_RAW_KEYS);
   uint8_t* ws = reinterpret_cast<uint8_t*>(O.workspace);
   uint32_t* ticket_ctr = reinterpret_cast<uint32_t*>(ws);
   uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
@@ -281,16 +394,19 @@ __global__ void __launch_bounds__(kTPB) rowblk_decode_kernel(Args A) {
   const uint64_t boff = A.in.block_off[b];
   const uint32_t blen = A.in.block_len[b];
   const uint8_t* gblk = A.in.blocks + boff;
+  STAMP(0);
 
   // ---- stage the block into LDS (16-byte coalesced loads) --------------------
   const uint64_t a0 = boff & ~uint64_t(15);
   const uint64_t a1 = (boff + blen + 15) & ~uint64_t(15);
-  const bool fits = (a1 - a0) <= uint64_t(kLdsBlkBytes);
+  const bool fits = blen <= kMaxFastLen;
   if (fits) {
     const uint4* src = reinterpret_cast<const uint4*>(A.in.blocks + a0);
     const uint32_t n16 = uint32_t((a1 - a0) >> 4);
-    for (uint32_t g = t; g < n16; g += kTPB) s.blk4[g] = src[g];
+    for (uint32_t g = t; g < n16; g += kTPB) s.blk4[1 + g] = src[g];
   }
+  const View V{reinterpret_cast<const uint8_t*>(s.blk4), reinterpret_cast<const uint32_t*>(s.blk4),
+               uint32_t(kPad + (boff & 15))};
   if (t == 0) {
     s.shift = uint32_t(boff & 15);
     // Init :248-256, readFirstKey :418-485 (cheap scalar checks from global)
@@ -318,141 +434,57 @@ __global__ void __launch_bounds__(kTPB) rowblk_decode_kernel(Args A) {
       }
     }
     s.status = st;
-    s.restarts_off = int32_t(roff);
+    s.roff = int32_t(roff);
     s.nres = (st == PBL_OK) ? uint32_t(nr) : 0;
+    s.S = (st == PBL_OK && nr > 0) ? uint32_t(kKvCap) / uint32_t(nr) : 1;
     s.slow = (st == PBL_OK && (!fits || uint32_t(nr) > uint32_t(kRunCap))) ? 1u : 0u;
-  }
-  __syncthreads();
-
-  // ---- LDS path: run walks ------------------------------------------------------
-  const uint32_t nres = s.nres;
-  const int32_t roff = s.restarts_off;
-  if (s.status == PBL_OK && !s.slow && roff > 0) {
-    // A1: one lane per restart run counts its entries and checks that the walk
-    // lands exactly on the next restart (else: general path).
-    for (uint32_t r = t; r < nres; r += kTPB) {
-      uint32_t st = uint32_t(roff) + 4 * r;
-      uint32_t s0 = lds_le32(s, st) & kRestartMask;
-      uint32_t e0 = (r + 1 < nres) ? (lds_le32(s, st + 4) & kRestartMask) : uint32_t(roff);
-      uint32_t cnt = 0;
-      bool ok = (r != 0 || s0 == 0) && s0 < e0 && e0 <= uint32_t(roff);
-      uint32_t pos = s0;
-      while (ok && pos < e0) {
-        uint32_t sh, un, vl;
-        int x = lds_varint(s, pos, e0, &sh);
-        int y = x ? lds_varint(s, pos + x, e0, &un) : 0;
-        int z = y ? lds_varint(s, pos + x + y, e0, &vl) : 0;
-        if (!z || (cnt == 0 && sh != 0)) { ok = false; break; }
-        uint64_t np = uint64_t(pos) + x + y + z + un + vl;
-        if (np > e0) { ok = false; break; }
-        pos = uint32_t(np);
-        cnt++;
-      }
-      if (!ok || pos != e0) atomicOr(&s.slow, 1u);
-      s.vout[r] = cnt;  // run counts (vout reused as scratch)
-    }
-    __syncthreads();
-    if (!s.slow) {
-      // exclusive scan of run counts -> run kv0 (2 runs per thread)
-      uint32_t r0 = 2 * t, r1 = 2 * t + 1;
-      uint32_t c0 = r0 < nres ? s.vout[r0] : 0, c1 = r1 < nres ? s.vout[r1] : 0;
-      uint32_t e0, ed, tot, totd;
-      block_excl_scan2(c0 + c1, 0, &e0, &ed, s.scratch, &tot, &totd);
-      __syncthreads();
-      if (r0 < nres) s.vout[r0] = e0;
-      if (r1 < nres) s.vout[r1] = e0 + c0;
-      if (t == 0) { s.nkv = tot; if (tot > uint32_t(kKvCap)) s.slow = 1; }
-      __syncthreads();
-    }
-    if (!s.slow) {
-      // A2: re-walk each run, recording per-entry geometry
-      for (uint32_t r = t; r < nres; r += kTPB) {
-        uint32_t st = uint32_t(roff) + 4 * r;
-        uint32_t w0 = lds_le32(s, st);
-        uint32_t s0 = w0 & kRestartMask;
-        uint32_t e0 = (r + 1 < nres) ? (lds_le32(s, st + 4) & kRestartMask) : uint32_t(roff);
-        uint32_t j = s.vout[r];
-        uint32_t pos = s0, prev_kl = 0;
-        bool first = true;
-        while (pos < e0) {
-          uint32_t sh, un, vl;
-          int x = lds_varint(s, pos, e0, &sh);
-          int y = lds_varint(s, pos + x, e0, &un);
-          int z = lds_varint(s, pos + x + y, e0, &vl);
-          if (sh > prev_kl) atomicMax(&s.status, uint32_t(PBL_CORRUPT_BOUNDS));
-          s.eoff[j] = uint16_t(pos);
-          s.ksrc[j] = uint16_t(pos + x + y + z);
-          s.sh[j] = uint16_t(sh) | (first ? kRunStart : 0);
-          s.klen[j] = uint16_t(sh + un);
-          s.vsrc[j] = uint16_t(pos + x + y + z + un);
-          s.vlen[j] = uint16_t(vl);
-          s.kvf[j] = first ? uint8_t(PBL_KV_RESTART | ((w0 >> 31) ? PBL_KV_RESTART_SAMEPFX : 0)) : 0;
-          prev_kl = sh + un;
-          pos += x + y + z + un + vl;
-          first = false;
-          j++;
-        }
-      }
-      __syncthreads();
-      // per-KV sizes (value-prefix classification needs the trailer kind)
-      const uint32_t nkv = s.nkv;
-      uint32_t kl2[2], vl2[2];
-#pragma unroll
-      for (int q = 0; q < 2; q++) {
-        uint32_t j = 2 * t + q;
-        kl2[q] = vl2[q] = 0;
-        if (j < nkv) {
-          uint8_t fl = s.kvf[j];
-          uint64_t tr = entry_trailer(s, j, &fl, flags);
-          uint32_t kl = s.klen[j];
-          kl2[q] = (flags & PBL_ROW_RAW_KEYS) ? kl : kl >= 8 ? kl - 8 : 0;
-          uint32_t vs = s.vsrc[j], vl = s.vlen[j];
-          if ((flags & PBL_ROW_VALUE_PREFIX) && !(flags & PBL_ROW_RAW_KEYS) && (tr & 0xff) == 1) {
-            if (vl == 0) {
-              atomicMax(&s.status, uint32_t(PBL_CORRUPT_BOUNDS));
-            } else {
-              uint8_t pre = lb(s, vs);
-              if ((pre & 0xC0) == 0 || (flags & PBL_ROW_NO_VALUER)) { vs++; vl--; }
-              else if ((pre & 0xC0) == 0x80) fl |= PBL_KV_VALBLK_HANDLE;
-              else fl |= PBL_KV_BLOB_HANDLE;
-            }
-          }
-          s.vsrc[j] = uint16_t(vs);
-          s.vlen[j] = uint16_t(vl);
-          s.kvf[j] = fl;
-          vl2[q] = vl;
-        }
-      }
-      uint32_t ek, ev, tk, tv;
-      block_excl_scan2(kl2[0] + kl2[1], vl2[0] + vl2[1], &ek, &ev, s.scratch, &tk, &tv);
-      {
-        uint32_t j = 2 * t;
-        if (j < nkv) { s.kout[j] = ek; s.vout[j] = ev; }
-        if (j + 1 < nkv) { s.kout[j + 1] = ek + kl2[0]; s.vout[j + 1] = ev + vl2[0]; }
-        if (t == 0) { s.kout[nkv] = tk; s.vout[nkv] = tv; s.tot_kb = tk; s.tot_vb = tv; }
-      }
-      __syncthreads();
-    }
-  } else if (t == 0) {
     s.nkv = 0;
     s.tot_kb = s.tot_vb = 0;
-    if (s.status == PBL_OK && !s.slow) {  // empty block (restarts offset 0)
-      s.kout[0] = s.vout[0] = 0;
+    s.kout[0] = s.vout[0] = 0;
+  }
+  __syncthreads();
+  STAMP(1);
+
+  // ---- P1: run walks + block scan of the per-run sums -----------------------------
+  const uint32_t nres = s.nres;
+  const uint32_t roff = uint32_t(s.roff);
+  const uint32_t S = s.S;
+  if (s.status == PBL_OK && !s.slow && roff > 0) {
+    // thread t owns run t (nres <= 256) or runs 2t, 2t+1
+    const bool two = nres > uint32_t(kTPB);
+    uint32_t rA = two ? 2 * t : t, rB = 2 * t + 1;
+    uint32_t cA = 0, kA = 0, vA = 0, cB = 0, kB = 0, vB = 0;
+    if (rA < nres) walk_run(s, V, rA, nres, roff, S, flags, &cA, &kA, &vA);
+    if (two && rB < nres) walk_run(s, V, rB, nres, roff, S, flags, &cB, &kB, &vB);
+    STAMP(2);
+    uint32_t e[3], tot[3];
+    block_excl_scan3(cA + cB, kA + kB, vA + vB, e, tot, s.scratch);
+    if (rA < nres) { s.aux[kRunKv0 + rA] = e[0]; s.aux[kRunKb0 + rA] = e[1]; s.aux[kRunVb0 + rA] = e[2]; }
+    if (two && rB < nres) {
+      s.aux[kRunKv0 + rB] = e[0] + cA; s.aux[kRunKb0 + rB] = e[1] + kA; s.aux[kRunVb0 + rB] = e[2] + vA;
+    }
+    if (t == 0) {
+      s.aux[kRunKv0 + nres] = tot[0];
+      s.nkv = tot[0];
+      s.tot_kb = tot[1];
+      s.tot_vb = tot[2];
+      s.kout[tot[0] <= uint32_t(kKvCap) ? tot[0] : 0] = tot[1];
+      s.vout[tot[0] <= uint32_t(kKvCap) ? tot[0] : 0] = tot[2];
+      if (tot[0] > uint32_t(kKvCap) || tot[1] > kMaxFastKeyBytes) s.slow = 1;
     }
   }
   __syncthreads();
+  STAMP(3);
 
   // ---- general path (wave 0 only) -------------------------------------------------
   if (s.slow && s.status == PBL_OK) {
     if (wave_id() != 0) return;
     // keybuf: the block staging area when the block is read from global memory,
     // else the per-KV arrays (unused on this path)
-    uint8_t* keybuf = fits ? reinterpret_cast<uint8_t*>(s.eoff)
-                           : reinterpret_cast<uint8_t*>(s.blk4);
-    uint32_t keycap = fits ? uint32_t(reinterpret_cast<uint8_t*>(s.scratch) -
-                                      reinterpret_cast<uint8_t*>(s.eoff))
+    uint8_t* keybuf = fits ? reinterpret_cast<uint8_t*>(s.eoff) : reinterpret_cast<uint8_t*>(s.blk4);
+    uint32_t keycap = fits ? uint32_t(reinterpret_cast<uint8_t*>(s.scratch) - reinterpret_cast<uint8_t*>(s.eoff))
                            : uint32_t(kLdsBlkBytes);
-    const uint8_t* src = fits ? reinterpret_cast<const uint8_t*>(s.blk4) + s.shift : gblk;
+    const uint8_t* src = fits ? reinterpret_cast<const uint8_t*>(s.blk4) + kPad + s.shift : gblk;
     SlowState ss;
     uint64_t dummy[kNumComp] = {0, 0, 0, 0};
     slow_walk(src, blen, flags, keybuf, keycap, 0, A, b, dummy, &ss);
@@ -464,81 +496,93 @@ __global__ void __launch_bounds__(kTPB) rowblk_decode_kernel(Args A) {
     agg[3] = ok ? ss.nr : 0;
     lookback(lb_state, nb, b, agg, excl, &O.totals->status_mask);
     uint32_t status = ss.status;
-    if (ok && (excl[0] + agg[0] > O.kv_cap || excl[1] + agg[1] > O.key_cap ||
-               excl[2] + agg[2] > O.val_cap || (O.restarts && excl[3] + agg[3] > O.rst_cap)))
-      status = PBL_OVERFLOW;
+    if (ok && overflows(O, excl, agg)) status = PBL_OVERFLOW;
     if (status == PBL_OK) {
       slow_walk(src, blen, flags, keybuf, keycap, 1, A, b, excl, &ss);
     } else if (lane_id() == 0 && excl[0] + b < O.kv_cap + nb) {
       O.key_off[excl[0] + b] = 0;
       O.val_off[excl[0] + b] = 0;
     }
-    if (lane_id() == 0) {
-      O.blk_kv_base[b] = excl[0];
-      O.blk_key_base[b] = excl[1];
-      O.blk_val_base[b] = excl[2];
-      if (O.blk_rst_base) O.blk_rst_base[b] = excl[3];
-      O.blk_status[b] = status;
-      atomicAdd(&O.totals->n_slow_blocks, 1u);
-      if (status != PBL_OK) {
-        atomicOr(&O.totals->status_mask, 1u << status);
-        atomicAdd(&O.totals->n_bad_blocks, 1u);
-      }
-      if (b == nb - 1) {
-        O.blk_kv_base[nb] = excl[0] + agg[0];
-        O.blk_key_base[nb] = excl[1] + agg[1];
-        O.blk_val_base[nb] = excl[2] + agg[2];
-        if (O.blk_rst_base) O.blk_rst_base[nb] = excl[3] + agg[3];
-        O.totals->n_kv = excl[0] + agg[0];
-        O.totals->key_bytes = excl[1] + agg[1];
-        O.totals->val_bytes = excl[2] + agg[2];
-        O.totals->n_restarts = excl[3] + agg[3];
-      }
-    }
+    if (lane_id() == 0) write_block_meta(O, b, nb, status, excl, agg, true);
     return;
   }
 
-  // ---- LDS path: look-back, then writes -------------------------------------------
+  // ---- P2 (+ look-back) ------------------------------------------------------------
   const bool ok = s.status == PBL_OK;
   const uint32_t nkv = ok ? s.nkv : 0;
+  if (ok && roff > 0 && vprefix) {
+    // value-prefix classification needs every trailer kind before the value
+    // totals are final: expand with all threads, classify, re-scan values
+    for (uint32_t q = t; q < nres * S; q += kTPB) expand_slot(s, V, q, S, roff, flags);
+    __syncthreads();
+    uint32_t vl2[2];
+#pragma unroll
+    for (int qq = 0; qq < 2; qq++) {
+      uint32_t j = 2 * t + qq;
+      vl2[qq] = 0;
+      if (j < nkv) {
+        uint8_t fl = s.kvf[j];
+        uint64_t tr = entry_trailer(s, V, j, &fl, flags);
+        uint32_t vs = s.vsrc[j], vl = s.vlen[j];
+        if ((tr & 0xff) == 1) {
+          if (vl == 0) {
+            atomicMax(&s.status, uint32_t(PBL_CORRUPT_BOUNDS));  // Go: i.val[0] panics
+          } else {
+            uint32_t pre = V.byte(vs);
+            if ((pre & 0xC0) == 0 || (flags & PBL_ROW_NO_VALUER)) { vs++; vl--; }
+            else if ((pre & 0xC0) == 0x80) fl |= PBL_KV_VALBLK_HANDLE;
+            else fl |= PBL_KV_BLOB_HANDLE;
+          }
+          s.vsrc[j] = uint16_t(vs);
+          s.vlen[j] = uint16_t(vl);
+        }
+        s.kvf[j] = fl;
+        vl2[qq] = vl;
+      }
+    }
+    uint32_t ev, ed, tv, td;
+    block_excl_scan2(vl2[0] + vl2[1], 0, &ev, &ed, s.scratch, &tv, &td);
+    {
+      uint32_t j = 2 * t;
+      if (j < nkv) s.vout[j] = ev;
+      if (j + 1 < nkv) s.vout[j + 1] = ev + vl2[0];
+      if (t == 0) { s.vout[nkv] = tv; s.tot_vb = tv; }
+    }
+    __syncthreads();
+    for (uint32_t j = t; j < nkv; j += kTPB) {
+      uint32_t vo = s.vout[j], vl = s.vlen[j];
+      for (uint32_t bk = (vo + kBkt - 1) / kBkt; bk * kBkt < vo + vl; bk++) s.aux[kVBkt + bk] = uint16_t(j);
+    }
+  }
+  STAMP(4);
   if (wave_id() == 0) {
     uint64_t agg[kNumComp], excl[kNumComp];
-    agg[0] = nkv;
-    agg[1] = ok ? s.tot_kb : 0;
-    agg[2] = ok ? s.tot_vb : 0;
-    agg[3] = ok ? nres : 0;
+    bool okk = s.status == PBL_OK;  // (vprefix classification may have flagged it)
+    agg[0] = okk ? nkv : 0;
+    agg[1] = okk ? s.tot_kb : 0;
+    agg[2] = okk ? s.tot_vb : 0;
+    agg[3] = okk ? nres : 0;
     lookback(lb_state, nb, b, agg, excl, &O.totals->status_mask);
+    STAMP(9);
     if (lane_id() == 0) {
       uint32_t status = s.status;
-      if (ok && (excl[0] + agg[0] > O.kv_cap || excl[1] + agg[1] > O.key_cap ||
-                 excl[2] + agg[2] > O.val_cap || (O.restarts && excl[3] + agg[3] > O.rst_cap)))
-        status = PBL_OVERFLOW;
+      if (okk && overflows(O, excl, agg)) status = PBL_OVERFLOW;
       s.status = status;
 #pragma unroll
       for (int c = 0; c < kNumComp; c++) s.bases[c] = excl[c];
-      O.blk_kv_base[b] = excl[0];
-      O.blk_key_base[b] = excl[1];
-      O.blk_val_base[b] = excl[2];
-      if (O.blk_rst_base) O.blk_rst_base[b] = excl[3];
-      O.blk_status[b] = status;
-      if (status != PBL_OK) {
-        atomicOr(&O.totals->status_mask, 1u << status);
-        atomicAdd(&O.totals->n_bad_blocks, 1u);
-        if (excl[0] + b < O.kv_cap + nb) { O.key_off[excl[0] + b] = 0; O.val_off[excl[0] + b] = 0; }
+      if (status != PBL_OK && excl[0] + b < O.kv_cap + nb) {
+        O.key_off[excl[0] + b] = 0;
+        O.val_off[excl[0] + b] = 0;
       }
-      if (b == nb - 1) {
-        O.blk_kv_base[nb] = excl[0] + agg[0];
-        O.blk_key_base[nb] = excl[1] + agg[1];
-        O.blk_val_base[nb] = excl[2] + agg[2];
-        if (O.blk_rst_base) O.blk_rst_base[nb] = excl[3] + agg[3];
-        O.totals->n_kv = excl[0] + agg[0];
-        O.totals->key_bytes = excl[1] + agg[1];
-        O.totals->val_bytes = excl[2] + agg[2];
-        O.totals->n_restarts = excl[3] + agg[3];
-      }
+      write_block_meta(O, b, nb, status, excl, agg, false);
     }
+  } else if (ok && roff > 0 && !vprefix) {
+    // waves 1-3 expand the slots while wave 0 waits on the look-back
+    for (uint32_t q = t - kWave; q < nres * S; q += kTPB - kWave) expand_slot(s, V, q, S, roff, flags);
+    STAMPT(10, kWave);
   }
   __syncthreads();
+  STAMP(5);
   if (s.status != PBL_OK) return;
 
   const uint64_t kvb = s.bases[0], kbb = s.bases[1], vbb = s.bases[2], rbb = s.bases[3];
@@ -549,79 +593,40 @@ __global__ void __launch_bounds__(kTPB) rowblk_decode_kernel(Args A) {
     O.val_off[o] = s.vout[j];
     if (j < nkv) {
       uint8_t fl = s.kvf[j];
-      uint64_t tr = entry_trailer(s, j, &fl, flags);
-      O.trailer[kvb + j] = tr;
+      O.trailer[kvb + j] = entry_trailer(s, V, j, &fl, flags);
       if (O.kv_flags) O.kv_flags[kvb + j] = fl;
       if (O.entry_off) O.entry_off[kvb + j] = s.eoff[j];
     }
   }
   if (O.restarts)
-    for (uint32_t r = t; r < nres; r += kTPB) O.restarts[rbb + r] = lds_le32(s, uint32_t(roff) + 4 * r);
+    for (uint32_t r = t; r < nres; r += kTPB) O.restarts[rbb + r] = V.le32(roff + 4 * r);
+  STAMP(6);
 
   // key bytes: 16-byte granules over [kbb, kbb + KB)
   {
     const uint64_t lo = kbb, hi = kbb + s.tot_kb;
     const uint64_t g0 = lo & ~uint64_t(15);
     for (uint64_t ga = g0 + 16ull * t; ga < hi; ga += 16ull * kTPB) {
-      uint4 g = make_uint4(0, 0, 0, 0);
-      uint64_t first = ga < lo ? lo : ga;
-      uint32_t o = uint32_t(first - lo);
-      // largest j with kout[j] <= o (skipping empty keys)
-      int lo_j = 0, hi_j = int(nkv) - 1;
-      while (lo_j < hi_j) {
-        int mid = (lo_j + hi_j + 1) >> 1;
-        if (s.kout[mid] <= o) lo_j = mid; else hi_j = mid - 1;
-      }
-      int j = lo_j;
-      int src = -1;  // resolved source entry for the current key/position
-#pragma unroll
-      for (int i = 0; i < 16; i++) {
-        uint64_t a = ga + i;
-        if (a < lo || a >= hi) continue;
-        uint32_t oo = uint32_t(a - lo);
-        while (s.kout[j + 1] <= oo) { j++; src = -1; }
-        uint32_t p = oo - s.kout[j];
-        if (src < 0) {
-          src = j;
-          while (p < uint32_t(s.sh[src] & 0x7fff)) src--;
-        } else {
-          while (src < j && uint32_t(s.sh[src + 1] & 0x7fff) <= p) src++;
-        }
-        put_byte(g, i, lb(s, s.ksrc[src] + p - (s.sh[src] & 0x7fff)));
-      }
-      store_granule(O.key_bytes, ga, lo, hi, g);
+      const uint64_t ga_lo = ga < lo ? lo : ga, ga_hi = ga + 16 < hi ? ga + 16 : hi;
+      uint4 w = key_granule(s, V, uint32_t(ga_lo - lo), uint32_t(ga_hi - lo), uint32_t(ga_lo - ga), nkv);
+      store16(O.key_bytes, ga, lo, hi, w);
     }
   }
+  STAMP(7);
   // value bytes: 16-byte granules over [vbb, vbb + VB)
   {
     const uint64_t lo = vbb, hi = vbb + s.tot_vb;
     const uint64_t g0 = lo & ~uint64_t(15);
     for (uint64_t ga = g0 + 16ull * t; ga < hi; ga += 16ull * kTPB) {
-      uint64_t first = ga < lo ? lo : ga;
-      uint32_t o = uint32_t(first - lo);
-      int lo_j = 0, hi_j = int(nkv) - 1;
-      while (lo_j < hi_j) {
-        int mid = (lo_j + hi_j + 1) >> 1;
-        if (s.vout[mid] <= o) lo_j = mid; else hi_j = mid - 1;
-      }
-      int j = lo_j;
-      uint4 g;
-      if (ga >= lo && ga + 16 <= hi && ga + 16 - lo <= s.vout[j + 1]) {
-        g = lds_gather16(s, s.vsrc[j] + (o - s.vout[j]));
-      } else {
-        g = make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-          uint64_t a = ga + i;
-          if (a < lo || a >= hi) continue;
-          uint32_t oo = uint32_t(a - lo);
-          while (s.vout[j + 1] <= oo) j++;
-          put_byte(g, i, lb(s, s.vsrc[j] + (oo - s.vout[j])));
-        }
-      }
-      store_granule(O.val_bytes, ga, lo, hi, g);
+      const uint64_t ga_lo = ga < lo ? lo : ga, ga_hi = ga + 16 < hi ? ga + 16 : hi;
+      uint4 w = val_granule(s, V, uint32_t(ga_lo - lo), uint32_t(ga_hi - lo), uint32_t(ga_lo - ga));
+      store16(O.val_bytes, ga, lo, hi, w);
     }
   }
+#ifdef PBL_STAMPS
+  __syncthreads();
+  STAMP(8);
+#endif
 }
 
 __global__ void rebase_kernel(uint64_t* kvb, uint64_t* kb, uint64_t* vb, uint64_t* rb, uint32_t n,
@@ -654,21 +659,20 @@ extern "C" {
 
 int pbl_abi_version(void) { return PBL_ABI_VERSION; }
 
-uint64_t pbl_workspace_bytes(uint32_t n_blocks) { return pbl::ws_bytes(n_blocks); }
+uint64_t pbl_workspace_bytes(uint32_t n_blocks) { return pbl::ws_alloc_bytes(n_blocks); }
 
 int pbl_decode_batch_colblk(const pbl_block_batch* batch, pbl_decode_out* out, void* stream);
 
 int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stream) {
   if (!batch || !out) return PBL_INVALID_ARG;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (!out->totals || !out->blk_kv_base || !out->blk_key_base || !out->blk_val_base ||
-      !out->blk_status)
+  if (!out->totals || !out->blk_kv_base || !out->blk_key_base || !out->blk_val_base || !out->blk_status)
     return PBL_INVALID_ARG;
   if (hipMemsetAsync(out->totals, 0, sizeof(pbl_totals), st) != hipSuccess) return PBL_DEVICE_ERROR;
   if (batch->n_blocks == 0) return PBL_OK;
-  if (!batch->blocks || !batch->block_off || !batch->block_len || !out->trailer ||
-      !out->key_off || !out->val_off || !out->key_bytes || !out->val_bytes || !out->workspace ||
-      out->workspace_bytes < pbl::ws_bytes(batch->n_blocks))
+  if (!batch->blocks || !batch->block_off || !batch->block_len || !out->trailer || !out->key_off ||
+      !out->val_off || !out->key_bytes || !out->val_bytes || !out->workspace ||
+      out->workspace_bytes < pbl::ws_alloc_bytes(batch->n_blocks))
     return PBL_INVALID_ARG;
   if (batch->format != PBL_FMT_ROW) return pbl_decode_batch_colblk(batch, out, stream);
   if (hipMemsetAsync(out->workspace, 0, pbl::ws_bytes(batch->n_blocks), st) != hipSuccess)
@@ -685,9 +689,9 @@ int pbl_rebase_blocks(pbl_decode_out* out, uint32_t n_blocks, uint64_t kv_base, 
   if (!out || !out->blk_kv_base || !out->blk_key_base || !out->blk_val_base) return PBL_INVALID_ARG;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   uint32_t n = n_blocks + 1;
-  hipLaunchKernelGGL(pbl::row::rebase_kernel, dim3((n + 255) / 256), dim3(256), 0, st,
-                     out->blk_kv_base, out->blk_key_base, out->blk_val_base, out->blk_rst_base,
-                     n_blocks, kv_base, key_base, val_base, rst_base);
+  hipLaunchKernelGGL(pbl::row::rebase_kernel, dim3((n + 255) / 256), dim3(256), 0, st, out->blk_kv_base,
+                     out->blk_key_base, out->blk_val_base, out->blk_rst_base, n_blocks, kv_base, key_base,
+                     val_base, rst_base);
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }
 

@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Summarize a scripts/gpu_prof.sh run (gpurun_out/prof) into profiles/<tag>_*.
+
+Writes <tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats output, copied),
+<tag>_pmc.json (per-dispatch means of every counter for the decode kernel) and
+profiles/pmc_traffic.json (HBM bytes per launch, gfx950-corrected per
+MI355X_MICROARCH.md §HBM: FETCH_SIZE x 2 for 16-B/lane streaming reads,
+WRITE_SIZE as is; both in KiB).
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+src = os.path.join(ROOT, "gpurun_out", "prof")
+dst = os.path.join(ROOT, "profiles")
+os.makedirs(dst, exist_ok=True)
+KERNEL = sys.argv[2] if len(sys.argv) > 2 else "rowblk_decode_kernel"
+NB = int(sys.argv[3]) if len(sys.argv) > 3 else 65536
+
+shutil.copy(os.path.join(src, "trace", "trace_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
+pmc = collections.defaultdict(list)
+for f in glob.glob(os.path.join(src, "*", "*_counter_collection.csv")):
+    for r in csv.DictReader(open(f)):
+        if KERNEL in r["Kernel_Name"]:
+            pmc[r["Counter_Name"]].append(float(r["Counter_Value"]))
+means = {k: sum(v) / len(v) for k, v in pmc.items()}
+stats = {}
+for r in csv.DictReader(open(os.path.join(src, "trace", "trace_kernel_stats.csv"))):
+    if KERNEL in r["Name"]:
+        stats = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
+                 "max_ns": float(r["MaxNs"])}
+out = {"kernel": KERNEL, "workload_blocks": NB, "trace": stats, "pmc_per_dispatch_mean": means}
+if "FETCH_SIZE" in means and "WRITE_SIZE" in means:
+    fetch = means["FETCH_SIZE"] * 2 * 1024
+    write = means["WRITE_SIZE"] * 1024
+    out["hbm_bytes_per_launch"] = fetch + write
+    json.dump({"kernel": KERNEL, "workload_blocks": NB, "block_size": 32768,
+               "fetch_bytes_corrected": fetch, "write_bytes": write,
+               "hbm_bytes_per_launch": fetch + write,
+               "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes; FETCH_SIZE(KiB)x2x1024 "
+                         "(gfx950 16-B/lane streaming-read correction), WRITE_SIZE(KiB)x1024",
+               "source": f"profiles/{tag}_pmc.json"}, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
+json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
+print(json.dumps(out, indent=1))

@@ -121,7 +121,7 @@ def test_oracle_hamlet_sst_against_h_txt(golden):
 def test_oracle_batch_layout_matches_block_decode(golden):
     blob, off, lens = _hamlet_batch(golden)
     r = oracle.rowblk_decode_batch(blob, off, lens)
-    assert r["n_kv"] == 1710 and r["status_mask"] == 1
+    assert r["n_kv"] == 1710 and r["status_mask"] == 0
     for b in range(len(off)):
         st, kvs, rs = oracle.rowblk_decode_block(blob[int(off[b]):int(off[b]) + int(lens[b])].tobytes())
         kv0 = int(r["blk_kv_base"][b])
@@ -178,7 +178,7 @@ def test_generator_blocks_decode_on_oracle():
     buf, off, lens, n_kv = gen_row_blocks(7, 8, 32768, 16, 16, 100)
     assert (lens <= 32768).all() and (lens > 32000).all()
     r = oracle.rowblk_decode_batch(buf, off, lens)
-    assert r["n_kv"] == n_kv and r["status_mask"] == 1
+    assert r["n_kv"] == n_kv and r["status_mask"] == 0
     # ~271 KVs / 17 restarts per 32 KiB block
     per = np.diff(r["blk_kv_base"].astype(np.int64))
     assert 250 <= per.min() and per.max() <= 290
