@@ -202,3 +202,18 @@ def test_full_size_batch_properties():
     for k in ARRAYS:
         if g[k] is not None:
             assert hashlib.sha256(g[k].tobytes()).digest() == hashlib.sha256(o[k].tobytes()).digest(), k
+
+
+def test_device_offset_concat_matches_exclusive_prefix():
+    import torch
+    from pebble_amd.batch import BlockBatch, decode, offset_concat
+    from pebble_amd.shard import exclusive_bases
+    buf, off, lens, n = gen_row_blocks(12, 8, 32768, 16, 16, 100)
+    out = decode(BlockBatch.from_host(buf, off, lens, "cuda"))
+    before = torch.stack([out.blk_kv_base[:9], out.blk_key_base[:9], out.blk_val_base[:9], out.blk_rst_base[:9]]).clone()
+    totals = torch.tensor([[5, 50, 500, 7], [11, 110, 1100, 13], [1, 2, 3, 4]], dtype=torch.int64, device="cuda")
+    offset_concat(out, totals.reshape(-1).contiguous(), 2)
+    torch.cuda.synchronize()
+    after = torch.stack([out.blk_kv_base[:9], out.blk_key_base[:9], out.blk_val_base[:9], out.blk_rst_base[:9]])
+    exp = exclusive_bases(totals, 2)
+    assert torch.equal(after - before, exp.view(4, 1).expand(4, 9))
