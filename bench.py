@@ -2,8 +2,12 @@
 """Benchmark: raw-block GiB/s decoded to KV arrays (device-resident).
 
 One "step" = one decode pass of the hot path over one batch of synthetic data
-blocks already resident in HBM (BASELINE.json config 2 per GPU: 64 Ki x 32 KiB
-row-format blocks, restart interval 16, 16 B user keys / 100 B values).  With
+blocks already resident in HBM.  Default workload (`--workload row`) is
+BASELINE.json config 2 per GPU: 64 Ki x 32 KiB row-format blocks, restart
+interval 16, 16 B user keys / 100 B values.  `--workload col` is config 3
+(64 Ki x 32 KiB colblk blocks, cockroachkvs crdb1 schema, 22 B keys / 128 B
+values); `--workload mixed` is config 4's per-GPU shard (128 Ki blocks, even
+ids row / odd ids colblk, 1 Mi blocks over 8 GPUs).  With
 N > 1 (torch.distributed.run, one rank per GPU, RCCL) every rank decodes its own
 64 Ki-block shard (weak scaling) and each step also performs the offset concat:
 an all-gather of per-rank totals and the rebase of the per-block bases.
@@ -36,7 +40,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--blocks", type=int, default=65536, help="blocks per GPU")
+    p.add_argument("--workload", choices=["row", "col", "mixed"], default="row")
+    p.add_argument("--blocks", type=int, default=0, help="blocks per GPU (0 = the workload's config)")
     p.add_argument("--block-size", type=int, default=32768)
     p.add_argument("--restart-interval", type=int, default=16)
     p.add_argument("--key-len", type=int, default=16)
@@ -80,16 +85,51 @@ def main():
 
     from pebble_amd import _native as N
     from pebble_amd.batch import BlockBatch, Capacity, DecodedBatch, decode, decode_into, offset_concat
+    from pebble_amd.colblk import gen_col_blocks
     from pebble_amd.rowblk import gen_row_blocks
 
-    nb = a.blocks
+    nb = a.blocks or (131072 if a.workload == "mixed" else 65536)
     flags = N.PBL_ROW_VALUE_PREFIX if a.value_prefix else 0
+    seed = a.seed + 7919 * rank
     t0 = time.time()
-    buf, off, lens, n_kv = gen_row_blocks(a.seed + 7919 * rank, nb, a.block_size, a.restart_interval,
-                                          a.key_len, a.val_len, a.value_prefix, n_threads=16)
+    block_fmt = None
+    if a.workload == "row":
+        fmt = N.PBL_FMT_ROW
+        buf, off, lens, n_kv = gen_row_blocks(seed, nb, a.block_size, a.restart_interval, a.key_len, a.val_len,
+                                              a.value_prefix, n_threads=16)
+        kernel = "rowblk_decode_kernel"
+        wl = (f"config2: {nb} x {a.block_size // 1024} KiB row-format blocks per GPU, restart interval "
+              f"{a.restart_interval}, {a.key_len} B keys / {a.val_len} B values" + (", value prefix" if a.value_prefix else ""))
+    elif a.workload == "col":
+        fmt = N.PBL_FMT_COL_CRDB1
+        buf, off, lens, n_kv = gen_col_blocks(seed, nb, a.block_size, n_threads=16)
+        kernel = "colblk_decode_kernel"
+        wl = (f"config3: {nb} x {a.block_size // 1024} KiB colblk blocks per GPU, cockroachkvs crdb1 schema "
+              f"(KeyGenConfig alphabet 26, RoachKeyLen 12, PrefixLenShared 4, 1 key/prefix), 128 B values")
+    else:
+        fmt = N.PBL_FMT_ROW
+        h = nb // 2
+        rb, ro, rl, rn = gen_row_blocks(seed, nb - h, a.block_size, a.restart_interval, a.key_len, a.val_len,
+                                        a.value_prefix, n_threads=16)
+        cb, co, cl, cn = gen_col_blocks(seed, h, a.block_size, n_threads=16)
+        # interleave: even block ids row, odd ids colblk, fixed stride
+        buf = np.zeros(nb * a.block_size + 16, np.uint8)
+        v = buf[: nb * a.block_size].reshape(nb, a.block_size)
+        v[0::2] = rb[: (nb - h) * a.block_size].reshape(nb - h, a.block_size)
+        v[1::2] = cb[: h * a.block_size].reshape(h, a.block_size)
+        del rb, cb
+        off = np.arange(nb, dtype=np.uint64) * a.block_size
+        lens = np.empty(nb, np.uint32)
+        lens[0::2], lens[1::2] = rl, cl
+        block_fmt = np.empty(nb, np.uint8)
+        block_fmt[0::2], block_fmt[1::2] = N.PBL_FMT_ROW, N.PBL_FMT_COL_CRDB1
+        n_kv = rn + cn
+        kernel = "mixed_decode_kernel"
+        wl = (f"config4 shard: {nb} x {a.block_size // 1024} KiB blocks per GPU, even ids row-format "
+              f"(config-2 shape), odd ids colblk crdb1 (config-3 shape)")
     gen_s = time.time() - t0
     input_bytes = int(lens.astype(np.int64).sum())
-    batch = BlockBatch.from_host(buf, off, lens, dev, N.PBL_FMT_ROW, flags)
+    batch = BlockBatch.from_host(buf, off, lens, dev, fmt, flags, block_format=block_fmt)
 
     # size the outputs exactly with one decode, then reuse them every step
     first = decode(batch)
@@ -150,7 +190,8 @@ def main():
         try:
             with open(tp) as f:
                 pt = json.load(f)
-            if pt.get("workload_blocks") == nb and pt.get("block_size") == a.block_size:
+            if (pt.get("workload_blocks") == nb and pt.get("block_size") == a.block_size
+                    and pt.get("workload", "row") == a.workload):
                 traffic = pt.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -159,12 +200,10 @@ def main():
         "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-        "config": {"workload": f"config2: {nb} x {a.block_size // 1024} KiB row-format blocks per GPU, "
-                               f"restart interval {a.restart_interval}, {a.key_len} B keys / {a.val_len} B values"
-                               + (", value prefix" if a.value_prefix else ""),
+        "config": {"workload": wl,
                    "blocks_per_gpu": nb, "input_bytes_per_gpu": input_bytes, "kvs_per_gpu": n_kv,
                    "parallelism": f"shard{world}" + ("+rccl_offset_concat" if world > 1 else "")},
-        "roofline": {"bound": "hbm", "kernel": "rowblk_decode_kernel", "achieved": round(achieved, 1),
+        "roofline": {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "alg_bytes_per_launch": ab, "kernel_ms": round(kern_ms, 4),
                      "input_GiB_per_s_kernel": round(input_bytes / (kern_ms * 1e-3) / 2**30, 1)},
@@ -176,22 +215,38 @@ def main():
         # bounded sample: the first 4096 blocks (128 MiB), repeated to ~cpu_baseline_seconds
         ns = min(nb, 4096)
         th = a.cpu_threads
-        t1 = oracle.rowblk_bench(buf, off[:ns], lens[:ns], flags, th, 0, 1)
-        reps = max(1, int(a.cpu_baseline_seconds / max(t1, 1e-3)))
-        tsec = oracle.rowblk_bench(buf, off[:ns], lens[:ns], flags, th, 0, reps)
-        sample_bytes = int(lens[:ns].astype(np.int64).sum()) * reps
-        tm1 = oracle.rowblk_bench(buf, off[:ns], lens[:ns], flags, th, 1, max(1, reps // 2))
+        # per-format samples: the first `ns` blocks of each format in the batch
+        parts = []
+        for f in ([fmt] if block_fmt is None else [N.PBL_FMT_ROW, N.PBL_FMT_COL_CRDB1]):
+            ids = np.arange(nb) if block_fmt is None else np.nonzero(block_fmt == f)[0]
+            ids = ids[:ns]
+            parts.append((f, np.ascontiguousarray(off[ids]), np.ascontiguousarray(lens[ids])))
+        budget = a.cpu_baseline_seconds / len(parts)
+        it_bytes = it_sec = m_bytes = m_sec = 0.0
+        reps_used = []
+        for f, po, pl in parts:
+            t1 = oracle.bench(buf, po, pl, f, flags, th, 0, 1)
+            reps = max(1, int(budget / max(t1, 1e-3)))
+            it_sec += oracle.bench(buf, po, pl, f, flags, th, 0, reps)
+            it_bytes += float(pl.astype(np.int64).sum()) * reps
+            mr = max(1, reps // 2)
+            m_sec += oracle.bench(buf, po, pl, f, flags, th, 1, mr)
+            m_bytes += float(pl.astype(np.int64).sum()) * mr
+            reps_used.append(reps)
+        src = {N.PBL_FMT_ROW: "oracle/rowblk_oracle.c (rowblk.Iter)",
+               N.PBL_FMT_COL_CRDB1: "oracle/colblk_oracle.c (colblk.DataBlockIter, crdb1)"}
         res["cpu_baseline"] = {
-            "value": round(sample_bytes / tsec / 2**30, 2), "unit": "GiB/s", "cores": th, "kind": "port",
-            "sample": f"{ns} blocks x {reps} passes of the same config-2 batch ({sample_bytes / 2**30:.1f} GiB), "
-                      f"iterate-only (rowblk.Iter semantics: key into a reused buffer, value zero-copy), "
-                      f"C restatement in oracle/rowblk_oracle.c on {th} threads",
-            "materialize_value": round(int(lens[:ns].astype(np.int64).sum()) * max(1, reps // 2) / tm1 / 2**30, 2),
-            "host_cpu": _cpu_model(), "seconds": round(tsec, 2),
+            "value": round(it_bytes / it_sec / 2**30, 2), "unit": "GiB/s", "cores": th, "kind": "port",
+            "sample": f"first {ns} blocks of each format in the batch x {reps_used} passes "
+                      f"({it_bytes / 2**30:.1f} GiB), iterate-only (Go iterator semantics: key materialized into "
+                      f"a reused buffer, value zero-copy, checksum), C restatement "
+                      f"{' + '.join(src[f] for f, _, _ in parts)} on {th} threads",
+            "materialize_value": round(m_bytes / m_sec / 2**30, 2),
+            "host_cpu": _cpu_model(), "seconds": round(it_sec, 2),
         }
 
     if a.e2e and rank == 0:
-        res["e2e_pcie"] = e2e_rate(buf, off, lens, flags, dev, cap)
+        res["e2e_pcie"] = e2e_rate(buf, off, lens, flags, dev, cap, fmt, block_fmt)
 
     res["gen_seconds"] = round(gen_s, 2)
     if rank == 0:
@@ -212,7 +267,7 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def e2e_rate(buf, off, lens, flags, dev, cap):
+def e2e_rate(buf, off, lens, flags, dev, cap, fmt=0, block_fmt=None):
     """Host-resident blocks -> H2D -> decode -> D2H of every output array,
     pipelined in chunks over two streams with pinned host memory."""
     from pebble_amd import _native as N
@@ -247,7 +302,8 @@ def e2e_rate(buf, off, lens, flags, dev, cap):
         with torch.cuda.stream(st):
             dbuf[: n * bs].copy_(host_in[c * chunk * bs:(c * chunk + n) * bs], non_blocking=True)
             ln[:n].copy_(lens_t[c * chunk:c * chunk + n], non_blocking=True)
-            b = BlockBatch(dbuf, o[:n], ln[:n], N.PBL_FMT_ROW, flags)
+            bf = None if block_fmt is None else torch.from_numpy(block_fmt[c * chunk:c * chunk + n]).to(dev)
+            b = BlockBatch(dbuf, o[:n], ln[:n], fmt, flags, bf)
             decode_into(b, out, st)
             # copy back capacity-bounded regions (exact sizes are known only after the kernel)
             hv.copy_(out.val_bytes[: per.val], non_blocking=True)

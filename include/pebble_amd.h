@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define PBL_ABI_VERSION 1
+#define PBL_ABI_VERSION 2
 
 /* ---- status codes (per block, and OR-ed as bit masks into totals) ---------- */
 enum {
@@ -76,6 +76,10 @@ enum {
 #define PBL_KV_VALBLK_HANDLE 0x10u /* value bytes are prefix+valblk.Handle        */
 #define PBL_KV_BLOB_HANDLE 0x20u   /* value bytes are prefix+blob handle / colblk external */
 #define PBL_KV_PREFIX_CHANGED 0x40u /* colblk prefixChanged bit                   */
+/* colblk rows: OBSOLETE = isObsolete bit (data_block.go:519); an isValueExternal
+   row (data_block.go:1700-1704) is VALBLK_HANDLE or BLOB_HANDLE by its first
+   (value-prefix) byte, and its value bytes are the raw column slice; the
+   trailer is trailers.At(row) unmasked; entry_off[] is the row index. */
 
 /* ---- batch descriptor ------------------------------------------------------- */
 typedef struct pbl_block_batch {
@@ -88,6 +92,8 @@ typedef struct pbl_block_batch {
   uint32_t format;           /* PBL_FMT_* for every block of the batch              */
   uint32_t flags;            /* PBL_ROW_* flags                                     */
   uint32_t reserved;
+  const uint8_t* block_format; /* optional [n_blocks] PBL_FMT_* per block (mixed
+                                row + colblk batches); NULL = `format` for all   */
 } pbl_block_batch;
 
 /* ---- batch totals (device struct, written by the decode kernel) -------------- */
@@ -198,6 +204,55 @@ size_t pbl_rowblk_writer_finish(pbl_rowblk_writer* w, uint8_t* dst, size_t dst_c
 uint64_t pbl_gen_row_blocks(uint64_t seed, uint32_t n_blocks, uint32_t block_size,
                             int restart_interval, uint32_t key_len, uint32_t val_len,
                             int value_prefix, uint8_t* dst, uint64_t* block_off,
+                            uint32_t* block_len, int n_threads);
+
+/* ---- colblk.DataBlockEncoder (format producer; host memory) ------------------ */
+/*
+ * sstable/colblk/data_block.go:600-790 with colblk.DefaultKeySchema
+ * (schema PBL_FMT_COL_DEFAULT, key prefix = bytes before the first '@', the
+ * testkeys comparer; data_block.go:207-345) or cockroachkvs.KeySchema
+ * (PBL_FMT_COL_CRDB1, cockroachkvs/cockroachkvs.go:505-766).
+ */
+typedef struct pbl_colblk_writer pbl_colblk_writer;
+pbl_colblk_writer* pbl_colblk_writer_new(uint32_t schema, int bundle_size);
+void pbl_colblk_writer_free(pbl_colblk_writer* w);
+void pbl_colblk_writer_reset(pbl_colblk_writer* w);
+/* Add one KV (DataBlockEncoder.Add after KeyWriter.ComparePrev).  prefix_len < 0
+ * = the schema's Split.  value_kind: 0 in place, 1 valblk handle, 2 blob handle
+ * (stored as prefix byte || value, isValueExternal set).  Returns 1 when the key's
+ * prefix equals the previous key's, 0 otherwise, PBL_INVALID_ARG (7) on a bad key. */
+int pbl_colblk_writer_add(pbl_colblk_writer* w, const uint8_t* key, size_t key_len, int64_t prefix_len,
+                          uint64_t trailer, const uint8_t* value, size_t value_len, int value_kind,
+                          int is_obsolete);
+uint32_t pbl_colblk_writer_rows(const pbl_colblk_writer* w);
+/* DataBlockEncoder.Size() as it was at `rows` rows (rows() or rows()-1). */
+size_t pbl_colblk_writer_size(const pbl_colblk_writer* w, uint32_t rows);
+/* Finish(rows, Size(rows)) with rows == rows() or rows()-1; copies the block to
+ * dst when dst_cap suffices; returns the block size (0 on a bad row count).  The
+ * writer must be reset before reuse. */
+size_t pbl_colblk_writer_finish(pbl_colblk_writer* w, uint32_t rows, uint8_t* dst, size_t dst_cap);
+
+/* cockroachkvs.KeyGenConfig (cockroachkvs/test_utils.go) + value length. */
+typedef struct pbl_colgen_config {
+  uint64_t seed;
+  uint32_t alphabet_len;       /* PrefixAlphabetLen                        */
+  uint32_t prefix_len_shared;  /* PrefixLenShared                          */
+  uint32_t roach_key_len;      /* RoachKeyLen                              */
+  uint32_t avg_keys_per_prefix;/* AvgKeysPerPrefix                         */
+  uint64_t base_wall_time;     /* BaseWallTime                             */
+  uint32_t pct_logical;        /* PercentLogical                           */
+  uint32_t value_len;
+} pbl_colgen_config;
+
+/*
+ * Synthetic colblk batch (config 3): per block, sorted KVs drawn per
+ * cockroachkvs.RandomKVs with a per-block seed, trailer MakeTrailer((block<<20)+k,
+ * SET), random value bytes; rows are added while the finished block stays
+ * <= block_size (Finish(rows-1) on overflow, as the sstable writer does) and
+ * blocks are placed at a fixed `block_size` stride.  Returns total rows.
+ */
+uint64_t pbl_gen_col_blocks(const pbl_colgen_config* cfg, uint32_t schema, uint32_t n_blocks,
+                            uint32_t block_size, uint8_t* dst, uint64_t* block_off,
                             uint32_t* block_len, int n_threads);
 
 #ifdef __cplusplus

@@ -25,22 +25,12 @@
  * the oracle reports a corruption status and emits no KVs for the block; the
  * device decoder does the same.
  */
+#define _POSIX_C_SOURCE 200809L
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
-enum { OK = 0, CORRUPT_NO_RESTARTS = 1, CORRUPT_FIRST_KEY = 2, CORRUPT_BOUNDS = 3 };
-
-#define FLAG_VALUE_PREFIX 0x1u
-#define FLAG_NO_VALUER 0x2u
-#define FLAG_RAW_KEYS 0x4u /* rowblk.RawIter (rowblk_iter.go:1743-1794) */
-
-#define KV_RESTART 0x01u
-#define KV_RESTART_SAMEPFX 0x02u
-#define KV_OBSOLETE 0x04u
-#define KV_INVALID_KEY 0x08u
-#define KV_VALBLK 0x10u
-#define KV_BLOB 0x20u
+#include "oracle.h"
 
 static const uint64_t TRAILER_OBSOLETE_MASK = (((uint64_t)1 << 56) - 1) << 8 | 191u;
 static const uint64_t TRAILER_OBSOLETE_BIT = 64u;
@@ -66,19 +56,6 @@ int orc_decode_varint(const uint8_t* p, const uint8_t* end, uint32_t* v) {
   return 0;
 }
 
-typedef struct orc_block_out {
-  /* counts (always written) */
-  uint64_t n_kv, key_bytes, val_bytes, n_restarts;
-  /* outputs; NULL = count only.  key_off/val_off hold n_kv+1 entries. */
-  uint64_t* trailer;
-  uint8_t* kv_flags;
-  uint32_t* entry_off;
-  uint32_t* key_off;
-  uint32_t* val_off;
-  uint8_t* keys;
-  uint8_t* vals;
-  uint32_t* restarts;
-} orc_block_out;
 
 /* Sequential decode of one row block exactly as rowblk.Iter First/Next sees it. */
 int orc_rowblk_decode(const uint8_t* blk, uint64_t len, uint32_t flags, orc_block_out* o) {
@@ -208,23 +185,6 @@ int orc_rowblk_decode(const uint8_t* blk, uint64_t len, uint32_t flags, orc_bloc
  * (pbl_decode_out): pass NULL output arrays to size, then call again with
  * arrays.  blk_*_base have n_blocks+1 entries.
  */
-typedef struct orc_batch_out {
-  uint64_t* trailer;
-  uint8_t* kv_flags;
-  uint32_t* entry_off;
-  uint32_t* key_off;
-  uint32_t* val_off;
-  uint8_t* key_bytes;
-  uint8_t* val_bytes;
-  uint32_t* restarts;
-  uint64_t* blk_kv_base;
-  uint64_t* blk_key_base;
-  uint64_t* blk_val_base;
-  uint64_t* blk_rst_base;
-  uint32_t* blk_status;
-  uint64_t n_kv, key_bytes_total, val_bytes_total, n_restarts;
-  uint32_t status_mask, n_bad_blocks;
-} orc_batch_out;
 
 int orc_rowblk_decode_batch(const uint8_t* blocks, const uint64_t* off, const uint32_t* len,
                             uint32_t n_blocks, uint32_t flags, orc_batch_out* bo) {

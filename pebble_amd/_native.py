@@ -30,6 +30,8 @@ STATUS_NAMES = {
     8: "DEVICE_ERROR", 9: "TIMEOUT",
 }
 
+ABI_VERSION = 2  # include/pebble_amd.h PBL_ABI_VERSION
+
 PBL_FMT_ROW = 0
 PBL_FMT_COL_DEFAULT = 1
 PBL_FMT_COL_CRDB1 = 2
@@ -55,6 +57,16 @@ class BlockBatchC(ctypes.Structure):
         ("blocks", _vp), ("block_off", _vp), ("block_len", _vp),
         ("n_blocks", ctypes.c_uint32), ("format", ctypes.c_uint32),
         ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+        ("block_format", _vp),
+    ]
+
+
+class ColGenConfigC(ctypes.Structure):
+    _fields_ = [
+        ("seed", ctypes.c_uint64), ("alphabet_len", ctypes.c_uint32),
+        ("prefix_len_shared", ctypes.c_uint32), ("roach_key_len", ctypes.c_uint32),
+        ("avg_keys_per_prefix", ctypes.c_uint32), ("base_wall_time", ctypes.c_uint64),
+        ("pct_logical", ctypes.c_uint32), ("value_len", ctypes.c_uint32),
     ]
 
 
@@ -102,6 +114,17 @@ SIGNATURES = {
     "pbl_gen_row_blocks": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                              ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                              _vp, _vp, _vp, ctypes.c_int]),
+    "pbl_colblk_writer_new": (_vp, [ctypes.c_uint32, ctypes.c_int]),
+    "pbl_colblk_writer_free": (None, [_vp]),
+    "pbl_colblk_writer_reset": (None, [_vp]),
+    "pbl_colblk_writer_add": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int64,
+                                             ctypes.c_uint64, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int,
+                                             ctypes.c_int]),
+    "pbl_colblk_writer_rows": (ctypes.c_uint32, [_vp]),
+    "pbl_colblk_writer_size": (ctypes.c_size_t, [_vp, ctypes.c_uint32]),
+    "pbl_colblk_writer_finish": (ctypes.c_size_t, [_vp, ctypes.c_uint32, _vp, ctypes.c_size_t]),
+    "pbl_gen_col_blocks": (ctypes.c_uint64, [ctypes.POINTER(ColGenConfigC), ctypes.c_uint32, ctypes.c_uint32,
+                                             ctypes.c_uint32, _vp, _vp, _vp, ctypes.c_int]),
 }
 
 _lib = None
@@ -126,7 +149,7 @@ def lib() -> ctypes.CDLL:
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    if L.pbl_abi_version() != 1:
+    if L.pbl_abi_version() != ABI_VERSION:
         raise RuntimeError("libpebble_amd.so ABI mismatch")
     _lib = L
     return L

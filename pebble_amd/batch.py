@@ -38,6 +38,7 @@ class BlockBatch:
     block_len: torch.Tensor     # int32 [n]  (uint32 in the ABI)
     format: int = N.PBL_FMT_ROW
     flags: int = 0
+    block_format: Optional[torch.Tensor] = None  # uint8 [n] per-block PBL_FMT_* (mixed batches)
 
     @property
     def n_blocks(self) -> int:
@@ -49,18 +50,22 @@ class BlockBatch:
 
     @classmethod
     def from_host(cls, blocks: np.ndarray, off: np.ndarray, lens: np.ndarray, device="cuda",
-                  fmt: int = N.PBL_FMT_ROW, flags: int = 0, non_blocking: bool = False) -> "BlockBatch":
+                  fmt: int = N.PBL_FMT_ROW, flags: int = 0, non_blocking: bool = False,
+                  block_format: Optional[np.ndarray] = None) -> "BlockBatch":
         blocks = np.ascontiguousarray(blocks, dtype=np.uint8)
         pad = np.zeros(len(blocks) + 16, np.uint8)
         pad[: len(blocks)] = blocks
         b = torch.from_numpy(pad).to(device, non_blocking=non_blocking)
         o = torch.from_numpy(np.ascontiguousarray(off, dtype=np.uint64).view(np.int64)).to(device)
         l = torch.from_numpy(np.ascontiguousarray(lens, dtype=np.uint32).view(np.int32)).to(device)
-        return cls(b, o, l, fmt, flags)
+        bf = None
+        if block_format is not None:
+            bf = torch.from_numpy(np.ascontiguousarray(block_format, dtype=np.uint8)).to(device)
+        return cls(b, o, l, fmt, flags, bf)
 
     @classmethod
     def from_blocks(cls, blocks: list, device="cuda", fmt: int = N.PBL_FMT_ROW, flags: int = 0,
-                    align: int = 8) -> "BlockBatch":
+                    align: int = 8, block_format=None) -> "BlockBatch":
         """Pack a list of block byte strings (each start `align`-aligned)."""
         offs, lens, pos = [], [], 0
         for bk in blocks:
@@ -71,11 +76,13 @@ class BlockBatch:
         buf = np.zeros(max(pos, 1), np.uint8)
         for o, bk in zip(offs, blocks):
             buf[o:o + len(bk)] = np.frombuffer(bk, np.uint8)
-        return cls.from_host(buf, np.array(offs, np.uint64), np.array(lens, np.uint32), device, fmt, flags)
+        return cls.from_host(buf, np.array(offs, np.uint64), np.array(lens, np.uint32), device, fmt, flags,
+                             block_format=None if block_format is None else np.asarray(block_format, np.uint8))
 
     def c_struct(self) -> N.BlockBatchC:
         return N.BlockBatchC(self.blocks.data_ptr(), self.block_off.data_ptr(), self.block_len.data_ptr(),
-                             self.n_blocks, self.format, self.flags, 0)
+                             self.n_blocks, self.format, self.flags, 0,
+                             self.block_format.data_ptr() if self.block_format is not None else None)
 
     def input_bytes(self) -> int:
         return int(self.block_len.to(torch.int64).sum().item()) if self.n_blocks else 0

@@ -92,20 +92,25 @@ __device__ inline void block_excl_scan2(uint32_t a, uint32_t b, uint32_t* ea, ui
   *tot_b = tb;
 }
 
-// Decoupled look-back (single-pass scan across blocks).  Executed by wave 0 of
-// the workgroup that owns virtual block `v` (tickets are handed out in launch
-// order, so every predecessor is already resident and publishes its aggregate
-// before it waits: no deadlock for any residency).  All components are walked
-// back together, kLbWin windows of 64 predecessors per round trip.  Returns
-// exclusive prefixes.
-__device__ inline void lookback(uint64_t* st, uint32_t n_blocks, uint32_t v,
-                                const uint64_t agg[kNumComp], uint64_t excl[kNumComp],
-                                uint32_t* timeout_flag) {
+// Decoupled look-back (single-pass scan across blocks), in two halves so a
+// workgroup can publish its aggregate as soon as it is known and resolve its
+// exclusive prefix later (after overlapping independent work).  Tickets are
+// handed out in launch order, so every predecessor is already resident and
+// publishes its aggregate before it waits: no deadlock for any residency.
+// Both halves are executed by wave 0 of the workgroup that owns virtual block `v`.
+__device__ inline void lb_publish(uint64_t* st, uint32_t n_blocks, uint32_t v, const uint64_t agg[kNumComp]) {
   const int l = lane_id();
   if (l < kNumComp) {
     uint64_t a = l == 0 ? agg[0] : l == 1 ? agg[1] : l == 2 ? agg[2] : agg[3];
     st_agent(st + uint64_t(l) * n_blocks + v, (v == 0 ? kStatePfx : kStateAgg) | (a & kValMask));
   }
+}
+
+// All components are walked back together, kLbWin windows of 64 predecessors
+// per round trip.  Returns exclusive prefixes and publishes the inclusive ones.
+__device__ inline void lb_resolve(uint64_t* st, uint32_t n_blocks, uint32_t v, const uint64_t agg[kNumComp],
+                                  uint64_t excl[kNumComp], uint32_t* timeout_flag) {
+  const int l = lane_id();
   uint64_t acc[kNumComp];
   int64_t top[kNumComp];
   bool done[kNumComp];
@@ -154,6 +159,64 @@ __device__ inline void lookback(uint64_t* st, uint32_t n_blocks, uint32_t v,
     uint64_t a = l == 0 ? agg[0] : l == 1 ? agg[1] : l == 2 ? agg[2] : agg[3];
     st_agent(st + uint64_t(l) * n_blocks + v, kStatePfx | ((e + a) & kValMask));
   }
+}
+
+__device__ inline void lookback(uint64_t* st, uint32_t n_blocks, uint32_t v, const uint64_t agg[kNumComp],
+                                uint64_t excl[kNumComp], uint32_t* timeout_flag) {
+  lb_publish(st, n_blocks, v, agg);
+  lb_resolve(st, n_blocks, v, agg, excl, timeout_flag);
+}
+
+// ---- shared by the row and colblk decoders --------------------------------
+struct Args {
+  pbl_block_batch in;
+  pbl_decode_out out;
+};
+
+// Store 16 bytes (w) covering global bytes [ga, ga+16) of which only [lo, hi)
+// belong to this block: one dwordx4 store when whole, byte stores at the edges.
+__device__ inline void store16(uint8_t* base, uint64_t ga, uint64_t lo, uint64_t hi, uint4 w) {
+  if (ga >= lo && ga + 16 <= hi) {
+    *reinterpret_cast<uint4*>(base + ga) = w;
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    uint32_t word = i < 4 ? w.x : i < 8 ? w.y : i < 12 ? w.z : w.w;
+    if (ga + i >= lo && ga + i < hi) base[ga + i] = uint8_t(word >> (8 * (i & 3)));
+  }
+}
+
+// Per-block results and batch totals, written by lane 0 of wave 0.
+__device__ inline void write_block_meta(const pbl_decode_out& O, uint32_t b, uint32_t nb, uint32_t status,
+                                        const uint64_t excl[kNumComp], const uint64_t agg[kNumComp],
+                                        bool slow) {
+  O.blk_kv_base[b] = excl[0];
+  O.blk_key_base[b] = excl[1];
+  O.blk_val_base[b] = excl[2];
+  if (O.blk_rst_base) O.blk_rst_base[b] = excl[3];
+  O.blk_status[b] = status;
+  if (slow) atomicAdd(&O.totals->n_slow_blocks, 1u);
+  if (status != PBL_OK) {
+    atomicOr(&O.totals->status_mask, 1u << status);
+    atomicAdd(&O.totals->n_bad_blocks, 1u);
+  }
+  if (b == nb - 1) {
+    O.blk_kv_base[nb] = excl[0] + agg[0];
+    O.blk_key_base[nb] = excl[1] + agg[1];
+    O.blk_val_base[nb] = excl[2] + agg[2];
+    if (O.blk_rst_base) O.blk_rst_base[nb] = excl[3] + agg[3];
+    O.totals->n_kv = excl[0] + agg[0];
+    O.totals->key_bytes = excl[1] + agg[1];
+    O.totals->val_bytes = excl[2] + agg[2];
+    O.totals->n_restarts = excl[3] + agg[3];
+  }
+}
+
+__device__ inline bool overflows(const pbl_decode_out& O, const uint64_t excl[kNumComp],
+                                 const uint64_t agg[kNumComp]) {
+  return excl[0] + agg[0] > O.kv_cap || excl[1] + agg[1] > O.key_cap || excl[2] + agg[2] > O.val_cap ||
+         (O.restarts && excl[3] + agg[3] > O.rst_cap);
 }
 
 }  // namespace pbl

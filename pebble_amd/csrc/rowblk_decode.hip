@@ -25,6 +25,7 @@
 // not fit the LDS limits, take the general path (rowblk_general.hip.h): a
 // wave-serial restatement of Iter.First/Next, bit-identical by construction.
 #include "common.hip.h"
+#include "colblk_block.hip.h"
 
 namespace pbl {
 namespace row {
@@ -172,20 +173,6 @@ __device__ inline uint64_t entry_trailer(const Lds& s, const View& V, int j, uin
   return raw & kTrailerObsoleteMask;
 }
 
-// Store 16 bytes (w) covering global bytes [ga, ga+16) of which only [lo, hi)
-// belong to this block: one dwordx4 store when whole, byte stores at the edges.
-__device__ inline void store16(uint8_t* base, uint64_t ga, uint64_t lo, uint64_t hi, uint4 w) {
-  if (ga >= lo && ga + 16 <= hi) {
-    *reinterpret_cast<uint4*>(base + ga) = w;
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    uint32_t word = i < 4 ? w.x : i < 8 ? w.y : i < 12 ? w.z : w.w;
-    if (ga + i >= lo && ga + i < hi) base[ga + i] = uint8_t(word >> (8 * (i & 3)));
-  }
-}
-
 // Block-wide exclusive scan of three u32 sequences (one value each per thread).
 __device__ inline void block_excl_scan3(uint32_t a, uint32_t b, uint32_t c, uint32_t* e, uint32_t* tot,
                                         uint32_t* scratch) {
@@ -211,10 +198,6 @@ __device__ inline void block_excl_scan3(uint32_t a, uint32_t b, uint32_t c, uint
   tot[2] = tt[2];
 }
 
-struct Args {
-  pbl_block_batch in;
-  pbl_decode_out out;
-};
 
 #ifdef PBL_STAMPS
 // diagnostic build only: per-block phase timestamps (s_memtime) written past
@@ -373,24 +356,21 @@ __device__ inline uint4 val_granule(const Lds& s, const View& V, uint32_t o, uin
 // ---------------------------------------------------------------------------
 // The decode kernel.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kTPB) rowblk_decode_kernel(Args A) {
-  __shared__ Lds s;
+// Decode row block b (the caller has taken ticket b).
+__device__ __forceinline__ void row_block(Lds& s, const Args& A, const uint32_t b) {
   const int t = threadIdx.x;
   const pbl_decode_out& O = A.out;
   const uint32_t nb = A.in.n_blocks;
   const uint32_t flags = A.in.flags;
   const bool vprefix = (flags & PBL_ROW_VALUE_PREFIX) && !(flags & PBL_ROW_RAW_KEYS);
   uint8_t* ws = reinterpret_cast<uint8_t*>(O.workspace);
-  uint32_t* ticket_ctr = reinterpret_cast<uint32_t*>(ws);
   uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
 
   if (t == 0) {
-    s.ticket = atomicAdd(ticket_ctr, 1u);
     s.status = PBL_OK;
     s.slow = 0;
   }
   __syncthreads();
-  const uint32_t b = s.ticket;
   const uint64_t boff = A.in.block_off[b];
   const uint32_t blen = A.in.block_len[b];
   const uint8_t* gblk = A.in.blocks + boff;
@@ -629,6 +609,32 @@ __global__ void __launch_bounds__(kTPB) rowblk_decode_kernel(Args A) {
 #endif
 }
 
+__global__ void __launch_bounds__(kTPB) rowblk_decode_kernel(Args A) {
+  __shared__ Lds s;
+  __shared__ uint32_t ticket;
+  if (threadIdx.x == 0) ticket = atomicAdd(reinterpret_cast<uint32_t*>(A.out.workspace), 1u);
+  __syncthreads();
+  row_block(s, A, ticket);
+}
+
+// Mixed row + colblk batch (config 4): per-block format from block_format[];
+// both paths share the ticket order and the look-back state.
+union MixedLds {
+  Lds row;
+  col::Lds col;
+};
+
+__global__ void __launch_bounds__(kTPB) mixed_decode_kernel(Args A) {
+  __shared__ MixedLds s;
+  __shared__ uint32_t ticket;
+  if (threadIdx.x == 0) ticket = atomicAdd(reinterpret_cast<uint32_t*>(A.out.workspace), 1u);
+  __syncthreads();
+  const uint32_t b = ticket;
+  const uint32_t fmt = A.in.block_format[b];
+  if (fmt == PBL_FMT_ROW) row_block(s.row, A, b);
+  else col::col_block(s.col, A, b, fmt);
+}
+
 __global__ void rebase_kernel(uint64_t* kvb, uint64_t* kb, uint64_t* vb, uint64_t* rb, uint32_t n,
                               uint64_t dkv, uint64_t dk, uint64_t dv, uint64_t dr) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -674,13 +680,16 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
       !out->val_off || !out->key_bytes || !out->val_bytes || !out->workspace ||
       out->workspace_bytes < pbl::ws_alloc_bytes(batch->n_blocks))
     return PBL_INVALID_ARG;
-  if (batch->format != PBL_FMT_ROW) return pbl_decode_batch_colblk(batch, out, stream);
+  if (!batch->block_format && batch->format != PBL_FMT_ROW) return pbl_decode_batch_colblk(batch, out, stream);
   if (hipMemsetAsync(out->workspace, 0, pbl::ws_bytes(batch->n_blocks), st) != hipSuccess)
     return PBL_DEVICE_ERROR;
-  pbl::row::Args a;
+  pbl::Args a;
   a.in = *batch;
   a.out = *out;
-  hipLaunchKernelGGL(pbl::row::rowblk_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
+  if (batch->block_format)
+    hipLaunchKernelGGL(pbl::row::mixed_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
+  else
+    hipLaunchKernelGGL(pbl::row::rowblk_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }
 

@@ -126,35 +126,4 @@ __device__ void slow_walk(const uint8_t* blk, uint64_t len, uint32_t flags, uint
   st->nr = uint64_t(nr);
 }
 
-// Per-block results and batch totals, written by lane 0 of wave 0.
-__device__ inline void write_block_meta(const pbl_decode_out& O, uint32_t b, uint32_t nb, uint32_t status,
-                                        const uint64_t excl[kNumComp], const uint64_t agg[kNumComp],
-                                        bool slow) {
-  O.blk_kv_base[b] = excl[0];
-  O.blk_key_base[b] = excl[1];
-  O.blk_val_base[b] = excl[2];
-  if (O.blk_rst_base) O.blk_rst_base[b] = excl[3];
-  O.blk_status[b] = status;
-  if (slow) atomicAdd(&O.totals->n_slow_blocks, 1u);
-  if (status != PBL_OK) {
-    atomicOr(&O.totals->status_mask, 1u << status);
-    atomicAdd(&O.totals->n_bad_blocks, 1u);
-  }
-  if (b == nb - 1) {
-    O.blk_kv_base[nb] = excl[0] + agg[0];
-    O.blk_key_base[nb] = excl[1] + agg[1];
-    O.blk_val_base[nb] = excl[2] + agg[2];
-    if (O.blk_rst_base) O.blk_rst_base[nb] = excl[3] + agg[3];
-    O.totals->n_kv = excl[0] + agg[0];
-    O.totals->key_bytes = excl[1] + agg[1];
-    O.totals->val_bytes = excl[2] + agg[2];
-    O.totals->n_restarts = excl[3] + agg[3];
-  }
-}
-
-__device__ inline bool overflows(const pbl_decode_out& O, const uint64_t excl[kNumComp],
-                                 const uint64_t agg[kNumComp]) {
-  return excl[0] + agg[0] > O.kv_cap || excl[1] + agg[1] > O.key_cap || excl[2] + agg[2] > O.val_cap ||
-         (O.restarts && excl[3] + agg[3] > O.rst_cap);
-}
 

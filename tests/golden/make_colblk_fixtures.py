@@ -1,0 +1,245 @@
+#!/usr/bin/env python3
+"""Columnar (colblk) golden fixtures, read as DATA from the reference's own
+datadriven test files (run in the container that has /root/reference; the GPU
+box only reads the generated tests/golden/colblk_golden.json).
+
+Every case is a whole serialized data block, recovered byte-for-byte from the
+`describe`/`finish`/`rewrite` hex dumps the reference's tests print
+(binfmt lines `NNN-MMM: x HEX` / `b BITS`), together with the KVs the
+reference's test wrote into that block:
+
+  sstable/colblk/testdata/data_block/*   DefaultKeySchema(testkeys.Comparer, bundle)
+        writer input:  `write` lines, parsed as data_block_test.go:76-109 does
+        (value-handle / blob-handle prefixes, obsolete marking, PrefixEqual)
+  cockroachkvs/testdata/block_encoding   cockroachkvs.KeySchema ("crdb1")
+        writer input:  the `init` lines; expected decode: the `keys` output
+        (cockroachkvs_test.go formatUserKey: `roachKey @ HEXVERSION #seq,KIND = value`)
+
+The expected per-row output is derived from the writer input alone (never from
+the dump), so a decoder that reproduces it from the dumped bytes is pinned to
+the reference's own encoder.
+"""
+from __future__ import annotations
+
+import ast
+import json
+import os
+import re
+import sys
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+KINDS = {"DEL": 0, "SET": 1, "MERGE": 2, "LOGDATA": 3, "SINGLEDEL": 7, "RANGEDEL": 15, "SEPARATOR": 17,
+         "SETWITHDEL": 18, "RANGEKEYDEL": 19, "RANGEKEYUNSET": 20, "RANGEKEYSET": 21, "INGESTSST": 22,
+         "DELSIZED": 23, "EXCISE": 24, "SYNTHETIC": 25, "INGESTSSTWITHBLOB": 26, "BDRY": 30, "INVALID": 191}
+# internal/base/internal.go:97-217 ; trailer = seq<<8 | kind (internal.go:279-314)
+SEQ_MAX = (1 << 56) - 1
+
+LINE = re.compile(r"(\d+)-(\d+): ([xb])((?: [0-9a-f]+)*)")
+
+
+def parse_datadriven(path: str):
+    sys.path.insert(0, HERE)
+    from make_fixtures import parse_datadriven as pdd  # same file format as the rowblk fixtures
+    lines = open(path).read().split("\n")
+    cases = pdd(path)
+    # attach source line numbers (first occurrence of each command line, in order)
+    pos = 0
+    for c in cases:
+        while pos < len(lines) and lines[pos] != c["cmd"]:
+            pos += 1
+        c["line"] = pos + 1
+        pos += 1
+    return cases
+
+
+def dump_to_bytes(text: str) -> bytes:
+    """Rebuild a block from binfmt lines; every byte must be covered exactly once."""
+    spans = []
+    for m in LINE.finditer(text):
+        a, b, kind, payload = int(m.group(1)), int(m.group(2)), m.group(3), m.group(4).replace(" ", "")
+        if kind == "x":
+            data = bytes.fromhex(payload)
+        else:
+            assert len(payload) % 8 == 0, payload
+            data = bytes(int(payload[i:i + 8], 2) for i in range(0, len(payload), 8))
+        assert len(data) == b - a, (a, b, payload)
+        spans.append((a, data))
+    n = max(a + len(d) for a, d in spans)
+    out = bytearray(n)
+    cov = bytearray(n)
+    for a, d in spans:
+        out[a:a + len(d)] = d
+        for i in range(a, a + len(d)):
+            cov[i] += 1
+    assert all(c == 1 for c in cov), "hex dump does not cover the block exactly once"
+    return bytes(out)
+
+
+def parse_ikey(s: str):
+    """base.ParseInternalKey (internal/base/internal.go:616-630)."""
+    i, j = s.index("#"), s.index(",")
+    seq = int(s[i + 1:j])
+    return s[:i].encode(), (seq << 8) | KINDS[s[j + 1:]]
+
+
+def testkeys_split(k: bytes) -> int:
+    """testkeys.Comparer.Split: prefix is everything before the first '@'."""
+    i = k.find(b"@")
+    return len(k) if i < 0 else i
+
+
+def default_schema_rows(write_lines):
+    """data_block_test.go:76-109 -> the rows the encoder saw."""
+    rows, prev_key, prev_kind = [], None, None
+    for line in write_lines:
+        obsolete = False
+        if line.endswith("obsolete"):
+            line, obsolete = line[: -len("obsolete")], True
+        j = line.index(":")
+        ukey, trailer = parse_ikey(line[:j])
+        value = line[j + 1:].encode()
+        prefix_equal = prev_key is not None and prev_key[:testkeys_split(prev_key)] == ukey[:testkeys_split(ukey)]
+        vp = None  # in place
+        if value.startswith(b"valueHandle"):
+            vp = 0x80 | (0x20 if prefix_equal else 0)   # block.ValueBlockHandlePrefix(prefixEqual, 0)
+        elif value.startswith(b"blobHandle"):
+            vp = 0x40 | (0x20 if prefix_equal else 0)   # block.BlobValueHandlePrefix(prefixEqual, 0)
+        if prev_key == ukey and prev_kind != 2:
+            obsolete = True
+        stored = value if vp is None else bytes([vp]) + value
+        rows.append({"key": ukey.hex(), "trailer": trailer, "value": stored.hex(), "raw_value": value.hex(),
+                     "vp": -1 if vp is None else vp, "external": vp is not None, "obsolete": obsolete,
+                     "prefix_changed": not prefix_equal, "prefix_len": testkeys_split(ukey)})
+        prev_key, prev_kind = ukey, trailer & 0xFF
+    return rows
+
+
+def data_block_cases():
+    out = []
+    d = os.path.join(REF, "sstable/colblk/testdata/data_block")
+    for fn in sorted(os.listdir(d)):
+        path = os.path.join(d, fn)
+        rel = os.path.relpath(path, REF)
+        bundle, written, finished = 16, [], None
+        for c in parse_datadriven(path):
+            cmd = c["cmd"].split()
+            if cmd[0] == "init":
+                bundle, written = 16, []
+                for a in cmd[1:]:
+                    if a.startswith("bundle-size="):
+                        bundle = int(a.split("=")[1])
+            elif cmd[0] == "write-block":
+                bundle, written, finished = 16, default_schema_rows([l for l in c["input"].split("\n") if l]), None
+            elif cmd[0] == "write":
+                written = written + [l for l in c["input"].split("\n") if l]
+            elif cmd[0] == "finish":
+                nrows = len(written)
+                for a in cmd[1:]:
+                    if a.startswith("rows="):
+                        nrows = int(a.split("=")[1])
+                all_rows = default_schema_rows(written)
+                rows = all_rows[:nrows]
+                blk = dump_to_bytes(c["expected"])
+                finished = (rows, blk)
+                out.append({"name": f"{fn}:{c['line']}", "source": f"{rel}:{c['line']}", "schema": "default",
+                            "bundle_size": bundle, "block": blk.hex(), "rows": rows, "encoder_exact": True,
+                            "writer_rows": all_rows, "finish_rows": nrows})
+            elif cmd[0] == "rewrite" and not c["expected"].startswith("error"):
+                frm = to = None
+                for a in cmd[1:]:
+                    if a.startswith("from="):
+                        frm = a.split("=", 1)[1].encode()
+                    if a.startswith("to="):
+                        to = a.split("=", 1)[1].encode()
+                rows = []
+                for r in finished[0]:
+                    k = bytes.fromhex(r["key"])
+                    p = testkeys_split(k)
+                    assert k[p:] == frm, (k, frm)
+                    rows.append(dict(r, key=(k[:p] + to).hex()))
+                blk = dump_to_bytes(c["expected"])
+                out.append({"name": f"{fn}:{c['line']}", "source": f"{rel}:{c['line']}", "schema": "default",
+                            "bundle_size": bundle, "block": blk.hex(), "rows": rows, "encoder_exact": False})
+    return out
+
+
+def go_unquote(s: str) -> bytes:
+    if s.startswith('"'):
+        return ast.literal_eval("b" + s)
+    return s.encode()
+
+
+def crdb_key(text: str):
+    """`roachKey [@ HEXVERSION] #seq,KIND = value` -> (user key, trailer, value)
+    (cockroachkvs_test.go parseUserKey / formatUserKey; cockroachkvs.go:140-309)."""
+    kpart, value = text.split(" = ", 1)
+    kpart, ik = kpart.rsplit(" #", 1)
+    seq, kind = ik.split(",")
+    if " @ " in kpart:
+        roach, ver = kpart.split(" @ ")
+        ver = bytes.fromhex(ver)
+    else:
+        roach, ver = kpart, b""
+    key = go_unquote(roach.strip()) + b"\x00"
+    if ver:
+        key += ver + bytes([len(ver) + 1])
+    return key, (int(seq) << 8) | KINDS[kind], value.encode()
+
+
+def crdb1_cases():
+    path = os.path.join(REF, "cockroachkvs/testdata/block_encoding")
+    rel = os.path.relpath(path, REF)
+    cases = parse_datadriven(path)
+    init = next(c for c in cases if c["cmd"].startswith("init"))
+    keys = next(c for c in cases if c["cmd"].startswith("keys"))
+    desc = next(c for c in cases if c["cmd"].startswith("describe"))
+    inp = [crdb_key(l) for l in init["input"].split("\n") if l]
+    exp = [crdb_key(l) for l in keys["expected"].split("\n") if l]
+    assert len(inp) == len(exp)
+    rows, prev = [], None
+    for (ik, it, iv), (ek, et, ev) in zip(inp, exp):
+        assert it == et and iv == ev
+        roach_len = len(ik) - (ik[-1] if ik[-1] != 0 else 0)  # roach key + sentinel
+        pc = prev is None or prev != ik[:roach_len]
+        rows.append({"key": ek.hex(), "in_key": ik.hex(), "trailer": et, "value": ev.hex(), "raw_value": iv.hex(),
+                     "vp": -1, "external": False, "obsolete": False, "prefix_changed": pc, "prefix_len": roach_len})
+        prev = ik[:roach_len]
+    blk = dump_to_bytes(desc["expected"])
+    return [{"name": f"block_encoding:{desc['line']}", "source": f"{rel}:{init['line']}-{desc['line']}",
+             "schema": "crdb1", "bundle_size": 16, "block": blk.hex(), "rows": rows, "encoder_exact": True,
+             "writer_rows": [dict(r, key=r["in_key"]) for r in rows], "finish_rows": len(rows)}]
+
+
+def codec_cases():
+    """Per-codec dumps (uints, raw_bytes, prefix_bytes, bitmap) are recorded
+    verbatim so codec decoders can be pinned individually."""
+    out = {}
+    for fn in ("uints", "raw_bytes", "prefix_bytes", "bitmap"):
+        path = os.path.join(REF, "sstable/colblk/testdata", fn)
+        rel = os.path.relpath(path, REF)
+        lst = []
+        for c in parse_datadriven(path):
+            if LINE.search(c["expected"]) and not c["expected"].startswith("error"):
+                try:
+                    blk = dump_to_bytes(c["expected"])
+                except AssertionError:
+                    continue
+                lst.append({"source": f"{rel}:{c['line']}", "cmd": c["cmd"], "input": c["input"],
+                            "bytes": blk.hex(), "dump": c["expected"]})
+        out[fn] = lst
+    return out
+
+
+def main():
+    cases = data_block_cases() + crdb1_cases()
+    res = {"data_blocks": cases, "codecs": codec_cases()}
+    p = os.path.join(HERE, "colblk_golden.json")
+    with open(p, "w") as f:
+        json.dump(res, f, indent=1)
+    print("wrote", p, len(cases), "data blocks,", {k: len(v) for k, v in res["codecs"].items()}, "codec dumps")
+
+
+if __name__ == "__main__":
+    main()
