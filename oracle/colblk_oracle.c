@@ -309,24 +309,81 @@ int orc_colblk_decode(const uint8_t* blk, uint64_t len, uint32_t schema, orc_blo
   return OK;
 }
 
-/* Iterate-only CPU baseline for colblk (SURVEY.md §8(d) mode i): key into a
- * reused buffer, value zero-copy, folded into a checksum. */
+/* Iterate-only CPU baseline for colblk (SURVEY.md §8(d) mode i), shaped like
+ * DataBlockIter.First/Next: PrefixBytes.SetNext keeps the shared + bundle prefix
+ * in a reused key buffer and copies only a row's suffix (prefix_bytes.go:303-356),
+ * the version is appended per MaterializeUserKey, the value is zero-copy; all of
+ * it folded into a checksum.  Typed loads of the column widths (no byte loops). */
+static inline uint64_t u_fast(const uint8_t* b, const ucol* u, uint32_t i) {
+  const uint8_t* p = b + u->at;
+  switch (u->w) {
+    case 0: return u->base;
+    case 1: return u->base + p[i];
+    case 2: { uint16_t v; memcpy(&v, p + 2ull * i, 2); return u->base + v; }
+    case 4: { uint32_t v; memcpy(&v, p + 4ull * i, 4); return u->base + v; }
+    default: { uint64_t v; memcpy(&v, p + 8ull * i, 8); return v; }
+  }
+}
+
 uint64_t orc_colblk_scan_checksum(const uint8_t* blk, uint64_t len, uint32_t schema, uint64_t* n_kv) {
   coldec c;
   *n_kv = 0;
   if (!init_decoder(blk, len, schema, &c)) return 0;
   uint8_t key[4096];
+  const uint8_t* pdata = blk + c.keys.rb.data;
+  const uint32_t shift = c.keys.shift, rows = c.d.rows;
+  if (c.shared_len > sizeof(key) / 2) return 0;
+  memcpy(key, pdata, c.shared_len);
+  uint32_t pre = c.shared_len;  /* shared + bundle prefix length in key[] */
+  uint32_t klen = pre;          /* roach key / prefix length */
   uint64_t h = 1469598103934665603ull;
-  for (uint32_t r = 0; r < c.d.rows; r++) {
-    int64_t kl = materialize(&c, r, NULL);
-    if (kl < 0 || kl > (int64_t)sizeof(key)) return 0;
-    materialize(&c, r, key);
-    uint64_t lo, hi;
-    if (!rb_slice(&c, &c.values, r, &lo, &hi)) return 0;
-    uint64_t tr = u_at(&c.d, &c.trailers, r);
-    h = (h ^ tr ^ key[kl ? kl - 1 : 0] ^ (hi > lo ? blk[lo] : 0) ^ (hi - lo)) * 1099511628211ull;
+  for (uint32_t r = 0; r < rows; r++) {
+    if ((r & ((1u << shift) - 1)) == 0) { /* bundle start: bundle prefix */
+      uint32_t bi = (r >> shift) + r;
+      uint32_t a = (uint32_t)u_fast(blk, &c.keys.rb.off, bi), z = (uint32_t)u_fast(blk, &c.keys.rb.off, bi + 1);
+      if (z < a || c.shared_len + (z - a) > sizeof(key) / 2) return 0;
+      memcpy(key + c.shared_len, pdata + a, z - a);
+      pre = c.shared_len + (z - a);
+      klen = pre;
+    }
+    uint32_t si = 1 + (r >> shift) + r;
+    uint32_t lo = (uint32_t)u_fast(blk, &c.keys.rb.off, si), hi = (uint32_t)u_fast(blk, &c.keys.rb.off, si + 1);
+    if (hi > lo) { /* SetNext: an empty suffix keeps the previous key */
+      if (pre + (hi - lo) > sizeof(key) / 2) return 0;
+      memcpy(key + pre, pdata + lo, hi - lo);
+      klen = pre + (hi - lo);
+    }
+    uint32_t n = klen;
+    if (schema == FMT_COL_CRDB1) {
+      uint64_t wall = u_fast(blk, &c.wall, r);
+      uint32_t logical = (uint32_t)u_fast(blk, &c.logical, r);
+      key[n++] = 0;
+      if (wall == 0 && logical == 0) {
+        uint32_t x = (uint32_t)u_fast(blk, &c.untyped.off, r), y = (uint32_t)u_fast(blk, &c.untyped.off, r + 1);
+        if (y > x) {
+          if (n + (y - x) + 1 > sizeof(key)) return 0;
+          memcpy(key + n, blk + c.untyped.data + x, y - x);
+          n += y - x;
+          key[n++] = (uint8_t)(y - x + 1);
+        }
+      } else {
+        uint64_t be = __builtin_bswap64(wall);
+        memcpy(key + n, &be, 8);
+        n += 8;
+        if (logical == 0) key[n++] = 9;
+        else { uint32_t bl = __builtin_bswap32(logical); memcpy(key + n, &bl, 4); n += 4; key[n++] = 13; }
+      }
+    } else {
+      uint32_t x = (uint32_t)u_fast(blk, &c.suffixes.off, r), y = (uint32_t)u_fast(blk, &c.suffixes.off, r + 1);
+      if (y < x || n + (y - x) > sizeof(key)) return 0;
+      memcpy(key + n, blk + c.suffixes.data + x, y - x);
+      n += y - x;
+    }
+    uint32_t vlo = (uint32_t)u_fast(blk, &c.values.off, r), vhi = (uint32_t)u_fast(blk, &c.values.off, r + 1);
+    uint64_t tr = u_fast(blk, &c.trailers, r);
+    h = (h ^ tr ^ key[n ? n - 1 : 0] ^ (vhi > vlo ? blk[c.values.data + vlo] : 0) ^ (vhi - vlo)) * 1099511628211ull;
   }
-  *n_kv = c.d.rows;
+  *n_kv = rows;
   return h;
 }
 

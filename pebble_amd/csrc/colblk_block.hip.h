@@ -40,7 +40,6 @@ enum { kDtBool = 1, kDtUint = 2, kDtBytes = 3, kDtPrefix = 4 };
 using lds_cu8 = __attribute__((address_space(3))) const uint8_t*;
 using lds_u8 = __attribute__((address_space(3))) uint8_t*;
 using lds_cu32 = __attribute__((address_space(3))) const uint32_t*;
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 using lds_u4 = __attribute__((address_space(3))) u32x4*;
 using glb_cu8 = __attribute__((address_space(1))) const uint8_t*;
 template <class T>

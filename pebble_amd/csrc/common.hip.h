@@ -9,6 +9,8 @@
 
 namespace pbl {
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // native 16-B vector
+
 constexpr int kTPB = 256;   // threads per workgroup (4 waves); one workgroup per block
 constexpr int kWave = 64;
 constexpr int kNumComp = 4; // look-back components: n_kv, key bytes, value bytes, restarts
@@ -126,7 +128,7 @@ __device__ inline void lb_resolve(uint64_t* st, uint32_t n_blocks, uint32_t v, c
         int64_t idx = top[c] - kWave * k - l;
         g[c][k] = (!done[c] && idx >= 0) ? ld_agent(st + uint64_t(c) * n_blocks + idx) : kStatePfx;
       }
-    bool waited = false;
+    int64_t wait_word = -1;  // a word that was not ready yet
 #pragma unroll
     for (int c = 0; c < kNumComp; c++) {
       bool stop = done[c];
@@ -138,18 +140,31 @@ __device__ inline void lb_resolve(uint64_t* st, uint32_t n_blocks, uint32_t v, c
         uint64_t notready = __ballot(state == 0);
         int first = pfx ? __builtin_ctzll(pfx) : 64;
         uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
-        if (notready & need) { waited = true; stop = true; continue; }
+        if (notready & need) {
+          if (wait_word < 0)
+            wait_word = int64_t(c) * n_blocks + (top[c] - kWave * k - __builtin_ctzll(notready & need));
+          stop = true;
+          continue;
+        }
         acc[c] += wave_sum((l <= first) ? (g[c][k] & kValMask) : 0ull);
         if (first < 64) { done[c] = true; stop = true; }
         else top[c] -= kWave;
       }
     }
-    if (waited) {
-      if (++spins > (1u << 24)) {
+    if (wait_word >= 0) {
+      // Poll the missing predecessor from ONE lane (a whole-window re-read per
+      // poll would flood this CU's memory queue), then re-read the window.
+      bool timed_out = false;
+      if (l == 0) {
+        while ((ld_agent(st + wait_word) >> 62) == 0) {
+          if (++spins > (1u << 22)) { timed_out = true; break; }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      if (__shfl(timed_out ? 1 : 0, 0, kWave)) {
         if (l == 0) atomicOr(timeout_flag, 1u << PBL_TIMEOUT);
         break;
       }
-      __builtin_amdgcn_s_sleep(1);
     }
   }
 #pragma unroll

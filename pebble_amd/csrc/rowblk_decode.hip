@@ -45,12 +45,12 @@ constexpr uint64_t kKindInvalid = 191u;
 constexpr int kSlotPos = 0;                          // [kKvCap] entry offset of slot q
 constexpr int kSlotCk = kSlotPos + kKvCap;           // [kKvCap] in-run user-key prefix of slot q
 constexpr int kSlotCv = kSlotCk + kKvCap;            // [kKvCap] in-run value prefix of slot q
-constexpr int kRunKv0 = kSlotCv + kKvCap;            // [kRunCap+1] first KV of run r
+constexpr int kSlotSh = kSlotCv + kKvCap;            // [kKvCap] shared length of slot q
+constexpr int kSlotPar = kSlotSh + kKvCap;           // [kKvCap] in-run index of slot q's prefix parent
+constexpr int kRunKv0 = kSlotPar + kKvCap;           // [kRunCap+1] first KV of run r
 constexpr int kRunKb0 = kRunKv0 + kRunCap + 1;       // [kRunCap+1] key-byte offset of run r
 constexpr int kRunVb0 = kRunKb0 + kRunCap + 1;       // [kRunCap+1] value-byte offset of run r
-constexpr int kKBkt = kRunVb0 + kRunCap + 1;         // [65536/kBkt+1] KV holding key byte b*kBkt
-constexpr int kVBkt = kKBkt + 65536 / kBkt + 1;      // [32768/kBkt+1] KV holding value byte b*kBkt
-constexpr int kAuxWords = (kVBkt + 32768 / kBkt + 1 + 7) & ~7;
+constexpr int kAuxWords = (kRunVb0 + kRunCap + 1 + 7) & ~7;
 
 struct Lds {
   uint4 blk4[kLdsBlkBytes / 16];  // block byte i at byte kPad+shift+i
@@ -67,8 +67,11 @@ struct Lds {
   uint16_t aux[kAuxWords];
   uint32_t scratch[16];
   uint64_t bases[kNumComp];
-  uint32_t ticket, status, slow, nkv, nres, S, shift, tot_kb, tot_vb;
+  uint32_t status, slow, nkv, nres, S, shift, tot_kb, tot_vb;
   int32_t roff;
+  // persistent kernel: tickets / descriptors of the next blocks
+  uint32_t nxt, n2, n2_len, nxt_len;
+  uint64_t n2_off, nxt_off;
 };
 
 // 16 bytes at LDS byte address a (any alignment): five dword reads + alignbyte
@@ -216,6 +219,31 @@ __device__ inline void block_excl_scan3(uint32_t a, uint32_t b, uint32_t c, uint
 
 #include "rowblk_general.hip.h"
 
+// Store bytes [lo, hi) of the 16-byte granule w to p[lo..hi) (p 16-B aligned)
+// with the fewest naturally aligned byte/short/dword/qword stores.
+__device__ __forceinline__ uint32_t granule_dword(const uint4& w, uint32_t k) {
+  return k == 0 ? w.x : k == 1 ? w.y : k == 2 ? w.z : w.w;
+}
+__device__ __forceinline__ void store_partial16(uint8_t* p, const uint4& w, uint32_t lo, uint32_t hi) {
+  uint32_t x = lo;
+  while (x < hi) {
+    const uint32_t d = granule_dword(w, x >> 2);
+    if ((x & 1) || hi - x < 2) {
+      p[x] = uint8_t(d >> (8 * (x & 3)));
+      x += 1;
+    } else if ((x & 3) || hi - x < 4) {
+      *reinterpret_cast<uint16_t*>(p + x) = uint16_t(d >> (8 * (x & 3)));
+      x += 2;
+    } else if ((x & 7) || hi - x < 8) {
+      *reinterpret_cast<uint32_t*>(p + x) = d;
+      x += 4;
+    } else {
+      *reinterpret_cast<uint2*>(p + x) = make_uint2(d, granule_dword(w, (x >> 2) + 1));
+      x += 8;
+    }
+  }
+}
+
 // P1 for run r: walk entries, park offsets and in-run output prefixes in the
 // slots of run r, return (count, user-key bytes, value bytes).  `ok` clears when
 // the run does not end exactly at the next restart (general path).
@@ -224,7 +252,7 @@ __device__ inline void walk_run(Lds& s, const View& V, uint32_t r, uint32_t nres
   uint32_t st = roff + 4 * r;
   uint32_t s0 = V.le32(st) & kRestartMask;
   uint32_t e0 = (r + 1 < nres) ? (V.le32(st + 4) & kRestartMask) : roff;
-  uint32_t cnt = 0, kb = 0, vb = 0, prev_kl = 0;
+  uint32_t cnt = 0, kb = 0, vb = 0, prev_kl = 0, prev_sh = 0, pp = 0, ppsh = 0;
   bool ok = (r != 0 || s0 == 0) && s0 < e0 && e0 <= roff;
   uint32_t pos = s0;
   while (ok && pos < e0) {
@@ -239,6 +267,26 @@ __device__ inline void walk_run(Lds& s, const View& V, uint32_t r, uint32_t nres
     s.aux[kSlotPos + q] = uint16_t(pos);
     s.aux[kSlotCk + q] = uint16_t(kb);
     s.aux[kSlotCv + q] = uint16_t(vb);
+    s.aux[kSlotSh + q] = uint16_t(sh);
+    // prefix parent = nearest earlier entry of the run with a smaller shared
+    // length (all-nearest-smaller-values walk over the parents: amortised O(1))
+    // The previous entry and its parent are kept in registers; deeper steps
+    // read the parked slots.
+    uint32_t par = cnt, parsh = 0;
+    if (sh != 0) {
+      uint32_t c = cnt - 1, csh = prev_sh;
+      if (csh >= sh) { c = pp; csh = ppsh; }
+      while (csh >= sh) {
+        c = s.aux[kSlotPar + r * S + c];
+        csh = s.aux[kSlotSh + r * S + c];
+      }
+      par = c;
+      parsh = csh;
+    }
+    s.aux[kSlotPar + q] = uint16_t(par);
+    prev_sh = sh;
+    pp = par;
+    ppsh = parsh;
     uint32_t kl = sh + un;
     kb += (flags & PBL_ROW_RAW_KEYS) ? kl : (kl >= 8 ? kl - 8 : 0);
     vb += vl;
@@ -262,7 +310,6 @@ __device__ inline void expand_slot(Lds& s, const View& V, uint32_t q, uint32_t S
   uint32_t pos = s.aux[kSlotPos + q], sh, un, vl;
   uint32_t h = entry_header(V, pos, roff, &sh, &un, &vl);
   uint32_t kl = sh + un;
-  uint32_t ukl = (flags & PBL_ROW_RAW_KEYS) ? kl : (kl >= 8 ? kl - 8 : 0);
   uint32_t ko = uint32_t(s.aux[kRunKb0 + r]) + s.aux[kSlotCk + q];
   uint32_t vo = uint32_t(s.aux[kRunVb0 + r]) + s.aux[kSlotCv + q];
   s.eoff[j] = uint16_t(pos);
@@ -276,79 +323,35 @@ __device__ inline void expand_slot(Lds& s, const View& V, uint32_t q, uint32_t S
   uint8_t fl = (!(flags & PBL_ROW_RAW_KEYS) && kl < 8) ? uint8_t(PBL_KV_INVALID_KEY) : uint8_t(0);
   if (k == 0) fl |= uint8_t(PBL_KV_RESTART | ((V.le32(roff + 4 * r) >> 31) ? PBL_KV_RESTART_SAMEPFX : 0));
   s.kvf[j] = fl;
-  // prefix parent: the nearest earlier entry of the run whose own bytes start
-  // below shared_j (entries in between contribute nothing to key j's prefix).
-  // Scanned through the run's parked slots, so no other thread's output is read.
-  {
-    uint32_t pj = j;
-    if (sh != 0) {
-      for (int kk = int(k) - 1; kk >= 0; kk--) {
-        uint32_t pq = r * S + uint32_t(kk);
-        uint32_t ppos = s.aux[kSlotPos + pq], psh;
-        // shared length of the parked entry: its first varint
-        uint32_t b0 = V.byte(ppos);
-        if (b0 < 128) psh = b0;
-        else { uint32_t un2, vl2; entry_header(V, ppos, roff, &psh, &un2, &vl2); }
-        if (psh < sh) { pj = kv0 + uint32_t(kk); break; }
-      }
-    }
-    s.par[j] = uint16_t(pj);
-  }
+  // prefix parent (computed in P1): the nearest earlier entry of the run whose
+  // own bytes start below shared_j; entries in between contribute nothing.
+  s.par[j] = uint16_t(sh != 0 ? kv0 + s.aux[kSlotPar + q] : j);
   // bucket b (bytes [b*kBkt, ...)) belongs to the KV that holds its first byte
-  for (uint32_t bk = (ko + kBkt - 1) / kBkt; bk * kBkt < ko + ukl; bk++) s.aux[kKBkt + bk] = uint16_t(j);
-  for (uint32_t bk = (vo + kBkt - 1) / kBkt; bk * kBkt < vo + vl; bk++) s.aux[kVBkt + bk] = uint16_t(j);
 }
 
-// One 16-byte key granule: user-key bytes [o, o1) (block relative) land at
-// granule bytes [q, ...).  Each key is the concatenation of its prefix-chain
-// segments: [shared_i, cur) of entry i, walking i = j, j-1, ... (rowblk_iter.go:403
-// unrolled backwards); every segment is one LDS gather merged under a mask.
-__device__ inline uint4 key_granule(const Lds& s, const View& V, uint32_t o, uint32_t o1, uint32_t q,
-                                    uint32_t nkv) {
-  int j = s.aux[kKBkt + o / kBkt];
+// Bytes [p_lo, p_hi) of the user key of KV j (length klen), placed at bytes
+// [q, ...) of a 16-byte granule.  The key is the concatenation of its prefix-
+// chain segments: [shared_i, cur) of entry i, walking i = j, par[j], ...
+// (rowblk_iter.go:403 unrolled backwards); each segment is one LDS gather
+// merged under a byte mask.
+__device__ __forceinline__ uint4 key_part(const Lds& s, const View& V, int j, uint32_t klen, uint32_t p_lo,
+                                          uint32_t p_hi, uint32_t q) {
   uint4 w = make_uint4(0, 0, 0, 0);
-  while (o < o1) {
-    while (s.kout[j + 1] <= o) j++;
-    uint32_t k0 = s.kout[j], k1 = s.kout[j + 1];
-    uint32_t p_lo = o - k0, p_hi = (o1 < k1 ? o1 : k1) - k0;
-    uint32_t cur = k1 - k0;  // user-key length
-    int i = j;
-    // contributing entries only: j, then prefix parents (par[] skips entries
-    // whose own bytes start at or above the current prefix length)
-    while (cur > p_lo) {
-      uint32_t shi = s.sh[i];
-      uint32_t lo_i = shi < cur ? shi : cur;
-      uint32_t a = lo_i > p_lo ? lo_i : p_lo, z = cur < p_hi ? cur : p_hi;
-      if (a < z) {
-        uint32_t gq = q + (a - p_lo);
-        int32_t src = int32_t(s.ksrc[i]) - int32_t(shi) + int32_t(a);  // block offset of key byte a
-        uint4 v = V.ld16(src - int32_t(gq));
-        if (gq == 0 && z - a == 16) w = v;
-        else merge16(w, v, gq, gq + (z - a));
-      }
-      cur = lo_i;
-      i = s.par[i];
+  uint32_t cur = klen;
+  int i = j;
+  while (cur > p_lo) {
+    const uint32_t shi = s.sh[i];
+    const uint32_t lo_i = shi < cur ? shi : cur;
+    const uint32_t a = lo_i > p_lo ? lo_i : p_lo, z = cur < p_hi ? cur : p_hi;
+    if (a < z) {
+      const uint32_t gq = q + (a - p_lo);
+      const int32_t src = int32_t(s.ksrc[i]) - int32_t(shi) + int32_t(a);  // block offset of key byte a
+      const uint4 v = V.ld16(src - int32_t(gq));
+      if (gq == 0 && z - a == 16) w = v;
+      else merge16(w, v, gq, gq + (z - a));
     }
-    q += p_hi - p_lo;
-    o += p_hi - p_lo;
-  }
-  (void)nkv;
-  return w;
-}
-
-// One 16-byte value granule: value bytes [o, o1) land at granule bytes [q, ...).
-__device__ inline uint4 val_granule(const Lds& s, const View& V, uint32_t o, uint32_t o1, uint32_t q) {
-  int j = s.aux[kVBkt + o / kBkt];
-  uint4 w = make_uint4(0, 0, 0, 0);
-  while (o < o1) {
-    while (s.vout[j + 1] <= o) j++;
-    uint32_t e = o1 < s.vout[j + 1] ? o1 : s.vout[j + 1];
-    int32_t src = int32_t(s.vsrc[j] + (o - s.vout[j]));
-    uint4 v = V.ld16(src - int32_t(q));
-    if (q == 0 && e - o == 16) w = v;
-    else merge16(w, v, q, q + (e - o));
-    q += e - o;
-    o = e;
+    cur = lo_i;
+    i = s.par[i];
   }
   return w;
 }
@@ -356,8 +359,132 @@ __device__ inline uint4 val_granule(const Lds& s, const View& V, uint32_t o, uin
 // ---------------------------------------------------------------------------
 // The decode kernel.
 // ---------------------------------------------------------------------------
-// Decode row block b (the caller has taken ticket b).
-__device__ __forceinline__ void row_block(Lds& s, const Args& A, const uint32_t b) {
+// Init checks of one row block (Init :248-256, readFirstKey :418-485) read
+// through `rd` (LDS when staged, else global).  Thread 0 only.
+template <class Rd>
+__device__ __forceinline__ void row_init(Lds& s, const Rd& rd, uint32_t blen, uint32_t flags, bool fits) {
+  uint32_t st = PBL_OK;
+  int64_t roff = 0;
+  int32_t nr = 0;
+  if (blen < 4) st = PBL_CORRUPT_BOUNDS;
+  else {
+    nr = int32_t(rd.le32(blen - 4));
+    if (nr == 0) st = PBL_CORRUPT_NO_RESTARTS;
+    else if (nr < 0) st = PBL_CORRUPT_BOUNDS;
+    else {
+      roff = int64_t(blen) - 4 * (1 + int64_t(nr));
+      if (roff < 0) st = PBL_CORRUPT_BOUNDS;
+      else if (roff > 0 && !(flags & PBL_ROW_RAW_KEYS)) {
+        if (rd.byte(0) != 0) st = PBL_CORRUPT_FIRST_KEY;
+        else {
+          uint32_t un, vl;
+          uint32_t n1 = rd.varint(1, blen, &un);
+          uint32_t n2 = n1 ? rd.varint(1 + n1, blen, &vl) : 0;
+          if (!n2) st = PBL_CORRUPT_BOUNDS;
+          else if (un < 8) st = PBL_CORRUPT_FIRST_KEY;
+        }
+      }
+    }
+  }
+  s.status = st;
+  s.roff = int32_t(roff);
+  s.nres = (st == PBL_OK) ? uint32_t(nr) : 0;
+  s.S = (st == PBL_OK && nr > 0) ? uint32_t(kKvCap) / uint32_t(nr) : 1;
+  s.slow = (st == PBL_OK && (!fits || uint32_t(nr) > uint32_t(kRunCap))) ? 1u : 0u;
+  s.nkv = 0;
+  s.tot_kb = s.tot_vb = 0;
+  s.kout[0] = s.vout[0] = 0;
+}
+
+struct LdsRd {  // staged block through the View
+  View V;
+  __device__ uint32_t byte(uint32_t i) const { return V.byte(i); }
+  __device__ uint32_t le32(uint32_t i) const { return V.le32(i); }
+  __device__ uint32_t varint(uint32_t p, uint32_t end, uint32_t* v) const { return lds_varint(V, p, end, v); }
+};
+struct GlbRd {  // unstaged block in global memory
+  const uint8_t* g;
+  __device__ uint32_t byte(uint32_t i) const { return g[i]; }
+  __device__ uint32_t le32(uint32_t i) const { return g_le32(g + i); }
+  __device__ uint32_t varint(uint32_t p, uint32_t end, uint32_t* v) const { return g_varint(g + p, g + end, v); }
+};
+
+// Stage block bytes from global memory into LDS (granule g of the 16-B aligned
+// source lands at blk4[1 + g]).
+__device__ __forceinline__ void row_stage(Lds& s, const uint8_t* blocks, uint64_t boff, uint32_t blen) {
+  const uint64_t a0 = boff & ~uint64_t(15);
+  const uint64_t a1 = (boff + blen + 15) & ~uint64_t(15);
+  const uint4* src = reinterpret_cast<const uint4*>(blocks + a0);
+  const uint32_t n16 = uint32_t((a1 - a0) >> 4);
+  for (uint32_t g = threadIdx.x; g < n16; g += kTPB) s.blk4[1 + g] = src[g];
+}
+
+constexpr int kPfWaves = kTPB / kWave - 1;                  // waves 1-3 prefetch
+constexpr int kPfThreads = kPfWaves * kWave;                // 192
+constexpr int kPfRegs = (kLdsBlkBytes / 16 + kPfThreads - 1) / kPfThreads;  // 11 granules / lane
+static_assert(kPfRegs == 11, "PBL_PF_LIST");
+// 11 named granule registers per prefetching lane (an array ends up in scratch:
+// it is live across the whole decode of the current block).
+#define PBL_PF_LIST(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10)
+
+// The next block, held in registers by waves 1-3 while the current one decodes.
+struct PfRegs {
+#define PBL_PF_DECL(i) u32x4 r##i;
+  PBL_PF_LIST(PBL_PF_DECL)
+#undef PBL_PF_DECL
+  // load the block at [off, off+len) (clamped: lanes past the end re-read the
+  // last granule instead of running off the block)
+  __device__ __forceinline__ void load(const uint8_t* blocks, uint64_t off, uint32_t len) {
+    const uint64_t a0 = off & ~uint64_t(15);
+    const uint32_t n16 = uint32_t((((off + len + 15) & ~uint64_t(15)) - a0) >> 4);
+    if (n16 == 0) return;
+    const u32x4* src = reinterpret_cast<const u32x4*>(blocks + a0);
+    const uint32_t l = threadIdx.x - kWave;
+#define PBL_PF_LOAD(i)                                               \
+    {                                                                \
+      const uint32_t g = l + uint32_t(i) * kPfThreads;               \
+      r##i = src[g < n16 ? g : n16 - 1];                             \
+    }
+    PBL_PF_LIST(PBL_PF_LOAD)
+#undef PBL_PF_LOAD
+  }
+  __device__ __forceinline__ void store(Lds& s, uint64_t off, uint32_t len) const {
+    const uint64_t a0 = off & ~uint64_t(15);
+    const uint32_t n16 = uint32_t((((off + len + 15) & ~uint64_t(15)) - a0) >> 4);
+    const uint32_t l = threadIdx.x - kWave;
+#define PBL_PF_STORE(i)                                              \
+    {                                                                \
+      const uint32_t g = l + uint32_t(i) * kPfThreads;               \
+      if (g < n16) reinterpret_cast<u32x4*>(s.blk4)[1 + g] = r##i;   \
+    }
+    PBL_PF_LIST(PBL_PF_STORE)
+#undef PBL_PF_STORE
+  }
+};
+
+// Persistent kernel hooks (wave 0 lane 0): take the next ticket right after
+// this block publishes its aggregate, and publish the next block's descriptor
+// once the look-back has resolved, so the next block starts decoding right
+// after this one's outputs: ticket order stays ~= processing order.
+__device__ __forceinline__ void next_descriptor(Lds& s, const Args& A, uint32_t tk) {
+  s.nxt = tk;
+  if (tk < A.in.n_blocks) {
+    s.nxt_off = A.in.block_off[tk];
+    s.nxt_len = A.in.block_len[tk];
+  }
+}
+// waves 1-3: start loading the next block into registers
+__device__ __forceinline__ void next_prefetch(Lds& s, const Args& A, bool persist, PfRegs& pf) {
+  if (persist && threadIdx.x >= kWave) {
+    const uint32_t n = s.nxt;
+    if (n < A.in.n_blocks && s.nxt_len <= kMaxFastLen) pf.load(A.in.blocks, s.nxt_off, s.nxt_len);
+  }
+}
+
+// Decode row block b whose bytes are staged in LDS (when blen <= kMaxFastLen).
+// `persist`: persistent mode (ticket for the next block + its prefetch into pf).
+__device__ __forceinline__ void row_process(Lds& s, const Args& A, const uint32_t b, const uint64_t boff,
+                                            const uint32_t blen, const bool persist, PfRegs& pf) {
   const int t = threadIdx.x;
   const pbl_decode_out& O = A.out;
   const uint32_t nb = A.in.n_blocks;
@@ -365,62 +492,15 @@ __device__ __forceinline__ void row_block(Lds& s, const Args& A, const uint32_t 
   const bool vprefix = (flags & PBL_ROW_VALUE_PREFIX) && !(flags & PBL_ROW_RAW_KEYS);
   uint8_t* ws = reinterpret_cast<uint8_t*>(O.workspace);
   uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
-
-  if (t == 0) {
-    s.status = PBL_OK;
-    s.slow = 0;
-  }
-  __syncthreads();
-  const uint64_t boff = A.in.block_off[b];
-  const uint32_t blen = A.in.block_len[b];
   const uint8_t* gblk = A.in.blocks + boff;
-  STAMP(0);
-
-  // ---- stage the block into LDS (16-byte coalesced loads) --------------------
-  const uint64_t a0 = boff & ~uint64_t(15);
-  const uint64_t a1 = (boff + blen + 15) & ~uint64_t(15);
   const bool fits = blen <= kMaxFastLen;
-  if (fits) {
-    const uint4* src = reinterpret_cast<const uint4*>(A.in.blocks + a0);
-    const uint32_t n16 = uint32_t((a1 - a0) >> 4);
-    for (uint32_t g = t; g < n16; g += kTPB) s.blk4[1 + g] = src[g];
-  }
+  STAMP(0);
   const View V{reinterpret_cast<const uint8_t*>(s.blk4), reinterpret_cast<const uint32_t*>(s.blk4),
                uint32_t(kPad + (boff & 15))};
   if (t == 0) {
     s.shift = uint32_t(boff & 15);
-    // Init :248-256, readFirstKey :418-485 (cheap scalar checks from global)
-    uint32_t st = PBL_OK;
-    int64_t roff = 0;
-    int32_t nr = 0;
-    if (blen < 4) st = PBL_CORRUPT_BOUNDS;
-    else {
-      nr = int32_t(g_le32(gblk + blen - 4));
-      if (nr == 0) st = PBL_CORRUPT_NO_RESTARTS;
-      else if (nr < 0) st = PBL_CORRUPT_BOUNDS;
-      else {
-        roff = int64_t(blen) - 4 * (1 + int64_t(nr));
-        if (roff < 0) st = PBL_CORRUPT_BOUNDS;
-        else if (roff > 0 && !(flags & PBL_ROW_RAW_KEYS)) {
-          if (gblk[0] != 0) st = PBL_CORRUPT_FIRST_KEY;
-          else {
-            uint32_t un, vl;
-            uint32_t n1 = g_varint(gblk + 1, gblk + blen, &un);
-            uint32_t n2 = n1 ? g_varint(gblk + 1 + n1, gblk + blen, &vl) : 0;
-            if (!n2) st = PBL_CORRUPT_BOUNDS;
-            else if (un < 8) st = PBL_CORRUPT_FIRST_KEY;
-          }
-        }
-      }
-    }
-    s.status = st;
-    s.roff = int32_t(roff);
-    s.nres = (st == PBL_OK) ? uint32_t(nr) : 0;
-    s.S = (st == PBL_OK && nr > 0) ? uint32_t(kKvCap) / uint32_t(nr) : 1;
-    s.slow = (st == PBL_OK && (!fits || uint32_t(nr) > uint32_t(kRunCap))) ? 1u : 0u;
-    s.nkv = 0;
-    s.tot_kb = s.tot_vb = 0;
-    s.kout[0] = s.vout[0] = 0;
+    if (fits) row_init(s, LdsRd{V}, blen, flags, true);
+    else row_init(s, GlbRd{gblk}, blen, flags, false);
   }
   __syncthreads();
   STAMP(1);
@@ -458,7 +538,6 @@ __device__ __forceinline__ void row_block(Lds& s, const Args& A, const uint32_t 
 
   // ---- general path (wave 0 only) -------------------------------------------------
   if (s.slow && s.status == PBL_OK) {
-    if (wave_id() != 0) return;
     // keybuf: the block staging area when the block is read from global memory,
     // else the per-KV arrays (unused on this path)
     uint8_t* keybuf = fits ? reinterpret_cast<uint8_t*>(s.eoff) : reinterpret_cast<uint8_t*>(s.blk4);
@@ -466,17 +545,27 @@ __device__ __forceinline__ void row_block(Lds& s, const Args& A, const uint32_t 
                            : uint32_t(kLdsBlkBytes);
     const uint8_t* src = fits ? reinterpret_cast<const uint8_t*>(s.blk4) + kPad + s.shift : gblk;
     SlowState ss;
-    uint64_t dummy[kNumComp] = {0, 0, 0, 0};
-    slow_walk(src, blen, flags, keybuf, keycap, 0, A, b, dummy, &ss);
     uint64_t agg[kNumComp], excl[kNumComp];
-    bool ok = ss.status == PBL_OK;
-    agg[0] = ok ? ss.nkv : 0;
-    agg[1] = ok ? ss.kb : 0;
-    agg[2] = ok ? ss.vb : 0;
-    agg[3] = ok ? ss.nr : 0;
-    lookback(lb_state, nb, b, agg, excl, &O.totals->status_mask);
-    uint32_t status = ss.status;
-    if (ok && overflows(O, excl, agg)) status = PBL_OVERFLOW;
+    uint32_t status = PBL_OK;
+    if (wave_id() == 0) {
+      uint64_t dummy[kNumComp] = {0, 0, 0, 0};
+      slow_walk(src, blen, flags, keybuf, keycap, 0, A, b, dummy, &ss);
+      bool ok = ss.status == PBL_OK;
+      agg[0] = ok ? ss.nkv : 0;
+      agg[1] = ok ? ss.kb : 0;
+      agg[2] = ok ? ss.vb : 0;
+      agg[3] = ok ? ss.nr : 0;
+      lookback(lb_state, nb, b, agg, excl, &O.totals->status_mask);
+      status = ss.status;
+      if (ok && overflows(O, excl, agg)) status = PBL_OVERFLOW;
+    }
+    if (persist) {
+      __syncthreads();
+      if (t == kWave) next_descriptor(s, A, atomicAdd(reinterpret_cast<uint32_t*>(ws), 1u));
+      __syncthreads();
+      next_prefetch(s, A, persist, pf);
+    }
+    if (wave_id() != 0) return;
     if (status == PBL_OK) {
       slow_walk(src, blen, flags, keybuf, keycap, 1, A, b, excl, &ss);
     } else if (lane_id() == 0 && excl[0] + b < O.kv_cap + nb) {
@@ -529,10 +618,6 @@ __device__ __forceinline__ void row_block(Lds& s, const Args& A, const uint32_t 
       if (t == 0) { s.vout[nkv] = tv; s.tot_vb = tv; }
     }
     __syncthreads();
-    for (uint32_t j = t; j < nkv; j += kTPB) {
-      uint32_t vo = s.vout[j], vl = s.vlen[j];
-      for (uint32_t bk = (vo + kBkt - 1) / kBkt; bk * kBkt < vo + vl; bk++) s.aux[kVBkt + bk] = uint16_t(j);
-    }
   }
   STAMP(4);
   if (wave_id() == 0) {
@@ -563,7 +648,17 @@ __device__ __forceinline__ void row_block(Lds& s, const Args& A, const uint32_t 
   }
   __syncthreads();
   STAMP(5);
-  if (s.status != PBL_OK) return;
+  // persistent mode: the next ticket is taken only now, after this block's prefix
+  // has resolved (a workgroup never holds a ticket while it waits), and is
+  // prefetched during the value copy below
+  if (s.status != PBL_OK) {
+    if (persist) {
+      if (t == kWave) next_descriptor(s, A, atomicAdd(reinterpret_cast<uint32_t*>(ws), 1u));
+      __syncthreads();
+      next_prefetch(s, A, persist, pf);
+    }
+    return;
+  }
 
   const uint64_t kvb = s.bases[0], kbb = s.bases[1], vbb = s.bases[2], rbb = s.bases[3];
   // per-KV arrays (coalesced, thread per KV)
@@ -581,26 +676,41 @@ __device__ __forceinline__ void row_block(Lds& s, const Args& A, const uint32_t 
   if (O.restarts)
     for (uint32_t r = t; r < nres; r += kTPB) O.restarts[rbb + r] = V.le32(roff + 4 * r);
   STAMP(6);
+  // the ticket for the next block is taken here (its latency overlaps the key
+  // copy); waves 1-3 start its prefetch before the value copy
+  if (persist && t == kWave) next_descriptor(s, A, atomicAdd(reinterpret_cast<uint32_t*>(ws), 1u));
 
-  // key bytes: 16-byte granules over [kbb, kbb + KB)
-  {
-    const uint64_t lo = kbb, hi = kbb + s.tot_kb;
-    const uint64_t g0 = lo & ~uint64_t(15);
-    for (uint64_t ga = g0 + 16ull * t; ga < hi; ga += 16ull * kTPB) {
-      const uint64_t ga_lo = ga < lo ? lo : ga, ga_hi = ga + 16 < hi ? ga + 16 : hi;
-      uint4 w = key_granule(s, V, uint32_t(ga_lo - lo), uint32_t(ga_hi - lo), uint32_t(ga_lo - ga), nkv);
-      store16(O.key_bytes, ga, lo, hi, w);
+  // key bytes: one thread per KV writes its user key (16-B aligned destination
+  // granules; the edge granules shared with neighbours as byte-exact partial
+  // stores)
+  for (uint32_t j = t; j < nkv; j += kTPB) {
+    const uint32_t k0 = s.kout[j], k1 = s.kout[j + 1];
+    const uint64_t d0 = kbb + k0, d1 = kbb + k1;
+    for (uint64_t a = d0 & ~uint64_t(15); a < d1; a += 16) {
+      const uint32_t lo = a < d0 ? uint32_t(d0 - a) : 0u, hi = a + 16 <= d1 ? 16u : uint32_t(d1 - a);
+      const uint32_t p_lo = uint32_t(a + lo - d0), p_hi = uint32_t(a + hi - d0);
+      const uint4 w = key_part(s, V, int(j), k1 - k0, p_lo, p_hi, lo);
+      if (lo == 0 && hi == 16) *reinterpret_cast<uint4*>(O.key_bytes + a) = w;
+      else store_partial16(O.key_bytes + a, w, lo, hi);
     }
   }
   STAMP(7);
-  // value bytes: 16-byte granules over [vbb, vbb + VB)
-  {
-    const uint64_t lo = vbb, hi = vbb + s.tot_vb;
-    const uint64_t g0 = lo & ~uint64_t(15);
-    for (uint64_t ga = g0 + 16ull * t; ga < hi; ga += 16ull * kTPB) {
-      const uint64_t ga_lo = ga < lo ? lo : ga, ga_hi = ga + 16 < hi ? ga + 16 : hi;
-      uint4 w = val_granule(s, V, uint32_t(ga_lo - lo), uint32_t(ga_hi - lo), uint32_t(ga_lo - ga));
-      store16(O.val_bytes, ga, lo, hi, w);
+  if (persist) {
+    __syncthreads();
+    next_prefetch(s, A, persist, pf);
+  }
+  // value bytes: one thread per KV copies its value (16-B aligned destination
+  // granules: whole ones as dwordx4 stores, the two edge granules it shares with
+  // its neighbours as byte-exact partial stores) -- no output-to-KV search
+  for (uint32_t j = t; j < nkv; j += kTPB) {
+    const uint32_t v0 = s.vout[j], n = s.vout[j + 1] - v0;
+    const int32_t src = int32_t(s.vsrc[j]);
+    const uint64_t d0 = vbb + v0, d1 = d0 + n;
+    for (uint64_t a = d0 & ~uint64_t(15); a < d1; a += 16) {
+      const uint4 w = V.ld16(src + int32_t(int64_t(a) - int64_t(d0)));
+      const uint32_t lo = a < d0 ? uint32_t(d0 - a) : 0u, hi = a + 16 <= d1 ? 16u : uint32_t(d1 - a);
+      if (lo == 0 && hi == 16) *reinterpret_cast<uint4*>(O.val_bytes + a) = w;
+      else store_partial16(O.val_bytes + a, w, lo, hi);
     }
   }
 #ifdef PBL_STAMPS
@@ -609,12 +719,40 @@ __device__ __forceinline__ void row_block(Lds& s, const Args& A, const uint32_t 
 #endif
 }
 
-__global__ void __launch_bounds__(kTPB) rowblk_decode_kernel(Args A) {
-  __shared__ Lds s;
-  __shared__ uint32_t ticket;
-  if (threadIdx.x == 0) ticket = atomicAdd(reinterpret_cast<uint32_t*>(A.out.workspace), 1u);
+// Non-persistent form: stage from global memory, then decode (mixed batches).
+__device__ __forceinline__ void row_block(Lds& s, const Args& A, const uint32_t b) {
+  const uint64_t boff = A.in.block_off[b];
+  const uint32_t blen = A.in.block_len[b];
+  if (blen <= kMaxFastLen) row_stage(s, A.in.blocks, boff, blen);
   __syncthreads();
-  row_block(s, A, ticket);
+  PfRegs unused;
+  row_process(s, A, b, boff, blen, false, unused);
+}
+
+// Persistent row kernel: each workgroup loops over tickets.  While block `cur`
+// writes its outputs, waves 1-3 load the NEXT block into registers (PfRegs), so
+// the HBM latency of staging overlaps the previous block's output phase.  The
+// next ticket is taken when the current block publishes its aggregate, keeping
+// ticket order ~= processing order; the smallest unfinished block always has
+// its predecessors published, so the look-back is deadlock-free for any residency.
+__global__ void __launch_bounds__(kTPB, 3) rowblk_decode_kernel(Args A) {
+  __shared__ Lds s;
+  const int t = threadIdx.x;
+  const uint32_t nb = A.in.n_blocks;
+  PfRegs pf;
+  if (t == 0) next_descriptor(s, A, atomicAdd(reinterpret_cast<uint32_t*>(A.out.workspace), 1u));
+  __syncthreads();
+  next_prefetch(s, A, true, pf);
+  while (true) {
+    __syncthreads();  // s.nxt is published; the previous block's LDS reads are done
+    const uint32_t cur = s.nxt;
+    if (cur >= nb) break;
+    const uint64_t cur_off = s.nxt_off;
+    const uint32_t cur_len = s.nxt_len;
+    if (t >= kWave && cur_len <= kMaxFastLen) pf.store(s, cur_off, cur_len);
+    __syncthreads();
+    row_process(s, A, cur, cur_off, cur_len, true, pf);
+  }
 }
 
 // Mixed row + colblk batch (config 4): per-block format from block_format[];
@@ -688,8 +826,18 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
   a.out = *out;
   if (batch->block_format)
     hipLaunchKernelGGL(pbl::row::mixed_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
-  else
-    hipLaunchKernelGGL(pbl::row::rowblk_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
+  else {
+    // persistent grid: as many workgroups as can be resident (never more than blocks)
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pbl::row::rowblk_decode_kernel, pbl::kTPB, 0) !=
+            hipSuccess)
+      return PBL_DEVICE_ERROR;
+    uint64_t grid = uint64_t(cus > 0 ? cus : 1) * uint64_t(per_cu > 0 ? per_cu : 1);
+    if (grid > batch->n_blocks) grid = batch->n_blocks;
+    hipLaunchKernelGGL(pbl::row::rowblk_decode_kernel, dim3(uint32_t(grid)), dim3(pbl::kTPB), 0, st, a);
+  }
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }
 

@@ -141,3 +141,23 @@ def test_mixed_batch_oracle():
     fmt = np.array([0, 0, 0, 2, 2, 2], np.uint8)
     r = oracle.decode_batch(buf, off, lens, 0, fmt)
     assert r["status_mask"] == 0 and r["n_kv"] == rn + cn
+
+
+def test_colblk_scan_checksum_matches_decode():
+    """The iterate-only CPU baseline (SetNext-shaped scan) sees the same KVs as
+    the oracle's full decode."""
+    M = (1 << 64) - 1
+    for schema in (SCHEMA_DEFAULT, SCHEMA_CRDB1):
+        rng = random.Random(40 + schema)
+        for n in (1, 17, 300):
+            rows = random_rows(rng, schema, n, shared=3)
+            blk, exp = build_block(schema, rows, rng.choice([1, 4, 16]))
+            buf = np.frombuffer(blk + bytes(16), np.uint8).copy()
+            h, cnt = oracle.colblk_scan_checksum(buf, np.array([0], np.uint64), np.array([len(blk)], np.uint32),
+                                                 schema)
+            st, kvs = oracle.colblk_decode_block(blk, schema)
+            x = 1469598103934665603
+            for k, tr, v, fl, _ in kvs:
+                raw = bytes([v[0]]) if v else b"\0"
+                x = ((x ^ tr ^ (k[-1] if k else 0) ^ raw[0] ^ len(v)) * 1099511628211) & M
+            assert cnt == n and h == x
