@@ -14,20 +14,31 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // native 16-B vect
 constexpr int kTPB = 256;   // threads per workgroup (4 waves); one workgroup per block
 constexpr int kWave = 64;
 constexpr int kNumComp = 4; // look-back components: n_kv, key bytes, value bytes, restarts
-constexpr int kLbWin = 4;   // look-back windows (of 64 predecessors) loaded per round trip
+constexpr int kLbWin = 8;   // look-back windows (of 64 predecessors) loaded per round trip
 
 // ---- workspace layout ------------------------------------------------------
-// [0,256): ticket counter (+ pad).  Then kNumComp arrays of n_blocks u64
-// granules {state:2 | value:62} written and read with agent-scope relaxed
-// atomics (8-byte sc1 accesses: the data IS the flag, no fences needed —
-// MI355X_MICROARCH.md "Valid forms", R2 granules).
+// [0,256): ticket counter (+ pad).  Then
+//   word[n_blocks]        one packed status word per block {state:2 | agg:62}:
+//                         state 1 = aggregate ready (4 counts packed below),
+//                         2 = inclusive prefix ready (in pfx[]), 3 = aggregate
+//                         too wide to pack (in wide[])
+//   pfx[kNumComp][n_blocks]   inclusive prefixes {state:2 | value:62}
+//   wide[kNumComp][n_blocks]  unpackable aggregates {state:2 | value:62}
+// All written and read with agent-scope relaxed 8-byte atomics (sc1): each word
+// carries its own state, so a reader that sees a status word before the
+// component words it announces simply polls those (no fences; MI355X_MICROARCH.md
+// "Valid forms", R2 granules).
 constexpr uint64_t kWsHeader = 256;
 constexpr uint64_t kStateAgg = 1ull << 62;
 constexpr uint64_t kStatePfx = 2ull << 62;
+constexpr uint64_t kStateWide = 3ull << 62;
 constexpr uint64_t kValMask = (1ull << 62) - 1;
+// packed aggregate fields: n_kv 14 | key bytes 18 | value bytes 18 | restarts 12
+constexpr int kPkBits[kNumComp] = {14, 18, 18, 12};
+constexpr int kPkShift[kNumComp] = {0, 14, 32, 50};
 
 __host__ __device__ inline uint64_t ws_bytes(uint32_t n_blocks) {
-  return kWsHeader + uint64_t(kNumComp) * n_blocks * 8ull;
+  return kWsHeader + uint64_t(1 + 2 * kNumComp) * n_blocks * 8ull;
 }
 #ifdef PBL_STAMPS
 constexpr uint64_t kStampWords = 16;  // diagnostic build: per-block phase stamps
@@ -96,83 +107,130 @@ __device__ inline void block_excl_scan2(uint32_t a, uint32_t b, uint32_t* ea, ui
 
 // Decoupled look-back (single-pass scan across blocks), in two halves so a
 // workgroup can publish its aggregate as soon as it is known and resolve its
-// exclusive prefix later (after overlapping independent work).  Tickets are
-// handed out in launch order, so every predecessor is already resident and
-// publishes its aggregate before it waits: no deadlock for any residency.
-// Both halves are executed by wave 0 of the workgroup that owns virtual block `v`.
+// exclusive prefix later.  Tickets are handed out in launch order, so every
+// predecessor is resident and publishes its aggregate before it waits: no
+// deadlock for any residency.  Both halves run on wave 0 of the workgroup that
+// owns virtual block `v`; `st` is the workspace after its header.
+__device__ inline bool agg_packable(const uint64_t agg[kNumComp]) {
+  return agg[0] < (1ull << kPkBits[0]) && agg[1] < (1ull << kPkBits[1]) && agg[2] < (1ull << kPkBits[2]) &&
+         agg[3] < (1ull << kPkBits[3]);
+}
+
 __device__ inline void lb_publish(uint64_t* st, uint32_t n_blocks, uint32_t v, const uint64_t agg[kNumComp]) {
   const int l = lane_id();
-  if (l < kNumComp) {
-    uint64_t a = l == 0 ? agg[0] : l == 1 ? agg[1] : l == 2 ? agg[2] : agg[3];
-    st_agent(st + uint64_t(l) * n_blocks + v, (v == 0 ? kStatePfx : kStateAgg) | (a & kValMask));
+  uint64_t* word = st;
+  uint64_t* pfx = st + n_blocks;
+  uint64_t* wide = pfx + uint64_t(kNumComp) * n_blocks;
+  const bool pk = agg_packable(agg);
+  if (v == 0 || !pk) {
+    // block 0: its inclusive prefix IS its aggregate; wide aggregates go to
+    // their own slots (the status word announces them)
+    if (l < kNumComp) {
+      uint64_t a = l == 0 ? agg[0] : l == 1 ? agg[1] : l == 2 ? agg[2] : agg[3];
+      uint64_t* dst = v == 0 ? pfx : wide;
+      st_agent(dst + uint64_t(l) * n_blocks + v, (v == 0 ? kStatePfx : kStateAgg) | (a & kValMask));
+    }
+  }
+  if (l == 0) {
+    uint64_t packed = 0;
+    if (pk)
+      for (int c = 0; c < kNumComp; c++) packed |= agg[c] << kPkShift[c];
+    st_agent(word + v, (v == 0 ? kStatePfx : pk ? kStateAgg : kStateWide) | packed);
   }
 }
 
-// All components are walked back together, kLbWin windows of 64 predecessors
-// per round trip.  Returns exclusive prefixes and publishes the inclusive ones.
+// Poll one component word until it carries `want` (single lane).
+__device__ inline uint64_t lb_poll(uint64_t* p, uint64_t want, uint32_t* spins, bool* timed_out) {
+  uint64_t x;
+  while (((x = ld_agent(p)) & ~kValMask) != want) {
+    if (++*spins > (1u << 22)) { *timed_out = true; return 0; }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return x & kValMask;
+}
+
 __device__ inline void lb_resolve(uint64_t* st, uint32_t n_blocks, uint32_t v, const uint64_t agg[kNumComp],
                                   uint64_t excl[kNumComp], uint32_t* timeout_flag) {
   const int l = lane_id();
-  uint64_t acc[kNumComp];
-  int64_t top[kNumComp];
-  bool done[kNumComp];
-#pragma unroll
-  for (int c = 0; c < kNumComp; c++) { acc[c] = 0; top[c] = int64_t(v) - 1; done[c] = v == 0; }
+  uint64_t* word = st;
+  uint64_t* pfx = st + n_blocks;
+  uint64_t* wide = pfx + uint64_t(kNumComp) * n_blocks;
+  uint64_t acc[kNumComp] = {0, 0, 0, 0};
+  int64_t top = int64_t(v) - 1;
+  bool done = v == 0;
   uint32_t spins = 0;
-  while (!(done[0] && done[1] && done[2] && done[3])) {
-    uint64_t g[kNumComp][kLbWin];
+  bool timed_out = false;
+  while (!done && !timed_out) {
+    uint64_t g[kLbWin];
 #pragma unroll
-    for (int c = 0; c < kNumComp; c++)
-#pragma unroll
-      for (int k = 0; k < kLbWin; k++) {
-        int64_t idx = top[c] - kWave * k - l;
-        g[c][k] = (!done[c] && idx >= 0) ? ld_agent(st + uint64_t(c) * n_blocks + idx) : kStatePfx;
-      }
-    int64_t wait_word = -1;  // a word that was not ready yet
-#pragma unroll
-    for (int c = 0; c < kNumComp; c++) {
-      bool stop = done[c];
-#pragma unroll
-      for (int k = 0; k < kLbWin; k++) {
-        if (stop) continue;
-        uint64_t state = g[c][k] >> 62;
-        uint64_t pfx = __ballot(state == 2);
-        uint64_t notready = __ballot(state == 0);
-        int first = pfx ? __builtin_ctzll(pfx) : 64;
-        uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
-        if (notready & need) {
-          if (wait_word < 0)
-            wait_word = int64_t(c) * n_blocks + (top[c] - kWave * k - __builtin_ctzll(notready & need));
-          stop = true;
-          continue;
-        }
-        acc[c] += wave_sum((l <= first) ? (g[c][k] & kValMask) : 0ull);
-        if (first < 64) { done[c] = true; stop = true; }
-        else top[c] -= kWave;
-      }
+    for (int k = 0; k < kLbWin; k++) {
+      const int64_t idx = top - kWave * k - l;
+      g[k] = idx >= 0 ? ld_agent(word + idx) : kStatePfx;  // (index -1 acts as a zero prefix)
     }
-    if (wait_word >= 0) {
+    int64_t wait_idx = -1;
+    const int64_t top0 = top;  // the windows were loaded from here
+#pragma unroll
+    for (int k = 0; k < kLbWin; k++) {
+      if (done || wait_idx >= 0) continue;
+      const int64_t idx = top0 - kWave * k - l;
+      const uint64_t state = g[k] & ~kValMask;
+      const uint64_t pfxm = __ballot(state == kStatePfx);
+      const uint64_t notready = __ballot(state == 0);
+      const int first = pfxm ? __builtin_ctzll(pfxm) : 64;
+      const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
+      if (notready & need) {
+        wait_idx = top0 - kWave * k - __builtin_ctzll(notready & need);
+        continue;
+      }
+      // contributions: packed aggregates, wide aggregates and the prefix at `first`
+      uint64_t c[kNumComp] = {0, 0, 0, 0};
+      if (l < first || (l == first && idx < 0)) {
+        if (state == kStateAgg) {
+#pragma unroll
+          for (int q = 0; q < kNumComp; q++) c[q] = (g[k] >> kPkShift[q]) & ((1ull << kPkBits[q]) - 1);
+        }
+      }
+      const bool fetch = idx >= 0 && ((l < first && state == kStateWide) || (l == first && state == kStatePfx));
+      if (fetch) {
+        const bool p = state == kStatePfx;
+        uint64_t* src = p ? pfx : wide;
+#pragma unroll
+        for (int q = 0; q < kNumComp; q++)
+          c[q] = lb_poll(src + uint64_t(q) * n_blocks + idx, p ? kStatePfx : kStateAgg, &spins, &timed_out);
+      }
+#pragma unroll
+      for (int q = 0; q < kNumComp; q++) acc[q] += wave_sum(c[q]);
+      if (first < 64) done = true;
+      else top -= kWave;
+    }
+    if (__ballot(timed_out)) { timed_out = true; break; }
+    if (!done && wait_idx >= 0) {
       // Poll the missing predecessor from ONE lane (a whole-window re-read per
-      // poll would flood this CU's memory queue), then re-read the window.
-      bool timed_out = false;
+      // poll would flood this CU's memory queue), then re-read the windows.
       if (l == 0) {
-        while ((ld_agent(st + wait_word) >> 62) == 0) {
+        while ((ld_agent(word + wait_idx) & ~kValMask) == 0) {
           if (++spins > (1u << 22)) { timed_out = true; break; }
           __builtin_amdgcn_s_sleep(2);
         }
       }
-      if (__shfl(timed_out ? 1 : 0, 0, kWave)) {
-        if (l == 0) atomicOr(timeout_flag, 1u << PBL_TIMEOUT);
-        break;
-      }
+      if (__shfl(timed_out ? 1 : 0, 0, kWave)) { timed_out = true; break; }
     }
   }
+  if (timed_out && l == 0) atomicOr(timeout_flag, 1u << PBL_TIMEOUT);
 #pragma unroll
-  for (int c = 0; c < kNumComp; c++) excl[c] = acc[c];
-  if (l < kNumComp && v > 0) {
-    uint64_t e = l == 0 ? excl[0] : l == 1 ? excl[1] : l == 2 ? excl[2] : excl[3];
-    uint64_t a = l == 0 ? agg[0] : l == 1 ? agg[1] : l == 2 ? agg[2] : agg[3];
-    st_agent(st + uint64_t(l) * n_blocks + v, kStatePfx | ((e + a) & kValMask));
+  for (int q = 0; q < kNumComp; q++) excl[q] = acc[q];
+  if (v > 0) {
+    if (l < kNumComp) {
+      uint64_t e = l == 0 ? excl[0] : l == 1 ? excl[1] : l == 2 ? excl[2] : excl[3];
+      uint64_t a = l == 0 ? agg[0] : l == 1 ? agg[1] : l == 2 ? agg[2] : agg[3];
+      st_agent(pfx + uint64_t(l) * n_blocks + v, kStatePfx | ((e + a) & kValMask));
+    }
+    if (l == 0) {
+      uint64_t packed = 0;
+      if (agg_packable(agg))
+        for (int q = 0; q < kNumComp; q++) packed |= agg[q] << kPkShift[q];
+      st_agent(word + v, kStatePfx | packed);
+    }
   }
 }
 

@@ -26,7 +26,7 @@ out = decode(b)
 for _ in range(3):
     out = decode(b)
 torch.cuda.synchronize()
-ws_state = 256 + 4 * nb * 8
+ws_state = 256 + 9 * nb * 8
 st = out.workspace[ws_state: ws_state + nb * 16 * 8].view(torch.int64).view(nb, 16).cpu().numpy()
 phases = [("load+init", 0, 1), ("P1 run walk", 1, 2), ("P1 scan", 2, 3), ("vprefix P2/P4", 3, 4),
           ("look-back (w0)", 4, 9), ("P2 expand (w1-3)", 4, 10), ("join barrier", 4, 5),

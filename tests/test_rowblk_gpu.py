@@ -217,3 +217,16 @@ def test_device_offset_concat_matches_exclusive_prefix():
     after = torch.stack([out.blk_kv_base[:9], out.blk_key_base[:9], out.blk_val_base[:9], out.blk_rst_base[:9]])
     exp = exclusive_bases(totals, 2)
     assert torch.equal(after - before, exp.view(4, 1).expand(4, 9))
+
+
+def test_wide_aggregates_in_lookback():
+    """Blocks whose counts overflow the packed look-back word (>= 16384 KVs,
+    >= 4096 restarts, >= 256 KiB of values) mixed with ordinary ones."""
+    small = gen_row_blocks(5, 6, 32768, 16, 16, 100)
+    many = gen_row_blocks(6, 2, 700000, 1, 16, 0)        # ~30 K KVs and restarts each
+    big = gen_row_blocks(7, 2, 600000, 16, 16, 3000)      # ~590 KB of values each
+    blocks = []
+    for buf, off, lens, _ in (small, many, big):
+        blocks += [bytes(buf[o:o + l]) for o, l in zip(off, lens)]
+    order = [0, 6, 1, 8, 2, 3, 7, 4, 9, 5]
+    check(*pack([blocks[i] for i in order]), 0, "wide aggregates")
