@@ -10,6 +10,7 @@
 namespace pbl {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // native 16-B vector
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));  // native 8-B vector
 
 constexpr int kTPB = 256;   // threads per workgroup (4 waves); one workgroup per block
 constexpr int kWave = 64;
@@ -49,11 +50,36 @@ __host__ __device__ inline uint64_t ws_alloc_bytes(uint32_t n_blocks) {
   return ws_bytes(n_blocks) + kStampWords * 8ull * n_blocks;
 }
 
+// Address-space-typed pointers.  A generic pointer compiles to FLAT
+// instructions, which count against BOTH vmcnt and lgkmcnt: an LDS read issued
+// after a FLAT store or load then waits for that global access (HBM latency)
+// before it can be consumed.  Every hot-path access goes through one of these.
+template <class T>
+using gptr = __attribute__((address_space(1))) T*;
+template <class T>
+using lptr = __attribute__((address_space(3))) T*;
+template <class T>
+__device__ __forceinline__ gptr<T> to_glb(T* p) {
+  return (gptr<T>)p;
+}
+template <class T>
+__device__ __forceinline__ lptr<T> to_lds_ptr(T* p) {
+  return (lptr<T>)p;
+}
+
+// device-scope atomics on global memory (global_atomic_*, never FLAT)
+__device__ inline uint32_t g_atomic_add(uint32_t* p, uint32_t v) {
+  return __hip_atomic_fetch_add(to_glb(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline uint32_t g_atomic_or(uint32_t* p, uint32_t v) {
+  return __hip_atomic_fetch_or(to_glb(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ inline uint64_t ld_agent(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(to_glb(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ inline void st_agent(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(to_glb(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ inline int lane_id() { return threadIdx.x & (kWave - 1); }
@@ -216,7 +242,7 @@ __device__ inline void lb_resolve(uint64_t* st, uint32_t n_blocks, uint32_t v, c
       if (__shfl(timed_out ? 1 : 0, 0, kWave)) { timed_out = true; break; }
     }
   }
-  if (timed_out && l == 0) atomicOr(timeout_flag, 1u << PBL_TIMEOUT);
+  if (timed_out && l == 0) g_atomic_or(timeout_flag, 1u << PBL_TIMEOUT);
 #pragma unroll
   for (int q = 0; q < kNumComp; q++) excl[q] = acc[q];
   if (v > 0) {
@@ -264,25 +290,26 @@ __device__ inline void store16(uint8_t* base, uint64_t ga, uint64_t lo, uint64_t
 __device__ inline void write_block_meta(const pbl_decode_out& O, uint32_t b, uint32_t nb, uint32_t status,
                                         const uint64_t excl[kNumComp], const uint64_t agg[kNumComp],
                                         bool slow) {
-  O.blk_kv_base[b] = excl[0];
-  O.blk_key_base[b] = excl[1];
-  O.blk_val_base[b] = excl[2];
-  if (O.blk_rst_base) O.blk_rst_base[b] = excl[3];
-  O.blk_status[b] = status;
-  if (slow) atomicAdd(&O.totals->n_slow_blocks, 1u);
+  to_glb(O.blk_kv_base)[b] = excl[0];
+  to_glb(O.blk_key_base)[b] = excl[1];
+  to_glb(O.blk_val_base)[b] = excl[2];
+  if (O.blk_rst_base) to_glb(O.blk_rst_base)[b] = excl[3];
+  to_glb(O.blk_status)[b] = status;
+  gptr<pbl_totals> T = to_glb(O.totals);
+  if (slow) g_atomic_add(&O.totals->n_slow_blocks, 1u);
   if (status != PBL_OK) {
-    atomicOr(&O.totals->status_mask, 1u << status);
-    atomicAdd(&O.totals->n_bad_blocks, 1u);
+    g_atomic_or(&O.totals->status_mask, 1u << status);
+    g_atomic_add(&O.totals->n_bad_blocks, 1u);
   }
   if (b == nb - 1) {
-    O.blk_kv_base[nb] = excl[0] + agg[0];
-    O.blk_key_base[nb] = excl[1] + agg[1];
-    O.blk_val_base[nb] = excl[2] + agg[2];
-    if (O.blk_rst_base) O.blk_rst_base[nb] = excl[3] + agg[3];
-    O.totals->n_kv = excl[0] + agg[0];
-    O.totals->key_bytes = excl[1] + agg[1];
-    O.totals->val_bytes = excl[2] + agg[2];
-    O.totals->n_restarts = excl[3] + agg[3];
+    to_glb(O.blk_kv_base)[nb] = excl[0] + agg[0];
+    to_glb(O.blk_key_base)[nb] = excl[1] + agg[1];
+    to_glb(O.blk_val_base)[nb] = excl[2] + agg[2];
+    if (O.blk_rst_base) to_glb(O.blk_rst_base)[nb] = excl[3] + agg[3];
+    T->n_kv = excl[0] + agg[0];
+    T->key_bytes = excl[1] + agg[1];
+    T->val_bytes = excl[2] + agg[2];
+    T->n_restarts = excl[3] + agg[3];
   }
 }
 

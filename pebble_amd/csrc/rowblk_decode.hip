@@ -24,6 +24,9 @@
 // Blocks whose restart table is inconsistent with a per-run walk, or that do
 // not fit the LDS limits, take the general path (rowblk_general.hip.h): a
 // wave-serial restatement of Iter.First/Next, bit-identical by construction.
+#include <stdlib.h>
+#include <string.h>
+
 #include "common.hip.h"
 #include "colblk_block.hip.h"
 
@@ -75,7 +78,7 @@ struct Lds {
 };
 
 // 16 bytes at LDS byte address a (any alignment): five dword reads + alignbyte
-__device__ inline uint4 lds_gather16(const uint32_t* W, uint32_t a) {
+__device__ inline uint4 lds_gather16(lptr<const uint32_t> W, uint32_t a) {
   uint32_t q = a >> 2, r = a & 3;
   uint32_t x0 = W[q], x1 = W[q + 1], x2 = W[q + 2], x3 = W[q + 3], x4 = W[q + 4];
   return make_uint4(__builtin_amdgcn_alignbyte(x1, x0, r), __builtin_amdgcn_alignbyte(x2, x1, r),
@@ -83,9 +86,11 @@ __device__ inline uint4 lds_gather16(const uint32_t* W, uint32_t a) {
 }
 
 // Read-only view of the staged block: its base offset lives in a register.
+struct View;
+__device__ __forceinline__ View lds_view(const void* lds, uint32_t base);
 struct View {
-  const uint8_t* B;   // LDS bytes (array start)
-  const uint32_t* W;  // LDS words (array start)
+  lptr<const uint8_t> B;   // LDS bytes (array start)
+  lptr<const uint32_t> W;  // LDS words (array start)
   uint32_t base;      // byte index of block byte 0 (kPad + shift)
   __device__ inline uint32_t byte(uint32_t i) const { return B[base + i]; }
   // 8 block bytes [i, i+8) as a little-endian u64 (three aligned LDS dword reads)
@@ -103,6 +108,11 @@ struct View {
   // 16 block bytes starting at block offset i (i may be up to 15 below 0)
   __device__ inline uint4 ld16(int32_t i) const { return lds_gather16(W, uint32_t(int32_t(base) + i)); }
 };
+
+__device__ __forceinline__ View lds_view(const void* lds, uint32_t base) {
+  return View{to_lds_ptr(reinterpret_cast<const uint8_t*>(lds)), to_lds_ptr(reinterpret_cast<const uint32_t*>(lds)),
+              base};
+}
 
 // mask of the low n bytes of a word, n clamped to [0, 4]
 __device__ inline uint32_t low_bytes(int n) {
@@ -220,25 +230,28 @@ __device__ inline void block_excl_scan3(uint32_t a, uint32_t b, uint32_t c, uint
 #include "rowblk_general.hip.h"
 
 // Store bytes [lo, hi) of the 16-byte granule w to p[lo..hi) (p 16-B aligned)
-// with the fewest naturally aligned byte/short/dword/qword stores.
-__device__ __forceinline__ uint32_t granule_dword(const uint4& w, uint32_t k) {
-  return k == 0 ? w.x : k == 1 ? w.y : k == 2 ? w.z : w.w;
-}
-__device__ __forceinline__ void store_partial16(uint8_t* p, const uint4& w, uint32_t lo, uint32_t hi) {
+// with the fewest naturally aligned byte/short/dword/qword stores.  The granule
+// is handled as two u64 halves and shifts: indexing its dwords with a runtime
+// index would place it in scratch (a scratch round trip per granule, whose
+// vmcnt wait drains every outstanding store).
+template <class P>
+__device__ __forceinline__ void store_partial16(P p, const uint4& w, uint32_t lo, uint32_t hi) {
+  const uint64_t qa = uint64_t(w.x) | (uint64_t(w.y) << 32);
+  const uint64_t qb = uint64_t(w.z) | (uint64_t(w.w) << 32);
   uint32_t x = lo;
   while (x < hi) {
-    const uint32_t d = granule_dword(w, x >> 2);
+    const uint64_t v = (x < 8 ? qa : qb) >> (8 * (x & 7));
     if ((x & 1) || hi - x < 2) {
-      p[x] = uint8_t(d >> (8 * (x & 3)));
+      *(gptr<uint8_t>)(p + x) = uint8_t(v);
       x += 1;
     } else if ((x & 3) || hi - x < 4) {
-      *reinterpret_cast<uint16_t*>(p + x) = uint16_t(d >> (8 * (x & 3)));
+      *(gptr<uint16_t>)(p + x) = uint16_t(v);
       x += 2;
     } else if ((x & 7) || hi - x < 8) {
-      *reinterpret_cast<uint32_t*>(p + x) = d;
+      *(gptr<uint32_t>)(p + x) = uint32_t(v);
       x += 4;
     } else {
-      *reinterpret_cast<uint2*>(p + x) = make_uint2(d, granule_dword(w, (x >> 2) + 1));
+      *(gptr<uint64_t>)(p + x) = v;
       x += 8;
     }
   }
@@ -438,7 +451,7 @@ struct PfRegs {
     const uint64_t a0 = off & ~uint64_t(15);
     const uint32_t n16 = uint32_t((((off + len + 15) & ~uint64_t(15)) - a0) >> 4);
     if (n16 == 0) return;
-    const u32x4* src = reinterpret_cast<const u32x4*>(blocks + a0);
+    gptr<const u32x4> src = to_glb(reinterpret_cast<const u32x4*>(blocks + a0));
     const uint32_t l = threadIdx.x - kWave;
 #define PBL_PF_LOAD(i)                                               \
     {                                                                \
@@ -495,8 +508,7 @@ __device__ __forceinline__ void row_process(Lds& s, const Args& A, const uint32_
   const uint8_t* gblk = A.in.blocks + boff;
   const bool fits = blen <= kMaxFastLen;
   STAMP(0);
-  const View V{reinterpret_cast<const uint8_t*>(s.blk4), reinterpret_cast<const uint32_t*>(s.blk4),
-               uint32_t(kPad + (boff & 15))};
+  const View V = lds_view(s.blk4, uint32_t(kPad + (boff & 15)));
   if (t == 0) {
     s.shift = uint32_t(boff & 15);
     if (fits) row_init(s, LdsRd{V}, blen, flags, true);
@@ -549,7 +561,7 @@ __device__ __forceinline__ void row_process(Lds& s, const Args& A, const uint32_
     uint32_t status = PBL_OK;
     if (wave_id() == 0) {
       uint64_t dummy[kNumComp] = {0, 0, 0, 0};
-      slow_walk(src, blen, flags, keybuf, keycap, 0, A, b, dummy, &ss);
+      slow_walk(src, blen, flags, keybuf, keycap, 0, A.out, b, dummy, &ss);
       bool ok = ss.status == PBL_OK;
       agg[0] = ok ? ss.nkv : 0;
       agg[1] = ok ? ss.kb : 0;
@@ -567,7 +579,7 @@ __device__ __forceinline__ void row_process(Lds& s, const Args& A, const uint32_
     }
     if (wave_id() != 0) return;
     if (status == PBL_OK) {
-      slow_walk(src, blen, flags, keybuf, keycap, 1, A, b, excl, &ss);
+      slow_walk(src, blen, flags, keybuf, keycap, 1, A.out, b, excl, &ss);
     } else if (lane_id() == 0 && excl[0] + b < O.kv_cap + nb) {
       O.key_off[excl[0] + b] = 0;
       O.val_off[excl[0] + b] = 0;
@@ -755,6 +767,8 @@ __global__ void __launch_bounds__(kTPB, 3) rowblk_decode_kernel(Args A) {
   }
 }
 
+#include "rowblk_pipe.hip.h"
+
 // Mixed row + colblk batch (config 4): per-block format from block_format[];
 // both paths share the ticket order and the look-back state.
 union MixedLds {
@@ -828,15 +842,23 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
     hipLaunchKernelGGL(pbl::row::mixed_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
   else {
     // persistent grid: as many workgroups as can be resident (never more than blocks)
+    // (PBL_ROW_KERNEL=single selects the one-block-per-workgroup persistent
+    // kernel, kept for A/B measurement; the default is the pipelined kernel)
+    const char* kv = getenv("PBL_ROW_KERNEL");
+    const bool single = kv && strcmp(kv, "single") == 0;
+    const void* fn = single ? reinterpret_cast<const void*>(pbl::row::rowblk_decode_kernel)
+                            : reinterpret_cast<const void*>(pbl::row::pipe::rowblk_pipe_kernel);
     int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pbl::row::rowblk_decode_kernel, pbl::kTPB, 0) !=
-            hipSuccess)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, pbl::kTPB, 0) != hipSuccess)
       return PBL_DEVICE_ERROR;
     uint64_t grid = uint64_t(cus > 0 ? cus : 1) * uint64_t(per_cu > 0 ? per_cu : 1);
     if (grid > batch->n_blocks) grid = batch->n_blocks;
-    hipLaunchKernelGGL(pbl::row::rowblk_decode_kernel, dim3(uint32_t(grid)), dim3(pbl::kTPB), 0, st, a);
+    if (single)
+      hipLaunchKernelGGL(pbl::row::rowblk_decode_kernel, dim3(uint32_t(grid)), dim3(pbl::kTPB), 0, st, a);
+    else
+      hipLaunchKernelGGL(pbl::row::pipe::rowblk_pipe_kernel, dim3(uint32_t(grid)), dim3(pbl::kTPB), 0, st, a);
   }
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }

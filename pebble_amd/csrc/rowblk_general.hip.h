@@ -32,8 +32,8 @@ __device__ inline uint32_t g_le32(const uint8_t* p) {
 }
 
 // pass 0 counts; pass 1 writes outputs at the given bases.
-__device__ void slow_walk(const uint8_t* blk, uint64_t len, uint32_t flags, uint8_t* keybuf,
-                          uint32_t keycap, int pass, const Args& A, uint32_t b,
+__device__ __noinline__ void slow_walk(const uint8_t* blk, uint64_t len, uint32_t flags, uint8_t* keybuf,
+                          uint32_t keycap, int pass, const pbl_decode_out O, uint32_t b,
                           const uint64_t* bases, SlowState* st) {
   const int l = lane_id();
   const uint8_t* end = blk + len;
@@ -44,7 +44,6 @@ __device__ void slow_walk(const uint8_t* blk, uint64_t len, uint32_t flags, uint
   int64_t offset = 0;
   uint32_t ri = 0;
   uint32_t status = PBL_OK;
-  const pbl_decode_out& O = A.out;
   while (offset >= 0 && offset < restarts) {
     const uint8_t* p = blk + offset;
     uint32_t shared, unshared, vlen;

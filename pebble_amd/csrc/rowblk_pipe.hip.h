@@ -1,0 +1,632 @@
+// rowblk_pipe.hip.h — the row-format decode as a two-stage, wave-specialised
+// pipeline inside a persistent 256-thread workgroup (two workgroups per CU).
+//
+//   wave 0 ("parse")     block a_i, staged in LDS buffer X[i&1]: Init checks,
+//                        the restart-run walks (lane per run, two passes: count,
+//                        then write per-KV metadata at final indices), prefix
+//                        parents, output-bucket tables; publishes a_i's
+//                        aggregate to the look-back state.  Never waits.
+//   waves 1-3 ("emit")   block a_{i-1}, parsed one iteration earlier (X[(i-1)&1],
+//                        meta slot M[(i-1)&1]): resolves its exclusive prefix
+//                        (its predecessors published at least an iteration ago,
+//                        so the look-back almost never waits), then writes the
+//                        per-KV arrays, restart words, and key / value bytes as
+//                        coalesced 16-B granules gathered from LDS; meanwhile the
+//                        same waves load block a_{i+1} into registers, stored to
+//                        the free LDS buffer after the iteration's barrier.
+//
+// The look-back is therefore off the critical path: a block's outputs are
+// placed one iteration after its sizes are published.  Deadlock freedom: only
+// resident workgroups take tickets; the parse stage never waits (except the
+// general path below, which waits only on smaller tickets), so the smallest
+// unpublished ticket always makes progress.
+//
+// Blocks outside the LDS limits (> 32 KiB, > kKv KVs or runs, > kKeyCap user-key
+// bytes, or a restart table inconsistent with per-run walks) take the general
+// path on wave 0 inside the parse stage (rowblk_general.hip.h: a wave-serial
+// restatement of Iter.First/Next), which resolves its own look-back.
+//
+// Semantics: cockroachdb/pebble sstable/rowblk/rowblk_iter.go — Init :241-276,
+// readFirstKey :418-485, readEntry :333-416, decodeInternalKey :487-504, value
+// prefix :1192-1199 (sstable/block/kv.go:14-41), decodeRestart :1092-1096.
+#pragma once
+
+namespace pipe {
+
+#ifdef PBL_STAMPS
+// diagnostic build only: per-block phase timestamps (s_memtime) written past the
+// look-back state in the workspace; never part of an output
+#define PSTAMP(A_, b_, i_, lane0_)                                                             \
+  do {                                                                                          \
+    if (lane0_)                                                                                 \
+      reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>((A_).out.workspace) +             \
+                                  ws_bytes((A_).in.n_blocks))[uint64_t(b_) * 16 + (i_)] =       \
+          __builtin_amdgcn_s_memtime();                                                         \
+  } while (0)
+#else
+#define PSTAMP(A_, b_, i_, lane0_) do {} while (0)
+#endif
+
+constexpr int kKv = 400;                       // KVs (and runs) per block on the pipelined path
+constexpr uint32_t kKeyCap = 16384;            // user-key bytes per block on the pipelined path
+constexpr int kBs = 7;                         // output bucket = 128 bytes
+constexpr int kKBkt = kKeyCap >> kBs;          // key buckets
+constexpr int kVBkt = kMaxFastLen >> kBs;      // value buckets (values <= block length)
+constexpr int kEmit = kTPB - kWave;            // emitter threads (waves 1-3)
+
+enum { kModeNone = 0, kModeFast = 1, kModeErr = 2, kModeDone = 3 };
+
+// One parsed block.  Offsets are block-relative (u16: the block is <= 32 KiB,
+// user-key bytes <= kKeyCap).
+struct Meta {
+  uint16_t eoff[kKv];      // entry offset (KVEncoding.Offset)
+  uint16_t ksrc[kKv];      // offset of the unshared key bytes
+  uint16_t sh[kKv];        // shared length
+  uint16_t klen[kKv];      // internal key length
+  uint16_t vsrc[kKv];      // value offset (after prefix stripping)
+  uint16_t par[kKv];       // prefix parent: max{i < j in run : shared_i < shared_j} (j itself if shared_j == 0)
+  uint16_t kout[kKv + 1];  // user-key output offsets
+  uint16_t vout[kKv + 1];  // value output offsets
+  uint16_t kbkt[kKBkt];    // KV holding key output byte q*128
+  uint16_t vbkt[kVBkt];    // KV holding value output byte q*128
+  uint8_t kvf[kKv];        // PBL_KV_* flags (OBSOLETE is added at emit time)
+  uint64_t boff;
+  uint32_t b, blen, status, mode, nkv, nres, roff, tot_kb, tot_vb;
+};
+
+struct PLds {
+  uint4 x[2][kLdsBlkBytes / 16];  // block staging, double-buffered
+  Meta m[2];
+  uint32_t nxt;                   // ticket of the block after the current one
+};
+static_assert(sizeof(PLds) <= 163840 / 2, "two pipelined workgroups per CU");
+
+// ---- parse-stage helpers (wave 0) --------------------------------------------
+
+struct RunAcc {
+  uint32_t cnt, kb, vb;
+};
+
+// Pass 1 over run r: count entries and output bytes; `ok` clears if the run is
+// not walkable per run (general path), `bad` sets on shared > len(previous key)
+// (rowblk_iter.go:403), `vbad` on a SET value without its prefix byte.
+__device__ __forceinline__ void run_count(const View& V, uint32_t r, uint32_t nres, uint32_t roff, uint32_t flags,
+                                          bool vprefix, RunAcc& acc, bool& ok, bool& bad, bool& vbad) {
+  const uint32_t st = roff + 4 * r;
+  const uint32_t s0 = V.le32(st) & kRestartMask;
+  const uint32_t e0 = (r + 1 < nres) ? (V.le32(st + 4) & kRestartMask) : roff;
+  if (!((r != 0 || s0 == 0) && s0 < e0 && e0 <= roff)) { ok = false; return; }
+  uint32_t pos = s0, cnt = 0, prev_kl = 0;
+  while (pos < e0) {
+    uint32_t sh, un, vl;
+    const uint32_t h = entry_header(V, pos, e0, &sh, &un, &vl);
+    if (!h || (cnt == 0 && sh != 0)) { ok = false; return; }
+    const uint64_t np = uint64_t(pos) + h + un + vl;
+    if (np > e0) { ok = false; return; }
+    if (cnt > 0 && sh > prev_kl) bad = true;
+    const uint32_t kl = sh + un;
+    uint32_t vlen = vl;
+    if (vprefix && kl >= 8) {
+      if (kl - 8 < sh) { ok = false; return; }  // kind byte inside the shared prefix
+      if ((V.byte(pos + h + (kl - 8 - sh)) & 0xBF) == 1) {
+        if (vl == 0) vbad = true;
+        else if ((V.byte(pos + h + un) & 0xC0) == 0 || (flags & PBL_ROW_NO_VALUER)) vlen--;
+      }
+    }
+    acc.kb += (flags & PBL_ROW_RAW_KEYS) ? kl : (kl >= 8 ? kl - 8 : 0);
+    acc.vb += vlen;
+    cnt++;
+    prev_kl = kl;
+    pos = uint32_t(np);
+  }
+  acc.cnt += cnt;
+}
+
+// Pass 2 over run r (validated by pass 1): per-KV metadata at final indices.
+__device__ __forceinline__ void run_write(Meta& M, const View& V, uint32_t r, uint32_t nres, uint32_t roff,
+                                          uint32_t flags, bool vprefix, RunAcc& acc) {
+  const uint32_t st = roff + 4 * r;
+  const uint32_t rw = V.le32(st);
+  const uint32_t s0 = rw & kRestartMask;
+  const uint32_t e0 = (r + 1 < nres) ? (V.le32(st + 4) & kRestartMask) : roff;
+  uint32_t pos = s0, j = acc.cnt, kb = acc.kb, vb = acc.vb;
+  uint32_t prev_sh = 0, pp = 0, ppsh = 0;
+  bool first = true;
+  while (pos < e0) {
+    uint32_t sh, un, vl;
+    const uint32_t h = entry_header(V, pos, e0, &sh, &un, &vl);
+    const uint32_t kl = sh + un;
+    uint32_t vs = pos + h + un, vlen = vl;
+    uint8_t fl = 0;
+    if (first) fl = uint8_t(PBL_KV_RESTART | ((rw >> 31) ? PBL_KV_RESTART_SAMEPFX : 0));
+    if (!(flags & PBL_ROW_RAW_KEYS) && kl < 8) fl |= PBL_KV_INVALID_KEY;
+    if (vprefix && kl >= 8 && (V.byte(pos + h + (kl - 8 - sh)) & 0xBF) == 1) {
+      const uint32_t pre = V.byte(vs);
+      if ((pre & 0xC0) == 0 || (flags & PBL_ROW_NO_VALUER)) { vs++; vlen--; }
+      else if ((pre & 0xC0) == 0x80) fl |= PBL_KV_VALBLK_HANDLE;
+      else fl |= PBL_KV_BLOB_HANDLE;
+    }
+    // prefix parent: all-nearest-smaller-values over the run (amortised O(1));
+    // the previous entry and its parent are kept in registers
+    uint32_t par = j, parsh = 0;
+    if (sh != 0) {
+      uint32_t c = j - 1, csh = prev_sh;
+      if (csh >= sh) { c = pp; csh = ppsh; }
+      while (csh >= sh) {
+        c = M.par[c];
+        csh = M.sh[c];
+      }
+      par = c;
+      parsh = csh;
+    }
+    M.eoff[j] = uint16_t(pos);
+    M.ksrc[j] = uint16_t(pos + h);
+    M.sh[j] = uint16_t(sh);
+    M.klen[j] = uint16_t(kl);
+    M.vsrc[j] = uint16_t(vs);
+    M.par[j] = uint16_t(par);
+    M.kout[j] = uint16_t(kb);
+    M.vout[j] = uint16_t(vb);
+    M.kvf[j] = fl;
+    prev_sh = sh;
+    pp = par;
+    ppsh = parsh;
+    kb += (flags & PBL_ROW_RAW_KEYS) ? kl : (kl >= 8 ? kl - 8 : 0);
+    vb += vlen;
+    j++;
+    first = false;
+    pos = pos + h + un + vl;
+  }
+  acc.cnt = j;
+  acc.kb = kb;
+  acc.vb = vb;
+}
+
+// Init checks (Init :248-256, readFirstKey :418-485) evaluated by every lane.
+// Returns the status; *roff_o / *nres_o are set when it is PBL_OK.
+template <class Rd>
+__device__ __forceinline__ uint32_t init_checks(const Rd& rd, uint32_t blen, uint32_t flags, uint32_t* roff_o,
+                                                uint32_t* nres_o) {
+  *roff_o = 0;
+  *nres_o = 0;
+  if (blen < 4) return PBL_CORRUPT_BOUNDS;
+  const uint32_t nw = rd.le32(blen - 4);
+  if (nw == 0) return PBL_CORRUPT_NO_RESTARTS;
+  if (nw >> 31) return PBL_CORRUPT_BOUNDS;
+  const uint64_t need = 4ull * (1ull + nw);
+  if (need > blen) return PBL_CORRUPT_BOUNDS;
+  const uint32_t roff = blen - uint32_t(need);
+  if (roff > 0 && !(flags & PBL_ROW_RAW_KEYS)) {
+    if (rd.byte(0) != 0) return PBL_CORRUPT_FIRST_KEY;
+    uint32_t un, vl;
+    const uint32_t n1 = rd.varint(1, blen, &un);
+    const uint32_t n2 = n1 ? rd.varint(1 + n1, blen, &vl) : 0;
+    if (!n2) return PBL_CORRUPT_BOUNDS;
+    if (un < 8) return PBL_CORRUPT_FIRST_KEY;
+  }
+  *roff_o = roff;
+  *nres_o = nw;
+  return PBL_OK;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_bcast_last(T v) {
+  return __shfl(v, kWave - 1, kWave);
+}
+
+// General path for one block (wave 0, inside the parse stage): a wave-serial
+// Iter.First/Next (rowblk_general.hip.h) that resolves its own look-back and
+// writes every output.  Kept out of line: it is rare and large.
+__device__ __noinline__ void parse_slow(Meta& M, uint4* X, const Args A) {
+  const int l = lane_id();
+  const uint32_t b = M.b, blen = M.blen;
+  const uint64_t boff = M.boff;
+  const uint32_t nb = A.in.n_blocks, flags = A.in.flags;
+  const bool fits = blen <= kMaxFastLen;
+  const uint8_t* gblk = A.in.blocks + boff;
+  uint8_t* ws = reinterpret_cast<uint8_t*>(A.out.workspace);
+  uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
+    // ---- general path (wave-serial Iter.Next), resolving its own look-back --------
+    // key buffer: the meta slot's per-KV arrays; if a key outgrows it, re-run
+    // from global memory with the whole staging buffer as the key buffer
+    bool from_lds = fits;
+    uint8_t* keybuf = reinterpret_cast<uint8_t*>(&M);
+    uint32_t keycap = uint32_t(offsetof(Meta, boff));
+    const uint8_t* src = fits ? reinterpret_cast<const uint8_t*>(X) + kPad + (boff & 15) : gblk;
+    if (!fits) { keybuf = reinterpret_cast<uint8_t*>(X); keycap = uint32_t(kLdsBlkBytes); }
+    SlowState ss;
+    uint64_t dummy[kNumComp] = {0, 0, 0, 0};
+    slow_walk(src, blen, flags, keybuf, keycap, 0, A.out, b, dummy, &ss);
+    if (ss.status == PBL_UNSUPPORTED && from_lds) {
+      from_lds = false;
+      src = gblk;
+      keybuf = reinterpret_cast<uint8_t*>(X);
+      keycap = uint32_t(kLdsBlkBytes);
+      slow_walk(src, blen, flags, keybuf, keycap, 0, A.out, b, dummy, &ss);
+    }
+    const bool okk = ss.status == PBL_OK;
+    uint64_t agg[kNumComp] = {okk ? ss.nkv : 0, okk ? ss.kb : 0, okk ? ss.vb : 0, okk ? ss.nr : 0};
+    uint64_t excl[kNumComp];
+    lookback(lb_state, nb, b, agg, excl, &A.out.totals->status_mask);
+    uint32_t st2 = ss.status;
+    if (okk && overflows(A.out, excl, agg)) st2 = PBL_OVERFLOW;
+    if (st2 == PBL_OK) slow_walk(src, blen, flags, keybuf, keycap, 1, A.out, b, excl, &ss);
+    else if (l == 0 && excl[0] + b < A.out.kv_cap + nb) {
+      A.out.key_off[excl[0] + b] = 0;
+      A.out.val_off[excl[0] + b] = 0;
+    }
+    if (l == 0) {
+      write_block_meta(A.out, b, nb, st2, excl, agg, true);
+      M.mode = kModeDone;
+    }
+}
+
+// Parse stage: wave 0, block M.b staged in X (if it fits).
+__device__ __forceinline__ void parse_block(Meta& M, uint4* X, const Args& A) {
+  const int l = lane_id();
+  const uint32_t b = M.b, blen = M.blen;
+  const uint64_t boff = M.boff;
+  const uint32_t nb = A.in.n_blocks, flags = A.in.flags;
+  const bool vprefix = (flags & PBL_ROW_VALUE_PREFIX) && !(flags & PBL_ROW_RAW_KEYS);
+  const bool fits = blen <= kMaxFastLen;
+  const uint8_t* gblk = A.in.blocks + boff;
+  uint8_t* ws = reinterpret_cast<uint8_t*>(A.out.workspace);
+  uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
+  const View V = lds_view(X, uint32_t(kPad + (boff & 15)));
+  PSTAMP(A, b, 0, l == 0);
+
+  uint32_t roff, nres;
+  uint32_t status = fits ? init_checks(LdsRd{V}, blen, flags, &roff, &nres)
+                         : init_checks(GlbRd{gblk}, blen, flags, &roff, &nres);
+  bool slow = status == PBL_OK && (!fits || nres > uint32_t(kKv));
+  uint32_t nkv = 0, tkb = 0, tvb = 0;
+  bool published = false;
+  if (status == PBL_OK && !slow && roff > 0) {
+    // lane l owns runs [r0, r1): contiguous, so a lane scan orders them
+    const uint32_t R = (nres + kWave - 1) / kWave;
+    const uint32_t r0 = min(uint32_t(l) * R, nres), r1 = min(r0 + R, nres);
+    RunAcc acc{0, 0, 0};
+    bool ok = true, bad = false, vbad = false;
+    for (uint32_t r = r0; r < r1 && ok; r++) run_count(V, r, nres, roff, flags, vprefix, acc, ok, bad, vbad);
+    PSTAMP(A, b, 1, l == 0);
+    const uint32_t ic = wave_incl_scan(acc.cnt), ik = wave_incl_scan(acc.kb), iv = wave_incl_scan(acc.vb);
+    nkv = wave_bcast_last(ic);
+    tkb = wave_bcast_last(ik);
+    tvb = wave_bcast_last(iv);
+    if (__ballot(bad)) status = PBL_CORRUPT_BOUNDS;
+    else if (__ballot(!ok) || nkv > uint32_t(kKv) || tkb > kKeyCap) slow = true;
+    else if (__ballot(vbad)) status = PBL_CORRUPT_BOUNDS;  // Go: i.val[0] on an empty SET value
+    if (status == PBL_OK && !slow) {
+      // the sizes are final: publish before the write pass
+      const uint64_t agg[kNumComp] = {nkv, tkb, tvb, nres};
+      lb_publish(lb_state, nb, b, agg);
+      published = true;
+      RunAcc w{ic - acc.cnt, ik - acc.kb, iv - acc.vb};
+      for (uint32_t r = r0; r < r1; r++) run_write(M, V, r, nres, roff, flags, vprefix, w);
+      PSTAMP(A, b, 2, l == 0);
+      if (l == 0) {
+        M.kout[nkv] = uint16_t(tkb);
+        M.vout[nkv] = uint16_t(tvb);
+      }
+      wave_sync();
+      // output buckets: the KV holding byte q*128 of the block's keys / values
+      for (uint32_t j = l; j < nkv; j += kWave) {
+        const uint32_t k0 = M.kout[j], k1 = M.kout[j + 1];
+        for (uint32_t q = (k0 + 127) >> kBs; (q << kBs) < k1; q++) M.kbkt[q] = uint16_t(j);
+        const uint32_t v0 = M.vout[j], v1 = M.vout[j + 1];
+        for (uint32_t q = (v0 + 127) >> kBs; (q << kBs) < v1; q++) M.vbkt[q] = uint16_t(j);
+      }
+    }
+  }
+
+  if (status == PBL_OK && slow) {
+    parse_slow(M, X, A);
+    return;
+  }
+  const bool okb = status == PBL_OK;
+  const uint64_t agg[kNumComp] = {okb ? nkv : 0, okb ? tkb : 0, okb ? tvb : 0, okb ? nres : 0};
+  if (!published) lb_publish(lb_state, nb, b, agg);
+  PSTAMP(A, b, 3, l == 0);
+  if (l == 0) {
+    M.kout[nkv] = uint16_t(tkb);  // (also the lone N+1 offset of a block with no entries)
+    M.vout[nkv] = uint16_t(tvb);
+    M.status = status;
+    M.mode = okb ? kModeFast : kModeErr;
+    M.nkv = nkv;
+    M.nres = okb ? nres : 0;
+    M.roff = roff;
+    M.tot_kb = tkb;
+    M.tot_vb = tvb;
+  }
+}
+
+// ---- emit-stage helpers (waves 1-3) --------------------------------------------
+
+// byte p of the internal key of KV j (source = max{i <= j : shared_i <= p})
+__device__ __forceinline__ uint32_t mkey_byte(const Meta& M, const View& V, int j, uint32_t p) {
+  while (p < uint32_t(M.sh[j])) j--;
+  return V.byte(M.ksrc[j] + p - M.sh[j]);
+}
+
+__device__ __forceinline__ uint64_t mtrailer(const Meta& M, const View& V, int j, uint8_t* fl, uint32_t flags) {
+  if (flags & PBL_ROW_RAW_KEYS) return 0;
+  const uint32_t kl = M.klen[j];
+  if (kl < 8) return kKindInvalid;
+  const uint32_t sh = M.sh[j];
+  uint64_t raw;
+  if (kl - 8 >= sh) {
+    raw = V.ld8(M.ksrc[j] + (kl - 8 - sh));
+  } else {
+    raw = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) raw |= uint64_t(mkey_byte(M, V, j, kl - 8 + i)) << (8 * i);
+  }
+  if (raw & 64u) *fl |= PBL_KV_OBSOLETE;
+  return raw & kTrailerObsoleteMask;
+}
+
+// Merge user-key bytes [p_lo, p_hi) of KV j (user-key length ukl) into granule
+// bytes [q, ...) of w: walk the prefix-parent chain, one LDS gather per segment.
+__device__ __forceinline__ void mkey_part(uint4& w, const Meta& M, const View& V, int j, uint32_t ukl,
+                                          uint32_t p_lo, uint32_t p_hi, uint32_t q) {
+  uint32_t cur = ukl;
+  int i = j;
+  while (cur > p_lo) {
+    const uint32_t shi = M.sh[i];
+    const uint32_t lo_i = shi < cur ? shi : cur;
+    const uint32_t a = lo_i > p_lo ? lo_i : p_lo, z = cur < p_hi ? cur : p_hi;
+    if (a < z) {
+      const uint32_t gq = q + (a - p_lo);
+      const int32_t src = int32_t(M.ksrc[i]) - int32_t(shi) + int32_t(a);
+      const uint4 v = V.ld16(src - int32_t(gq));
+      if (gq == 0 && z - a == 16) w = v;
+      else merge16(w, v, gq, gq + (z - a));
+    }
+    cur = lo_i;
+    i = M.par[i];
+  }
+}
+
+__device__ __forceinline__ void put16(gptr<uint8_t> base, uint64_t a, const uint4& w, uint32_t lo, uint32_t hi) {
+  if (lo == 0 && hi == 16) *(gptr<u32x4>)(base + a) = u32x4{w.x, w.y, w.z, w.w};
+  else store_partial16(base + a, w, lo, hi);
+}
+
+// Emit stage, part 1 (waves 1-3): resolve the exclusive prefix of block M.b
+// (parsed in the previous iteration) and write its block metadata.  Every
+// emitter wave resolves the (normally ready) prefix itself: no cross-wave
+// hand-off inside the stage.  Returns whether the block's outputs are written.
+__device__ __forceinline__ bool emit_resolve(const Meta& M, const Args& A, uint64_t excl[kNumComp]) {
+  const uint32_t mode = M.mode;
+  if (mode != kModeFast && mode != kModeErr) return false;
+  const int tb = int(threadIdx.x) - kWave;
+  const uint32_t b = M.b, nb = A.in.n_blocks;
+  const pbl_decode_out& O = A.out;
+  uint8_t* ws = reinterpret_cast<uint8_t*>(O.workspace);
+  uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
+  uint32_t status = M.status;
+  const bool okb = status == PBL_OK;
+  const uint64_t agg[kNumComp] = {okb ? M.nkv : 0, okb ? M.tot_kb : 0, okb ? M.tot_vb : 0, okb ? M.nres : 0};
+  PSTAMP(A, b, 4, tb == 0);
+  lb_resolve(lb_state, nb, b, agg, excl, &O.totals->status_mask);
+  PSTAMP(A, b, 5, tb == 0);
+  if (okb && overflows(O, excl, agg)) status = PBL_OVERFLOW;
+  if (tb == 0) {
+    if (status != PBL_OK && excl[0] + b < O.kv_cap + nb) {
+      to_glb(O.key_off)[excl[0] + b] = 0;
+      to_glb(O.val_off)[excl[0] + b] = 0;
+    }
+    write_block_meta(O, b, nb, status, excl, agg, false);
+  }
+  return status == PBL_OK;
+}
+
+// Emit stage, part 2 (waves 1-3): per-KV arrays, restart words, key and value
+// bytes of block M.b at the resolved bases.
+__device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const Args& A, const uint64_t* excl) {
+  const int tb = int(threadIdx.x) - kWave;
+  const uint32_t b = M.b, flags = A.in.flags;
+  const pbl_decode_out& O = A.out;
+  const uint32_t nkv = M.nkv, nres = M.nres, roff = M.roff, tkb = M.tot_kb, tvb = M.tot_vb;
+  const View V = lds_view(X, uint32_t(kPad + (M.boff & 15)));
+  const uint64_t kvb = excl[0], kbb = excl[1], vbb = excl[2], rbb = excl[3];
+
+  const gptr<uint32_t> key_off = to_glb(O.key_off), val_off = to_glb(O.val_off);
+  const gptr<uint64_t> trailer = to_glb(O.trailer);
+  const gptr<uint8_t> kv_flags = to_glb(O.kv_flags);
+  const gptr<uint32_t> entry_off = to_glb(O.entry_off), restarts = to_glb(O.restarts);
+
+  // per-KV arrays (coalesced, thread per KV)
+  for (uint32_t j = tb; j <= nkv; j += kEmit) {
+    const uint64_t o = kvb + b + j;
+    key_off[o] = M.kout[j];
+    val_off[o] = M.vout[j];
+    if (j < nkv) {
+      uint8_t fl = M.kvf[j];
+      trailer[kvb + j] = mtrailer(M, V, int(j), &fl, flags);
+      if (O.kv_flags) kv_flags[kvb + j] = fl;
+      if (O.entry_off) entry_off[kvb + j] = M.eoff[j];
+    }
+  }
+  if (O.restarts)
+    for (uint32_t r = tb; r < nres; r += kEmit) restarts[rbb + r] = V.le32(roff + 4 * r);
+  PSTAMP(A, b, 6, tb == 0);
+
+  // key bytes: one 16-B aligned output granule per thread; each the merge of
+  // the segments of the 1-2 keys it overlaps (each key its prefix chain)
+  if (tkb) {
+    const uint64_t d0 = kbb, d1 = kbb + tkb;
+    for (uint64_t a = (d0 & ~uint64_t(15)) + 16 * uint64_t(tb); a < d1; a += 16 * kEmit) {
+      const uint32_t lo = a < d0 ? uint32_t(d0 - a) : 0u, hi = a + 16 <= d1 ? 16u : uint32_t(d1 - a);
+      const uint32_t o = uint32_t(a + lo - d0), oe = uint32_t(a + hi - d0);
+      uint32_t j = M.kbkt[o >> kBs];
+      while (M.kout[j + 1] <= o) j++;
+      uint4 w = make_uint4(0, 0, 0, 0);
+      for (;;) {
+        const uint32_t k0 = M.kout[j], k1 = M.kout[j + 1];
+        const uint32_t s = o > k0 ? o : k0, e = oe < k1 ? oe : k1;
+        if (s < e) mkey_part(w, M, V, int(j), k1 - k0, s - k0, e - k0, uint32_t(d0 + s - a));
+        if (k1 >= oe) break;
+        j++;
+      }
+      put16(to_glb(O.key_bytes), a, w, lo, hi);
+    }
+  }
+  PSTAMP(A, b, 7, tb == 0);
+  // value bytes: same granule scheme, one LDS gather per value segment
+  if (tvb) {
+    const uint64_t d0 = vbb, d1 = vbb + tvb;
+    for (uint64_t a = (d0 & ~uint64_t(15)) + 16 * uint64_t(tb); a < d1; a += 16 * kEmit) {
+      const uint32_t lo = a < d0 ? uint32_t(d0 - a) : 0u, hi = a + 16 <= d1 ? 16u : uint32_t(d1 - a);
+      const uint32_t o = uint32_t(a + lo - d0), oe = uint32_t(a + hi - d0);
+      uint32_t j = M.vbkt[o >> kBs];
+      while (M.vout[j + 1] <= o) j++;
+      uint4 w = make_uint4(0, 0, 0, 0);
+      for (;;) {
+        const uint32_t v0 = M.vout[j], v1 = M.vout[j + 1];
+        const uint32_t s = o > v0 ? o : v0, e = oe < v1 ? oe : v1;
+        const uint32_t gq = uint32_t(d0 + s - a);
+        const int32_t src = int32_t(M.vsrc[j]) + int32_t(s - v0);
+        const uint4 v = V.ld16(src - int32_t(gq));
+        if (gq == 0 && e - s == 16) w = v;
+        else merge16(w, v, gq, gq + (e - s));
+        if (v1 >= oe) break;
+        j++;
+      }
+      put16(to_glb(O.val_bytes), a, w, lo, hi);
+    }
+  }
+  PSTAMP(A, b, 8, tb == 0);
+#ifdef PBL_STAMPS
+  // the last emitter wave to finish: per-wave end stamps
+  PSTAMP(A, b, 9 + (tb >> 6), (tb & 63) == 0);
+#endif
+}
+
+// The next block, held in registers by the parse wave (64 lanes x 33 granules
+// >= the 2051 granules of the largest staged block) between its load at the
+// start of an iteration and its store to LDS after the iteration's first
+// barrier.  The registers are live only inside the parse wave's branch, so the
+// emit waves' register budget (and their vmcnt drains) never see these loads.
+constexpr int kPfRegs0 = (kLdsBlkBytes / 16 + kWave - 1) / kWave;
+static_assert(kPfRegs0 == 33, "PBL_PF0_LIST");
+#define PBL_PF0_LIST(X)                                                                                    \
+  X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18) \
+  X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32)
+
+struct PfWave {
+#define PBL_PF0_DECL(i) u32x4 r##i;
+  PBL_PF0_LIST(PBL_PF0_DECL)
+#undef PBL_PF0_DECL
+  __device__ __forceinline__ static uint32_t granules(uint64_t off, uint32_t len) {
+    return uint32_t((((off + len + 15) & ~uint64_t(15)) - (off & ~uint64_t(15))) >> 4);
+  }
+  // lanes past the end re-read the last granule instead of running off the block
+  __device__ __forceinline__ void load(const uint8_t* blocks, uint64_t off, uint32_t len) {
+    const uint32_t n16 = granules(off, len);
+    gptr<const u32x4> src = to_glb(reinterpret_cast<const u32x4*>(blocks + (off & ~uint64_t(15))));
+    const uint32_t l = lane_id();
+#define PBL_PF0_LOAD(i)                                  \
+    {                                                    \
+      const uint32_t g = l + uint32_t(i) * kWave;        \
+      r##i = src[g < n16 ? g : n16 - 1];                 \
+    }
+    PBL_PF0_LIST(PBL_PF0_LOAD)
+#undef PBL_PF0_LOAD
+  }
+  __device__ __forceinline__ void store(uint4* X, uint64_t off, uint32_t len) const {
+    const uint32_t n16 = granules(off, len);
+    lptr<u32x4> dst = to_lds_ptr(reinterpret_cast<u32x4*>(X)) + 1;
+    const uint32_t l = lane_id();
+#define PBL_PF0_STORE(i)                                 \
+    {                                                    \
+      const uint32_t g = l + uint32_t(i) * kWave;        \
+      if (g < n16) dst[g] = r##i;                        \
+    }
+    PBL_PF0_LIST(PBL_PF0_STORE)
+#undef PBL_PF0_STORE
+  }
+};
+
+// The pipelined persistent kernel.  Iteration i: wave 0 loads a_{i+1} into
+// registers and parses a_i from X[i&1] into M[i&1]; waves 1-3 emit a_{i-1}
+// from X/M[(i-1)&1].  After the first barrier wave 0 stores a_{i+1} into
+// X[(i+1)&1] (free again) and rotates the descriptors; the second barrier
+// publishes them.  Each role executes its own copies of the two barriers, so
+// the prefetch registers stay confined to the parse wave's code.
+__global__ void __launch_bounds__(kTPB, 2) rowblk_pipe_kernel(Args A) {
+  __shared__ PLds S;
+  const int t = threadIdx.x;
+  const uint32_t nb = A.in.n_blocks;
+  uint32_t* tick = A.out.workspace ? reinterpret_cast<uint32_t*>(A.out.workspace) : nullptr;
+  if (t == 0) {
+    const uint32_t t0 = g_atomic_add(tick, 1u);
+    S.m[0].b = t0;
+    S.m[0].mode = kModeNone;
+    S.m[1].mode = kModeNone;
+    S.m[1].b = nb;
+    if (t0 < nb) {
+      S.m[0].boff = to_glb(A.in.block_off)[t0];
+      S.m[0].blen = to_glb(A.in.block_len)[t0];
+      S.nxt = g_atomic_add(tick, 1u);
+    } else {
+      S.nxt = nb;
+    }
+  }
+  __syncthreads();
+  if (t < kWave && S.m[0].b < nb && S.m[0].blen <= kMaxFastLen) {
+    PfWave pf;
+    pf.load(A.in.blocks, S.m[0].boff, S.m[0].blen);
+    pf.store(S.x[0], S.m[0].boff, S.m[0].blen);
+  }
+  __syncthreads();
+  for (uint32_t i = 0;; i++) {
+    Meta& cur = S.m[i & 1];
+    Meta& prv = S.m[(i + 1) & 1];
+    const uint32_t cb = cur.b, nx = S.nxt;
+    if (cb >= nb && prv.mode == kModeNone) break;
+    uint64_t nx_off = 0;
+    uint32_t nx_len = 0;
+    if (nx < nb) {
+      nx_off = to_glb(A.in.block_off)[nx];
+      nx_len = to_glb(A.in.block_len)[nx];
+    }
+    if (t < kWave) {
+      if (cb < nb) parse_block(cur, S.x[i & 1], A);
+    } else {
+      uint64_t excl[kNumComp];
+      if (emit_resolve(prv, A, excl)) emit_write(prv, S.x[(i + 1) & 1], A, excl);
+    }
+    __syncthreads();
+    PSTAMP(A, cb, 13, t == 0 && cb < nb);
+    PSTAMP(A, prv.b, 12, t == kWave && prv.mode != kModeNone);
+    // stage a_{i+1} into the buffer the emit just released (all threads,
+    // synchronous: the loads' latency is exposed once per iteration)
+    if (nx < nb && nx_len <= kMaxFastLen) {
+      const uint32_t n16 = PfWave::granules(nx_off, nx_len);
+      gptr<const u32x4> src = to_glb(reinterpret_cast<const u32x4*>(A.in.blocks + (nx_off & ~uint64_t(15))));
+      lptr<u32x4> dst = to_lds_ptr(reinterpret_cast<u32x4*>(S.x[(i + 1) & 1])) + 1;
+      u32x4 r[9];
+#pragma unroll
+      for (int k = 0; k < 9; k++) {
+        const uint32_t g = t + k * kTPB;
+        r[k] = src[g < n16 ? g : n16 - 1];
+      }
+#pragma unroll
+      for (int k = 0; k < 9; k++) {
+        const uint32_t g = t + k * kTPB;
+        if (g < n16) dst[g] = r[k];
+      }
+    }
+    if (t == 0) {
+      prv.b = nx < nb ? nx : nb;
+      prv.boff = nx_off;
+      prv.blen = nx_len;
+      prv.mode = kModeNone;
+      S.nxt = nx < nb ? g_atomic_add(tick, 1u) : nb;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace pipe
