@@ -224,8 +224,9 @@ __device__ inline void lb_resolve(uint64_t* st, uint32_t n_blocks, uint32_t v, c
         for (int q = 0; q < kNumComp; q++)
           c[q] = lb_poll(src + uint64_t(q) * n_blocks + idx, p ? kStatePfx : kStateAgg, &spins, &timed_out);
       }
+      // per-lane partial sums; the cross-lane reduction happens once, at the end
 #pragma unroll
-      for (int q = 0; q < kNumComp; q++) acc[q] += wave_sum(c[q]);
+      for (int q = 0; q < kNumComp; q++) acc[q] += c[q];
       if (first < 64) done = true;
       else top -= kWave;
     }
@@ -244,7 +245,7 @@ __device__ inline void lb_resolve(uint64_t* st, uint32_t n_blocks, uint32_t v, c
   }
   if (timed_out && l == 0) g_atomic_or(timeout_flag, 1u << PBL_TIMEOUT);
 #pragma unroll
-  for (int q = 0; q < kNumComp; q++) excl[q] = acc[q];
+  for (int q = 0; q < kNumComp; q++) excl[q] = wave_sum(acc[q]);
   if (v > 0) {
     if (l < kNumComp) {
       uint64_t e = l == 0 ? excl[0] : l == 1 ? excl[1] : l == 2 ? excl[2] : excl[3];

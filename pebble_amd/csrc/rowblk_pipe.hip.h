@@ -63,16 +63,20 @@ struct Meta {
   uint16_t ksrc[kKv];      // offset of the unshared key bytes
   uint16_t sh[kKv];        // shared length
   uint16_t klen[kKv];      // internal key length
-  uint16_t vsrc[kKv];      // value offset (after prefix stripping)
   uint16_t par[kKv];       // prefix parent: max{i < j in run : shared_i < shared_j} (j itself if shared_j == 0)
   uint16_t kout[kKv + 1];  // user-key output offsets
-  uint16_t vout[kKv + 1];  // value output offsets
+  uint32_t vp[kKv + 5];    // value output offset | value source offset (after prefix stripping) << 16;
+                           // entries nkv..nkv+4 hold the block's value total (window reads)
   uint16_t kbkt[kKBkt];    // KV holding key output byte q*128
   uint16_t vbkt[kVBkt];    // KV holding value output byte q*128
   uint8_t kvf[kKv];        // PBL_KV_* flags (OBSOLETE is added at emit time)
   uint64_t boff;
+  uint64_t excl[kNumComp];  // exclusive prefix (resolved by the parse wave)
   uint32_t b, blen, status, mode, nkv, nres, roff, tot_kb, tot_vb;
 };
+
+__device__ __forceinline__ uint32_t vout_of(const Meta& M, uint32_t j) { return M.vp[j] & 0xffffu; }
+__device__ __forceinline__ uint32_t vsrc_of(const Meta& M, uint32_t j) { return M.vp[j] >> 16; }
 
 struct PLds {
   uint4 x[2][kLdsBlkBytes / 16];  // block staging, double-buffered
@@ -82,6 +86,28 @@ struct PLds {
 static_assert(sizeof(PLds) <= 163840 / 2, "two pipelined workgroups per CU");
 
 // ---- parse-stage helpers (wave 0) --------------------------------------------
+
+// Entry header (rowblk_iter.go:345-398: three uint32 varints) decoded without
+// branches from the 8 bytes at the entry: each varint 1 or 2 bytes.  Returns
+// false if any needs 3+ bytes (value >= 16384: the block takes the general path).
+__device__ __forceinline__ bool hdr2(uint64_t w, uint32_t* sh, uint32_t* un, uint32_t* vl, uint32_t* h) {
+  uint32_t p = 0, v[3];
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const uint32_t x = uint32_t(w >> (8 * p));
+    const uint32_t b0 = x & 0xff, b1 = (x >> 8) & 0xff;
+    const bool two = (b0 & 0x80) != 0;
+    v[k] = two ? ((b0 & 0x7f) | (b1 << 7)) : b0;
+    ok = ok && !(two && (b1 & 0x80));
+    p += two ? 2 : 1;
+  }
+  *sh = v[0];
+  *un = v[1];
+  *vl = v[2];
+  *h = p;
+  return ok;
+}
 
 struct RunAcc {
   uint32_t cnt, kb, vb;
@@ -98,12 +124,11 @@ __device__ __forceinline__ void run_count(const View& V, uint32_t r, uint32_t nr
   if (!((r != 0 || s0 == 0) && s0 < e0 && e0 <= roff)) { ok = false; return; }
   uint32_t pos = s0, cnt = 0, prev_kl = 0;
   while (pos < e0) {
-    uint32_t sh, un, vl;
-    const uint32_t h = entry_header(V, pos, e0, &sh, &un, &vl);
-    if (!h || (cnt == 0 && sh != 0)) { ok = false; return; }
-    const uint64_t np = uint64_t(pos) + h + un + vl;
-    if (np > e0) { ok = false; return; }
-    if (cnt > 0 && sh > prev_kl) bad = true;
+    uint32_t sh, un, vl, h;
+    const bool hok = hdr2(V.ld8(pos), &sh, &un, &vl, &h);
+    const uint32_t np = pos + h + un + vl;  // < 2^18: no overflow
+    if (!hok || (cnt == 0 && sh != 0) || np > e0) { ok = false; return; }
+    bad = bad || (cnt > 0 && sh > prev_kl);
     const uint32_t kl = sh + un;
     uint32_t vlen = vl;
     if (vprefix && kl >= 8) {
@@ -117,7 +142,7 @@ __device__ __forceinline__ void run_count(const View& V, uint32_t r, uint32_t nr
     acc.vb += vlen;
     cnt++;
     prev_kl = kl;
-    pos = uint32_t(np);
+    pos = np;
   }
   acc.cnt += cnt;
 }
@@ -133,8 +158,8 @@ __device__ __forceinline__ void run_write(Meta& M, const View& V, uint32_t r, ui
   uint32_t prev_sh = 0, pp = 0, ppsh = 0;
   bool first = true;
   while (pos < e0) {
-    uint32_t sh, un, vl;
-    const uint32_t h = entry_header(V, pos, e0, &sh, &un, &vl);
+    uint32_t sh, un, vl, h;
+    hdr2(V.ld8(pos), &sh, &un, &vl, &h);
     const uint32_t kl = sh + un;
     uint32_t vs = pos + h + un, vlen = vl;
     uint8_t fl = 0;
@@ -163,10 +188,9 @@ __device__ __forceinline__ void run_write(Meta& M, const View& V, uint32_t r, ui
     M.ksrc[j] = uint16_t(pos + h);
     M.sh[j] = uint16_t(sh);
     M.klen[j] = uint16_t(kl);
-    M.vsrc[j] = uint16_t(vs);
     M.par[j] = uint16_t(par);
     M.kout[j] = uint16_t(kb);
-    M.vout[j] = uint16_t(vb);
+    M.vp[j] = vb | (vs << 16);
     M.kvf[j] = fl;
     prev_sh = sh;
     pp = par;
@@ -180,6 +204,118 @@ __device__ __forceinline__ void run_write(Meta& M, const View& V, uint32_t r, ui
   acc.cnt = j;
   acc.kb = kb;
   acc.vb = vb;
+}
+
+// Single-walk form of passes 1+2 for runs of at most kRunBuf entries (every
+// run of a block written with restart interval <= 16): the run is walked once,
+// each entry's header parked in two packed registers (static indices: no
+// scratch), and the per-KV metadata is written from registers once the block
+// scan has placed the run.
+constexpr int kRunBuf = 16;
+
+struct RunBuf {
+  uint32_t ea[kRunBuf];  // pos | shared << 16
+  uint32_t eb[kRunBuf];  // unshared | header length << 14 | value length << 17
+  uint32_t cnt, s0, rw;
+};
+
+// Walk run r once.  `ok` clears as in run_count; `over` sets if the run has more
+// than kRunBuf entries.
+__device__ __forceinline__ void run_walk(const View& V, uint32_t r, uint32_t nres, uint32_t roff, uint32_t flags,
+                                         bool vprefix, RunBuf& B, RunAcc& acc, bool& ok, bool& bad, bool& vbad,
+                                         bool& over) {
+  const uint32_t st = roff + 4 * r;
+  B.rw = V.le32(st);
+  const uint32_t s0 = B.rw & kRestartMask;
+  const uint32_t e0 = (r + 1 < nres) ? (V.le32(st + 4) & kRestartMask) : roff;
+  B.s0 = s0;
+  B.cnt = 0;
+  if (!((r != 0 || s0 == 0) && s0 < e0 && e0 <= roff)) { ok = false; return; }
+  uint32_t pos = s0, cnt = 0, prev_kl = 0;
+  bool go = true;
+#pragma unroll
+  for (int k = 0; k < kRunBuf; k++) {
+    if (go && pos < e0) {
+      uint32_t sh, un, vl, h;
+      const bool hok = hdr2(V.ld8(pos), &sh, &un, &vl, &h);
+      const uint32_t np = pos + h + un + vl;
+      if (!hok || (k == 0 && sh != 0) || np > e0) {
+        ok = false;
+        go = false;
+      } else {
+        bad = bad || (k > 0 && sh > prev_kl);
+        const uint32_t kl = sh + un;
+        uint32_t vlen = vl;
+        if (vprefix && kl >= 8) {
+          if (kl - 8 < sh) { ok = false; go = false; }
+          else if ((V.byte(pos + h + (kl - 8 - sh)) & 0xBF) == 1) {
+            if (vl == 0) vbad = true;
+            else if ((V.byte(pos + h + un) & 0xC0) == 0 || (flags & PBL_ROW_NO_VALUER)) vlen--;
+          }
+        }
+        B.ea[k] = pos | (sh << 16);
+        B.eb[k] = un | (h << 14) | (vl << 17);
+        acc.kb += (flags & PBL_ROW_RAW_KEYS) ? kl : (kl >= 8 ? kl - 8 : 0);
+        acc.vb += vlen;
+        cnt++;
+        prev_kl = kl;
+        pos = np;
+      }
+    }
+  }
+  if (go && pos < e0) over = true;
+  B.cnt = cnt;
+  acc.cnt += cnt;
+}
+
+// Write the parked entries of one run at final indices (acc = the run's bases).
+__device__ __forceinline__ void run_emit_meta(Meta& M, const View& V, const RunBuf& B, uint32_t flags, bool vprefix,
+                                              RunAcc acc) {
+  uint32_t j = acc.cnt, kb = acc.kb, vb = acc.vb;
+  uint32_t prev_sh = 0, pp = 0, ppsh = 0;
+#pragma unroll
+  for (int k = 0; k < kRunBuf; k++) {
+    if (uint32_t(k) < B.cnt) {
+      const uint32_t pos = B.ea[k] & 0xffffu, sh = B.ea[k] >> 16;
+      const uint32_t un = B.eb[k] & 0x3fffu, h = (B.eb[k] >> 14) & 7u, vl = B.eb[k] >> 17;
+      const uint32_t kl = sh + un;
+      uint32_t vs = pos + h + un, vlen = vl;
+      uint8_t fl = 0;
+      if (k == 0) fl = uint8_t(PBL_KV_RESTART | ((B.rw >> 31) ? PBL_KV_RESTART_SAMEPFX : 0));
+      if (!(flags & PBL_ROW_RAW_KEYS) && kl < 8) fl |= PBL_KV_INVALID_KEY;
+      if (vprefix && kl >= 8 && (V.byte(pos + h + (kl - 8 - sh)) & 0xBF) == 1) {
+        const uint32_t pre = V.byte(vs);
+        if ((pre & 0xC0) == 0 || (flags & PBL_ROW_NO_VALUER)) { vs++; vlen--; }
+        else if ((pre & 0xC0) == 0x80) fl |= PBL_KV_VALBLK_HANDLE;
+        else fl |= PBL_KV_BLOB_HANDLE;
+      }
+      uint32_t par = j, parsh = 0;
+      if (sh != 0) {
+        uint32_t c = j - 1, csh = prev_sh;
+        if (csh >= sh) { c = pp; csh = ppsh; }
+        while (csh >= sh) {
+          c = M.par[c];
+          csh = M.sh[c];
+        }
+        par = c;
+        parsh = csh;
+      }
+      M.eoff[j] = uint16_t(pos);
+      M.ksrc[j] = uint16_t(pos + h);
+      M.sh[j] = uint16_t(sh);
+      M.klen[j] = uint16_t(kl);
+      M.par[j] = uint16_t(par);
+      M.kout[j] = uint16_t(kb);
+      M.vp[j] = vb | (vs << 16);
+      M.kvf[j] = fl;
+      prev_sh = sh;
+      pp = par;
+      ppsh = parsh;
+      kb += (flags & PBL_ROW_RAW_KEYS) ? kl : (kl >= 8 ? kl - 8 : 0);
+      vb += vlen;
+      j++;
+    }
+  }
 }
 
 // Init checks (Init :248-256, readFirstKey :418-485) evaluated by every lane.
@@ -286,8 +422,19 @@ __device__ __forceinline__ void parse_block(Meta& M, uint4* X, const Args& A) {
     const uint32_t R = (nres + kWave - 1) / kWave;
     const uint32_t r0 = min(uint32_t(l) * R, nres), r1 = min(r0 + R, nres);
     RunAcc acc{0, 0, 0};
-    bool ok = true, bad = false, vbad = false;
-    for (uint32_t r = r0; r < r1 && ok; r++) run_count(V, r, nres, roff, flags, vprefix, acc, ok, bad, vbad);
+    bool ok = true, bad = false, vbad = false, over = false;
+    RunBuf RB;
+    const bool single = R == 1;
+    if (single) {
+      if (r0 < nres) run_walk(V, r0, nres, roff, flags, vprefix, RB, acc, ok, bad, vbad, over);
+      else RB.cnt = 0;
+    }
+    const bool walked = single && !__ballot(over);
+    if (!walked) {
+      acc = RunAcc{0, 0, 0};
+      ok = true; bad = false; vbad = false;
+      for (uint32_t r = r0; r < r1 && ok; r++) run_count(V, r, nres, roff, flags, vprefix, acc, ok, bad, vbad);
+    }
     PSTAMP(A, b, 1, l == 0);
     const uint32_t ic = wave_incl_scan(acc.cnt), ik = wave_incl_scan(acc.kb), iv = wave_incl_scan(acc.vb);
     nkv = wave_bcast_last(ic);
@@ -302,18 +449,18 @@ __device__ __forceinline__ void parse_block(Meta& M, uint4* X, const Args& A) {
       lb_publish(lb_state, nb, b, agg);
       published = true;
       RunAcc w{ic - acc.cnt, ik - acc.kb, iv - acc.vb};
-      for (uint32_t r = r0; r < r1; r++) run_write(M, V, r, nres, roff, flags, vprefix, w);
+      if (walked) run_emit_meta(M, V, RB, flags, vprefix, w);
+      else
+        for (uint32_t r = r0; r < r1; r++) run_write(M, V, r, nres, roff, flags, vprefix, w);
       PSTAMP(A, b, 2, l == 0);
-      if (l == 0) {
-        M.kout[nkv] = uint16_t(tkb);
-        M.vout[nkv] = uint16_t(tvb);
-      }
+      if (l < 5) M.vp[nkv + l] = tvb;
+      if (l == 0) M.kout[nkv] = uint16_t(tkb);
       wave_sync();
       // output buckets: the KV holding byte q*128 of the block's keys / values
       for (uint32_t j = l; j < nkv; j += kWave) {
         const uint32_t k0 = M.kout[j], k1 = M.kout[j + 1];
         for (uint32_t q = (k0 + 127) >> kBs; (q << kBs) < k1; q++) M.kbkt[q] = uint16_t(j);
-        const uint32_t v0 = M.vout[j], v1 = M.vout[j + 1];
+        const uint32_t v0 = vout_of(M, j), v1 = vout_of(M, j + 1);
         for (uint32_t q = (v0 + 127) >> kBs; (q << kBs) < v1; q++) M.vbkt[q] = uint16_t(j);
       }
     }
@@ -327,11 +474,24 @@ __device__ __forceinline__ void parse_block(Meta& M, uint4* X, const Args& A) {
   const uint64_t agg[kNumComp] = {okb ? nkv : 0, okb ? tkb : 0, okb ? tvb : 0, okb ? nres : 0};
   if (!published) lb_publish(lb_state, nb, b, agg);
   PSTAMP(A, b, 3, l == 0);
+  // resolve this block's exclusive prefix now: the parse wave has slack, the
+  // emit waves then start on their stores at once next iteration
+  uint64_t excl[kNumComp];
+  lb_resolve(lb_state, nb, b, agg, excl, &A.out.totals->status_mask);
+  PSTAMP(A, b, 4, l == 0);
+  if (okb && overflows(A.out, excl, agg)) status = PBL_OVERFLOW;
   if (l == 0) {
+    if (status != PBL_OK && excl[0] + b < A.out.kv_cap + nb) {
+      to_glb(A.out.key_off)[excl[0] + b] = 0;
+      to_glb(A.out.val_off)[excl[0] + b] = 0;
+    }
+    write_block_meta(A.out, b, nb, status, excl, agg, false);
+#pragma unroll
+    for (int c = 0; c < kNumComp; c++) M.excl[c] = excl[c];
     M.kout[nkv] = uint16_t(tkb);  // (also the lone N+1 offset of a block with no entries)
-    M.vout[nkv] = uint16_t(tvb);
+    M.vp[nkv] = tvb;
     M.status = status;
-    M.mode = okb ? kModeFast : kModeErr;
+    M.mode = status == PBL_OK ? kModeFast : kModeDone;
     M.nkv = nkv;
     M.nres = okb ? nres : 0;
     M.roff = roff;
@@ -397,28 +557,11 @@ __device__ __forceinline__ void put16(gptr<uint8_t> base, uint64_t a, const uint
 // emitter wave resolves the (normally ready) prefix itself: no cross-wave
 // hand-off inside the stage.  Returns whether the block's outputs are written.
 __device__ __forceinline__ bool emit_resolve(const Meta& M, const Args& A, uint64_t excl[kNumComp]) {
-  const uint32_t mode = M.mode;
-  if (mode != kModeFast && mode != kModeErr) return false;
-  const int tb = int(threadIdx.x) - kWave;
-  const uint32_t b = M.b, nb = A.in.n_blocks;
-  const pbl_decode_out& O = A.out;
-  uint8_t* ws = reinterpret_cast<uint8_t*>(O.workspace);
-  uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
-  uint32_t status = M.status;
-  const bool okb = status == PBL_OK;
-  const uint64_t agg[kNumComp] = {okb ? M.nkv : 0, okb ? M.tot_kb : 0, okb ? M.tot_vb : 0, okb ? M.nres : 0};
-  PSTAMP(A, b, 4, tb == 0);
-  lb_resolve(lb_state, nb, b, agg, excl, &O.totals->status_mask);
-  PSTAMP(A, b, 5, tb == 0);
-  if (okb && overflows(O, excl, agg)) status = PBL_OVERFLOW;
-  if (tb == 0) {
-    if (status != PBL_OK && excl[0] + b < O.kv_cap + nb) {
-      to_glb(O.key_off)[excl[0] + b] = 0;
-      to_glb(O.val_off)[excl[0] + b] = 0;
-    }
-    write_block_meta(O, b, nb, status, excl, agg, false);
-  }
-  return status == PBL_OK;
+  (void)A;
+  if (M.mode != kModeFast) return false;
+#pragma unroll
+  for (int c = 0; c < kNumComp; c++) excl[c] = M.excl[c];
+  return true;
 }
 
 // Emit stage, part 2 (waves 1-3): per-KV arrays, restart words, key and value
@@ -430,6 +573,7 @@ __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const 
   const uint32_t nkv = M.nkv, nres = M.nres, roff = M.roff, tkb = M.tot_kb, tvb = M.tot_vb;
   const View V = lds_view(X, uint32_t(kPad + (M.boff & 15)));
   const uint64_t kvb = excl[0], kbb = excl[1], vbb = excl[2], rbb = excl[3];
+  PSTAMP(A, b, 5, tb == 0);
 
   const gptr<uint32_t> key_off = to_glb(O.key_off), val_off = to_glb(O.val_off);
   const gptr<uint64_t> trailer = to_glb(O.trailer);
@@ -440,7 +584,7 @@ __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const 
   for (uint32_t j = tb; j <= nkv; j += kEmit) {
     const uint64_t o = kvb + b + j;
     key_off[o] = M.kout[j];
-    val_off[o] = M.vout[j];
+    val_off[o] = vout_of(M, j);
     if (j < nkv) {
       uint8_t fl = M.kvf[j];
       trailer[kvb + j] = mtrailer(M, V, int(j), &fl, flags);
@@ -473,27 +617,93 @@ __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const 
     }
   }
   PSTAMP(A, b, 7, tb == 0);
-  // value bytes: same granule scheme, one LDS gather per value segment
+  // value bytes: one 16-B aligned output granule per thread, two granules per
+  // step with their LDS round trips interleaved: (1) bucket -> first KV,
+  // (2) a 5-word window of packed (vout | vsrc) words -> the KV holding the
+  // granule's first byte and the next one, (3) both segments gathered at once,
+  // merged when the granule straddles two values.  Granules touching 3+ values
+  // (values < 16 B) or more than 3 bucket steps take the general loop.
   if (tvb) {
     const uint64_t d0 = vbb, d1 = vbb + tvb;
-    for (uint64_t a = (d0 & ~uint64_t(15)) + 16 * uint64_t(tb); a < d1; a += 16 * kEmit) {
-      const uint32_t lo = a < d0 ? uint32_t(d0 - a) : 0u, hi = a + 16 <= d1 ? 16u : uint32_t(d1 - a);
-      const uint32_t o = uint32_t(a + lo - d0), oe = uint32_t(a + hi - d0);
-      uint32_t j = M.vbkt[o >> kBs];
-      while (M.vout[j + 1] <= o) j++;
-      uint4 w = make_uint4(0, 0, 0, 0);
-      for (;;) {
-        const uint32_t v0 = M.vout[j], v1 = M.vout[j + 1];
-        const uint32_t s = o > v0 ? o : v0, e = oe < v1 ? oe : v1;
-        const uint32_t gq = uint32_t(d0 + s - a);
-        const int32_t src = int32_t(M.vsrc[j]) + int32_t(s - v0);
-        const uint4 v = V.ld16(src - int32_t(gq));
-        if (gq == 0 && e - s == 16) w = v;
-        else merge16(w, v, gq, gq + (e - s));
-        if (v1 >= oe) break;
-        j++;
+    const gptr<uint8_t> vbytes = to_glb(O.val_bytes);
+    uint64_t a = (d0 & ~uint64_t(15)) + 16 * uint64_t(tb);
+    for (; a < d1; a += 32 * kEmit) {
+      uint4 w[2];
+      uint32_t lo[2], hi[2], o[2], oe[2], j0[2];
+      bool live[2];
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const uint64_t g = a + uint64_t(u) * 16 * kEmit;
+        live[u] = g < d1;
+        lo[u] = g < d0 ? uint32_t(d0 - g) : 0u;
+        hi[u] = !live[u] ? 0u : (g + 16 <= d1 ? 16u : uint32_t(d1 - g));
+        o[u] = live[u] ? uint32_t(g + lo[u] - d0) : 0u;
+        oe[u] = live[u] ? uint32_t(g + hi[u] - d0) : 0u;
+        j0[u] = M.vbkt[o[u] >> kBs];
       }
-      put16(to_glb(O.val_bytes), a, w, lo, hi);
+      uint32_t vw[2][5];
+#pragma unroll
+      for (int u = 0; u < 2; u++)
+#pragma unroll
+        for (int k = 0; k < 5; k++) vw[u][k] = M.vp[j0[u] + k];
+      uint4 ga[2], gb[2];
+      uint32_t sa[2], ea[2], sb[2], eb[2];
+      bool gen[2];
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const uint32_t q = o[u];
+        const bool s1 = (vw[u][1] & 0xffff) <= q;
+        const bool s2 = s1 && (vw[u][2] & 0xffff) <= q;
+        const bool s3 = s2 && (vw[u][3] & 0xffff) <= q;
+        const uint32_t k = uint32_t(s1) + uint32_t(s2) + uint32_t(s3);
+        const uint32_t A0 = k == 0 ? vw[u][0] : k == 1 ? vw[u][1] : k == 2 ? vw[u][2] : vw[u][3];
+        const uint32_t A1 = k == 0 ? vw[u][1] : k == 1 ? vw[u][2] : k == 2 ? vw[u][3] : vw[u][4];
+        const uint32_t A2 = k == 0 ? vw[u][2] : k == 1 ? vw[u][3] : k == 2 ? vw[u][4] : vw[u][4];
+        const uint32_t v0 = A0 & 0xffff, v1 = A1 & 0xffff, v2 = A2 & 0xffff;
+        // general loop if the window ran out, or the granule reaches a third value
+        gen[u] = live[u] && ((s3 && (vw[u][4] & 0xffff) <= q) || (oe[u] > v1 && oe[u] > v2) || k == 3);
+        sa[u] = q;
+        ea[u] = oe[u] < v1 ? oe[u] : v1;
+        sb[u] = v1;
+        eb[u] = oe[u] < v2 ? oe[u] : v2;
+        const uint32_t gqa = uint32_t(d0 + sa[u] - (a + uint64_t(u) * 16 * kEmit));
+        ga[u] = V.ld16(int32_t(A0 >> 16) + int32_t(sa[u] - v0) - int32_t(gqa));
+        const uint32_t gqb = gqa + (sb[u] - sa[u]);
+        // (only read when the granule straddles into the next value: keep the
+        // address inside the block otherwise)
+        gb[u] = V.ld16(oe[u] > v1 && !gen[u] ? int32_t(A1 >> 16) - int32_t(gqb) : 0);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        if (!live[u]) continue;
+        const uint64_t g = a + uint64_t(u) * 16 * kEmit;
+        if (!gen[u]) {
+          const uint32_t gqa = uint32_t(d0 + sa[u] - g);
+          if (gqa == 0 && ea[u] - sa[u] == 16) {
+            w[u] = ga[u];
+          } else {
+            w[u] = make_uint4(0, 0, 0, 0);
+            merge16(w[u], ga[u], gqa, gqa + (ea[u] - sa[u]));
+            if (oe[u] > sb[u]) {
+              const uint32_t gqb = gqa + (sb[u] - sa[u]);
+              merge16(w[u], gb[u], gqb, gqb + (eb[u] - sb[u]));
+            }
+          }
+        } else {
+          uint32_t j = j0[u];
+          while (vout_of(M, j + 1) <= o[u]) j++;
+          w[u] = make_uint4(0, 0, 0, 0);
+          for (;;) {
+            const uint32_t v0 = vout_of(M, j), v1 = vout_of(M, j + 1);
+            const uint32_t s_ = o[u] > v0 ? o[u] : v0, e_ = oe[u] < v1 ? oe[u] : v1;
+            const uint32_t gq = uint32_t(d0 + s_ - g);
+            merge16(w[u], V.ld16(int32_t(vsrc_of(M, j)) + int32_t(s_ - v0) - int32_t(gq)), gq, gq + (e_ - s_));
+            if (v1 >= oe[u]) break;
+            j++;
+          }
+        }
+        put16(vbytes, g, w[u], lo[u], hi[u]);
+      }
     }
   }
   PSTAMP(A, b, 8, tb == 0);
@@ -501,6 +711,20 @@ __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const 
   // the last emitter wave to finish: per-wave end stamps
   PSTAMP(A, b, 9 + (tb >> 6), (tb & 63) == 0);
 #endif
+}
+
+__device__ __forceinline__ void pf_store_to(const PfRegs& pf, uint4* X, uint64_t off, uint32_t len) {
+  const uint64_t a0 = off & ~uint64_t(15);
+  const uint32_t n16 = uint32_t((((off + len + 15) & ~uint64_t(15)) - a0) >> 4);
+  const uint32_t l = threadIdx.x - kWave;
+  lptr<u32x4> dst = to_lds_ptr(reinterpret_cast<u32x4*>(X)) + 1;
+#define PBL_PF_STORE2(i)                                   \
+  {                                                        \
+    const uint32_t g = l + uint32_t(i) * kPfThreads;       \
+    if (g < n16) dst[g] = pf.r##i;                         \
+  }
+  PBL_PF_LIST(PBL_PF_STORE2)
+#undef PBL_PF_STORE2
 }
 
 // The next block, held in registers by the parse wave (64 lanes x 33 granules
@@ -591,33 +815,26 @@ __global__ void __launch_bounds__(kTPB, 2) rowblk_pipe_kernel(Args A) {
       nx_off = to_glb(A.in.block_off)[nx];
       nx_len = to_glb(A.in.block_len)[nx];
     }
+    const bool pf_on = nx < nb && nx_len <= kMaxFastLen;
+    PfRegs pf;
     if (t < kWave) {
       if (cb < nb) parse_block(cur, S.x[i & 1], A);
     } else {
       uint64_t excl[kNumComp];
+#ifdef PBL_EXP_NO_EMIT
+      emit_resolve(prv, A, excl);  // diagnostic build: parse timing without the emit stage
+#else
       if (emit_resolve(prv, A, excl)) emit_write(prv, S.x[(i + 1) & 1], A, excl);
+#endif
+      // the next block's loads go out once this wave's stores are issued: they
+      // land while the parse wave finishes (no prefetch registers live during
+      // the emit loops)
+      if (pf_on) pf.load(A.in.blocks, nx_off, nx_len);
     }
     __syncthreads();
     PSTAMP(A, cb, 13, t == 0 && cb < nb);
     PSTAMP(A, prv.b, 12, t == kWave && prv.mode != kModeNone);
-    // stage a_{i+1} into the buffer the emit just released (all threads,
-    // synchronous: the loads' latency is exposed once per iteration)
-    if (nx < nb && nx_len <= kMaxFastLen) {
-      const uint32_t n16 = PfWave::granules(nx_off, nx_len);
-      gptr<const u32x4> src = to_glb(reinterpret_cast<const u32x4*>(A.in.blocks + (nx_off & ~uint64_t(15))));
-      lptr<u32x4> dst = to_lds_ptr(reinterpret_cast<u32x4*>(S.x[(i + 1) & 1])) + 1;
-      u32x4 r[9];
-#pragma unroll
-      for (int k = 0; k < 9; k++) {
-        const uint32_t g = t + k * kTPB;
-        r[k] = src[g < n16 ? g : n16 - 1];
-      }
-#pragma unroll
-      for (int k = 0; k < 9; k++) {
-        const uint32_t g = t + k * kTPB;
-        if (g < n16) dst[g] = r[k];
-      }
-    }
+    if (t >= kWave && pf_on) pf_store_to(pf, S.x[(i + 1) & 1], nx_off, nx_len);
     if (t == 0) {
       prv.b = nx < nb ? nx : nb;
       prv.boff = nx_off;

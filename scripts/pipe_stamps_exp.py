@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """Diagnostic: per-phase cycle breakdown of the pipelined row decode kernel.
 
-Runs the PBL_STAMPS build (libpebble_amd_diag.so) on a config-2 batch and prints
+Runs the PBL_STAMPS build (libpebble_amd_exp.so) on a config-2 batch and prints
 per-phase median / mean / p90 shader cycles per block.  Stamps (rowblk_pipe.hip.h):
-  0 parse start, 1 count pass + scan, 2 write pass, 3 parse end (published),
-  4 look-back resolved (parse wave), 5 emit start, 6 per-KV arrays, 7 keys, 8 values (wave 1),
+  0 parse start, 1 count pass + scan, 2 write pass, 3 parse end (published)
+  4 emit start, 5 look-back resolved, 6 per-KV arrays, 7 keys, 8 values (wave 1),
   9-11 per-emitter-wave end, 12 iteration barrier (emit side), 13 iteration
   barrier (parse side).
 Read the shares, not the absolute length: the stamps themselves perturb timing.
@@ -13,7 +13,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["PBL_LIB"] = os.path.join(ROOT, "pebble_amd", "libpebble_amd_diag.so")
+os.environ["PBL_LIB"] = os.path.join(ROOT, "pebble_amd", "libpebble_amd_exp.so")
 sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
@@ -33,9 +33,9 @@ torch.cuda.synchronize()
 ws_state = 256 + 9 * nb * 8
 st = out.workspace[ws_state: ws_state + nb * 16 * 8].view(torch.int64).view(nb, 16).cpu().numpy()
 phases = [("parse: init+count+scan", 0, 1), ("parse: write pass", 1, 2), ("parse: buckets+publish", 2, 3),
-          ("parse total", 0, 3), ("parse: look-back resolve", 3, 4), ("resolved -> emit start", 4, 5),
+          ("parse total", 0, 3), ("parse end -> emit start", 3, 4), ("emit: look-back", 4, 5),
           ("emit: per-KV", 5, 6), ("emit: keys", 6, 7), ("emit: values (w1)", 7, 8),
-          ("emit total (w1)", 5, 8), ("emit w1 end -> barrier", 8, 12), ("parse end -> barrier", 4, 13)]
+          ("emit total (w1)", 4, 8), ("emit w1 end -> barrier", 8, 12), ("parse end -> barrier", 3, 13)]
 print(f"blocks={nb} ri={ri} kvs={n}")
 for nm, a, z in phases:
     m = (st[:, a] > 0) & (st[:, z] > 0)
@@ -43,8 +43,8 @@ for nm, a, z in phases:
     if d.size:
         print(f"{nm:26s} median {np.median(d):9.0f} mean {np.mean(d):9.0f} p90 {np.percentile(d, 90):9.0f} cycles")
 for w in (9, 10, 11):
-    m = (st[:, 5] > 0) & (st[:, w] > 0)
-    d = (st[m, w] - st[m, 5]).astype(np.float64)
+    m = (st[:, 4] > 0) & (st[:, w] > 0)
+    d = (st[m, w] - st[m, 4]).astype(np.float64)
     print(f"emit wave {w - 8} start->end     median {np.median(d):9.0f} p90 {np.percentile(d, 90):9.0f}")
 t0 = st[:, 0][st[:, 0] > 0]
 t1 = st[:, 8][st[:, 8] > 0]
