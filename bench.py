@@ -97,7 +97,7 @@ def main():
         fmt = N.PBL_FMT_ROW
         buf, off, lens, n_kv = gen_row_blocks(seed, nb, a.block_size, a.restart_interval, a.key_len, a.val_len,
                                               a.value_prefix, n_threads=16)
-        kernel = "rowblk_decode_kernel"
+        kernel = "rowblk_decode_kernel" if os.environ.get("PBL_ROW_KERNEL") == "single" else "rowblk_pipe_kernel"
         wl = (f"config2: {nb} x {a.block_size // 1024} KiB row-format blocks per GPU, restart interval "
               f"{a.restart_interval}, {a.key_len} B keys / {a.val_len} B values" + (", value prefix" if a.value_prefix else ""))
     elif a.workload == "col":

@@ -20,7 +20,7 @@ tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
 src = os.path.join(ROOT, "gpurun_out", "prof")
 dst = os.path.join(ROOT, "profiles")
 os.makedirs(dst, exist_ok=True)
-KERNEL = sys.argv[2] if len(sys.argv) > 2 else "rowblk_decode_kernel"
+KERNEL = sys.argv[2] if len(sys.argv) > 2 else "rowblk_pipe_kernel"
 NB = int(sys.argv[3]) if len(sys.argv) > 3 else 65536
 
 shutil.copy(os.path.join(src, "trace", "trace_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
