@@ -117,6 +117,16 @@ struct Src {
     return g_le(g + o, w);
   }
   __device__ __forceinline__ uint64_t le_u(uint32_t o, uint32_t w) const {  // unaligned, header fields
+    if (o + 8 <= nhead) {
+      // one round trip: three aligned LDS dwords around [o, o+8) and a funnel
+      // shift (the staged head has 8 readable bytes past nhead)
+      const uint32_t a = uint32_t(reinterpret_cast<uintptr_t>(head)) + o;
+      lds_cu32 W = (lds_cu32)(uintptr_t)(a & ~3u);
+      const uint32_t r = a & 3;
+      const uint32_t x0 = W[0], x1 = W[1], x2 = W[2];
+      const uint64_t v = uint64_t(__builtin_amdgcn_alignbyte(x2, x1, r)) << 32 | __builtin_amdgcn_alignbyte(x1, x0, r);
+      return w >= 8 ? v : (v & ((1ull << (8 * w)) - 1));
+    }
     uint64_t v = 0;
     for (int i = int(w) - 1; i >= 0; i--) v = v << 8 | byte(o + i);
     return v;
@@ -241,6 +251,68 @@ __device__ __forceinline__ uint32_t parse_block(const Src& S, uint32_t schema, D
   const UCol& vo = D->v_off;
   D->v_lo = vo.w ? uint32_t(S.le_u(vo.at, vo.w)) : 0;
   D->v_hi = vo.w ? uint32_t(S.le_u(vo.at + rows * vo.w, vo.w)) : 0;
+  if (D->shared_len > D->data_len || D->v_lo > D->v_hi) return PBL_CORRUPT_BOUNDS;
+  return PBL_OK;
+}
+
+// Same decode, one lane per column (wave 0, all 64 lanes call it): each lane
+// reads its directory entry and decodes its column's encoding; the statuses
+// combine by ballot exactly as the serial order would (every header failure is
+// PBL_CORRUPT_COLBLK_HEADER; the final bounds check is PBL_CORRUPT_BOUNDS).
+// Lane 0 writes the shared fields; each column lane writes its own fields.
+__device__ __forceinline__ uint32_t parse_block_wave(const Src& S, uint32_t schema, Desc* D) {
+  const int l = lane_id();
+  if (schema != PBL_FMT_COL_DEFAULT && schema != PBL_FMT_COL_CRDB1) return PBL_UNSUPPORTED;
+  const uint32_t nsc = schema == PBL_FMT_COL_CRDB1 ? 4 : 2;
+  Dir dir;
+  dir.custom = 4 + (schema == PBL_FMT_COL_CRDB1 ? 1 : 0);
+  if (S.len < dir.custom + 7) return PBL_CORRUPT_COLBLK_HEADER;
+  dir.ncols = uint32_t(S.le_u(dir.custom + 1, 2));
+  const uint32_t rows = uint32_t(S.le_u(dir.custom + 3, 4));
+  if (l == 0) D->rows = rows;
+  uint64_t s = 0, nx = 0, e = 0;
+  bool ok = true;
+  uint32_t c = 0xffffffffu;  // this lane's column
+  if (uint32_t(l) < nsc + 5) c = uint32_t(l);
+  if (c == 0) {  // key column 0: PrefixBytes ("empty PrefixBytes" panics for 0 rows)
+    ok = dir.column(S, 0, kDtPrefix, &s, &nx) && rows != 0 && s < S.len;
+    if (ok) {
+      const uint32_t sh = S.byte(uint32_t(s));
+      D->pb_shift = sh;
+      ok = sh <= 16;
+      if (ok) {
+        const uint32_t nbund = 1 + ((rows - 1) >> sh);
+        ok = dec_rawbytes(S, s + 1, rows + nbund, &D->pb_off, &D->pb_data, &e) && e == nx;
+        if (ok) {
+          const UCol& po = D->pb_off;
+          D->shared_len = po.w ? uint32_t(S.le_u(po.at, po.w)) : 0;
+          D->data_len = po.w ? uint32_t(S.le_u(po.at + (rows + nbund) * po.w, po.w)) : 0;
+        }
+      }
+    }
+  } else if (schema == PBL_FMT_COL_CRDB1 && (c == 1 || c == 2)) {
+    ok = dir.column(S, c, kDtUint, &s, &nx) && dec_uints(S, s, rows, c == 1 ? &D->wall : &D->logical, &e) && e == nx;
+  } else if (c == nsc - 1) {  // untyped versions (crdb1) / suffixes (default)
+    ok = dir.column(S, c, kDtBytes, &s, &nx) && dec_rawbytes(S, s, rows, &D->rb_off, &D->rb_data, &e) && e == nx;
+  } else if (c == nsc) {
+    ok = dir.column(S, c, kDtUint, &s, &nx) && dec_uints(S, s, rows, &D->trailers, &e) && e == nx;
+  } else if (c == nsc + 1) {
+    ok = dir.column(S, c, kDtBool, &s, &nx) && dec_bitmap(S, s, rows, &D->pc_at, &e) && e == nx;
+  } else if (c == nsc + 2) {
+    ok = dir.column(S, c, kDtBytes, &s, &nx) && dec_rawbytes(S, s, rows, &D->v_off, &D->v_data, &e) && e == nx;
+    if (ok) {
+      D->key_end = uint32_t(s);
+      const UCol& vo = D->v_off;
+      D->v_lo = vo.w ? uint32_t(S.le_u(vo.at, vo.w)) : 0;
+      D->v_hi = vo.w ? uint32_t(S.le_u(vo.at + rows * vo.w, vo.w)) : 0;
+    }
+  } else if (c == nsc + 3) {
+    ok = dir.column(S, c, kDtBool, &s, &nx) && dec_bitmap(S, s, rows, &D->ext_at, &e) && e == nx;
+  } else if (c == nsc + 4) {
+    ok = dir.column(S, c, kDtBool, &s, &nx) && dec_bitmap(S, s, rows, &D->obs_at, &e) && e == nx;
+  }
+  if (__ballot(!ok)) return PBL_CORRUPT_COLBLK_HEADER;
+  wave_sync();
   if (D->shared_len > D->data_len || D->v_lo > D->v_hi) return PBL_CORRUPT_BOUNDS;
   return PBL_OK;
 }
@@ -430,9 +502,12 @@ __device__ __forceinline__ void col_block(Lds& s, const Args& A, uint32_t b, uin
   __syncthreads();
   const Src S{(lds_cu8)to_lds(s.head4), (lds_cu8)to_lds(s.tail4), (glb_cu8)(A.in.blocks + boff), nhead, tail_lo,
               blen};
-  if (t == 0) {
-    s.d.status = parse_block(S, schema, &s.d);
-    s.status = s.d.status;
+  if (wave_id() == 0) {
+    const uint32_t st = parse_block_wave(S, schema, &s.d);
+    if (lane_id() == 0) {
+      s.d.status = st;
+      s.status = st;
+    }
   }
   __syncthreads();
   if (s.status == PBL_OK && s.d.key_end <= nhead) col_rows<true>(s, A, b, schema, S);
@@ -564,7 +639,7 @@ __device__ __forceinline__ void col_rows(Lds& s, const Args& A, uint32_t b, uint
     const uint64_t src_lo = A.in.block_off[b] + d.v_data + d.v_lo;  // in `blocks`
     const uint64_t n = d.v_hi - d.v_lo;
     const uint64_t lo = vbb, hi = vbb + n;
-    const uint8_t* G = A.in.blocks;
+    const gptr<const uint8_t> G = to_glb(A.in.blocks);
     for (uint64_t ga = (lo & ~uint64_t(15)) + 16ull * t; ga < hi; ga += 16ull * kTPB) {
       // source bytes for destination [ga, ga+16): [sx, sx+16), sx may precede src_lo
       const int64_t sx = int64_t(src_lo) + int64_t(ga) - int64_t(lo);
@@ -572,8 +647,14 @@ __device__ __forceinline__ void col_rows(Lds& s, const Args& A, uint32_t b, uint
       const uint32_t sh = uint32_t(sx - sa);
       const int64_t s_end = int64_t(src_lo + n);
       uint4 x = make_uint4(0, 0, 0, 0), y = make_uint4(0, 0, 0, 0);
-      if (sa + 16 > int64_t(src_lo) && sa < s_end) x = *reinterpret_cast<const uint4*>(G + sa);
-      if (sh && sa + 32 > int64_t(src_lo) && sa + 16 < s_end) y = *reinterpret_cast<const uint4*>(G + sa + 16);
+      if (sa + 16 > int64_t(src_lo) && sa < s_end) {
+        const u32x4 v = *(gptr<const u32x4>)(G + sa);
+        x = make_uint4(v.x, v.y, v.z, v.w);
+      }
+      if (sh && sa + 32 > int64_t(src_lo) && sa + 16 < s_end) {
+        const u32x4 v = *(gptr<const u32x4>)(G + sa + 16);
+        y = make_uint4(v.x, v.y, v.z, v.w);
+      }
       store16(O.val_bytes, ga, lo, hi, sh ? funnel16(x, y, sh) : x);
     }
   }

@@ -1,8 +1,12 @@
 // colblk_decode.hip — gfx950 decoder for batches of Pebble columnar (colblk)
 // data blocks (colblk.DefaultKeySchema / cockroachkvs "crdb1").  One 256-thread
 // workgroup per block in ticket order; per-block work in colblk_block.hip.h.
+#include <stdlib.h>
+#include <string.h>
+
 #include "common.hip.h"
 #include "colblk_block.hip.h"
+#include "colblk_pipe.hip.h"
 
 namespace pbl {
 namespace col {
@@ -28,6 +32,21 @@ extern "C" int pbl_decode_batch_colblk(const pbl_block_batch* batch, pbl_decode_
   pbl::Args a;
   a.in = *batch;
   a.out = *out;
-  hipLaunchKernelGGL(pbl::col::colblk_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
+  // default: the persistent lagged-look-back kernel (colblk_pipe.hip.h);
+  // PBL_COL_KERNEL=single selects the one-block-per-workgroup kernel (A/B)
+  const char* kv = getenv("PBL_COL_KERNEL");
+  if (kv && strcmp(kv, "single") == 0) {
+    hipLaunchKernelGGL(pbl::col::colblk_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
+  } else {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pbl::col::cpipe::colblk_pipe_kernel, pbl::kTPB, 0) !=
+            hipSuccess)
+      return PBL_DEVICE_ERROR;
+    uint64_t grid = uint64_t(cus > 0 ? cus : 1) * uint64_t(per_cu > 0 ? per_cu : 1);
+    if (grid > batch->n_blocks) grid = batch->n_blocks;
+    hipLaunchKernelGGL(pbl::col::cpipe::colblk_pipe_kernel, dim3(uint32_t(grid)), dim3(pbl::kTPB), 0, st, a);
+  }
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }

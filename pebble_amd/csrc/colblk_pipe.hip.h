@@ -1,0 +1,385 @@
+// colblk_pipe.hip.h — persistent, lagged-look-back form of the colblk decode
+// (one 256-thread workgroup loops over tickets; 4 workgroups per CU).
+//
+// Iteration i of a workgroup, whole-workgroup phases:
+//   parse  block a_i from slot[i&1]: header + column directory (lane 0), key
+//          sizes and bounds checks (thread per row), block scan, and the
+//          aggregate is PUBLISHED to the look-back state;
+//   emit   block a_{i-1} from slot[(i-1)&1], parsed one phase earlier: its
+//          exclusive prefix is resolved (normally without waiting: every
+//          predecessor published at least a phase ago), then per-row arrays,
+//          keys (built in LDS, leaving as aligned 16-B stores) and values
+//          (one contiguous range, global -> global);
+//   the head/tail of block a_{i+1}, loaded into registers at the start of the
+//          iteration, goes to the slot the emit released.
+// The look-back's wait is thus off the critical path (colblk_block.hip.h's
+// one-block-per-workgroup form waits for it in-line).
+//
+// Semantics are those of colblk_block.hip.h (same helpers; DataBlockDecoder.Init
+// sstable/colblk/data_block.go:1096-1109, DataBlockIter.Next :1662-1708).
+#pragma once
+
+namespace pbl {
+namespace col {
+namespace cpipe {
+
+constexpr uint32_t kHeadBuf = kStage + 16;  // head bytes + the block's 16-B phase
+constexpr uint32_t kTailBuf = kTail + 32;   // tail bytes + phase + partial granule
+enum { kNone = 0, kFast = 1, kErr = 2 };
+
+#ifdef PBL_STAMPS
+// diagnostic build only: per-block phase timestamps past the look-back state
+#define CSTAMP(A_, b_, i_)                                                                      \
+  do {                                                                                          \
+    if (threadIdx.x == 0)                                                                       \
+      reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>((A_).out.workspace) +             \
+                                  ws_bytes((A_).in.n_blocks))[uint64_t(b_) * 16 + (i_)] =       \
+          __builtin_amdgcn_s_memtime();                                                         \
+  } while (0)
+#else
+#define CSTAMP(A_, b_, i_) do {} while (0)
+#endif
+
+struct Slot {
+  uint4 head4[kHeadBuf / 16];
+  uint4 tail4[kTailBuf / 16];
+  Desc d;
+  uint64_t boff;
+  uint64_t agg[kNumComp];
+  uint32_t b, blen, nhead, tail_lo, shift, status, mode, tot0;
+  uint32_t fast;  // header parsed and the key columns inside the staged head
+};
+
+struct CLds {
+  Slot s[2];
+  uint4 key4[(kKeyBuf + 2 * kKeyPad) / 16];
+  uint64_t red[4];
+  uint64_t bases[kNumComp];
+  uint32_t scratch[16];
+  uint32_t bad, nxt, st;
+};
+static_assert(sizeof(CLds) <= 163840 / 4, "four pipelined colblk workgroups per CU");
+
+__device__ __forceinline__ Src slot_src(const Slot& P, const Args& A) {
+  return Src{(lds_cu8)to_lds(P.head4) + P.shift, (lds_cu8)to_lds(P.tail4) + P.shift,
+             (glb_cu8)(A.in.blocks + P.boff), P.nhead, P.tail_lo, P.blen};
+}
+
+// Head / tail geometry of a block (same split as col_block).
+__device__ __forceinline__ void geometry(uint32_t blen, uint32_t* nhead, uint32_t* tail_lo) {
+  *nhead = blen < kStage ? blen : kStage;
+  *tail_lo = blen > kTail ? ((blen - kTail) & ~15u) : 0;
+}
+
+// Raw 16-B aligned granules of the head and tail regions, held in registers
+// (4 + 1 per thread cover 12 KiB + 16 B and 512 + 32 B).
+struct ColPf {
+  u32x4 h0, h1, h2, h3, tl;
+  __device__ __forceinline__ void load(const uint8_t* blocks, uint64_t boff, uint32_t blen) {
+    uint32_t nhead, tail_lo;
+    geometry(blen, &nhead, &tail_lo);
+    const uint64_t a0 = boff & ~uint64_t(15);
+    const uint32_t nh = uint32_t(((boff + nhead + 15) & ~uint64_t(15)) - a0) >> 4;
+    gptr<const u32x4> H = to_glb(reinterpret_cast<const u32x4*>(blocks + a0));
+    const uint32_t t = threadIdx.x;
+    h0 = H[t < nh ? t : nh - 1];
+    h1 = H[t + 256 < nh ? t + 256 : nh - 1];
+    h2 = H[t + 512 < nh ? t + 512 : nh - 1];
+    h3 = H[t + 768 < nh ? t + 768 : nh - 1];
+    const uint64_t b0 = (boff + tail_lo) & ~uint64_t(15);
+    const uint32_t nt = uint32_t(((boff + blen + 15) & ~uint64_t(15)) - b0) >> 4;
+    gptr<const u32x4> T = to_glb(reinterpret_cast<const u32x4*>(blocks + b0));
+    tl = T[t < nt ? t : nt - 1];
+  }
+  __device__ __forceinline__ void store(Slot& P, uint64_t boff, uint32_t blen) const {
+    uint32_t nhead, tail_lo;
+    geometry(blen, &nhead, &tail_lo);
+    const uint32_t nh = uint32_t(((boff + nhead + 15) & ~uint64_t(15)) - (boff & ~uint64_t(15))) >> 4;
+    const uint64_t b0 = (boff + tail_lo) & ~uint64_t(15);
+    const uint32_t nt = uint32_t(((boff + blen + 15) & ~uint64_t(15)) - b0) >> 4;
+    lptr<u32x4> H = to_lds_ptr(reinterpret_cast<u32x4*>(P.head4));
+    lptr<u32x4> T = to_lds_ptr(reinterpret_cast<u32x4*>(P.tail4));
+    const uint32_t t = threadIdx.x;
+    if (t < nh) H[t] = h0;
+    if (t + 256 < nh) H[t + 256] = h1;
+    if (t + 512 < nh) H[t + 512] = h2;
+    if (t + 768 < nh) H[t + 768] = h3;
+    if (t < nt) T[t] = tl;
+  }
+};
+
+// Slot bookkeeping for block b (thread 0 computes; all threads see it after the
+// caller's barrier).  Blocks whose start is not 8-B aligned are staged with the
+// funnel shift instead (8-B column reads from LDS need 8-B alignment).
+__device__ __forceinline__ void slot_setup(Slot& P, uint32_t b, uint64_t boff, uint32_t blen) {
+  P.b = b;
+  P.boff = boff;
+  P.blen = blen;
+  geometry(blen, &P.nhead, &P.tail_lo);
+  P.shift = (boff & 7) == 0 ? uint32_t(boff & 15) : 0u;
+  P.mode = kNone;
+}
+__device__ __forceinline__ void slot_stage_funnel(Slot& P, const Args& A) {
+  const uint64_t a1 = (P.boff + P.blen + 15) & ~uint64_t(15);
+  stage((lds_u4)to_lds(P.head4), A.in.blocks, P.boff, a1, 0, P.nhead);
+  stage((lds_u4)to_lds(P.tail4), A.in.blocks, P.boff, a1, P.tail_lo, P.blen - P.tail_lo);
+}
+
+// ---- parse phase (whole workgroup) ------------------------------------------------
+template <bool F>
+__device__ __forceinline__ void col_parse_rows(CLds& L, Slot& P, const Args& A, uint32_t schema, const Src& S) {
+  const int t = threadIdx.x;
+  const uint32_t nb = A.in.n_blocks;
+  uint8_t* ws = reinterpret_cast<uint8_t*>(A.out.workspace);
+  uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
+  const Desc& d = P.d;
+  const bool hdr_ok = P.status == PBL_OK;
+  const uint32_t rows = hdr_ok ? d.rows : 0;
+  const uint32_t nch = (rows + kChunk - 1) / kChunk;
+  uint32_t k0 = 0;
+  uint64_t my_kb = 0;
+  bool my_bad = false;
+  for (uint32_t c = 0; c < nch; c++) {
+    const uint32_t r = c * kChunk + t;
+    if (r < rows) {
+      const RowParts p = row_parts<F>(S, d, schema, r);
+      my_bad |= !p.ok || !value_ok(S, d, r);
+      my_kb += p.klen;
+      if (c == 0) k0 = p.klen;
+    }
+  }
+  if (my_bad) L.bad = 1;
+  uint32_t excl0, tot0, de, dt;
+  block_excl_scan2(k0, 0u, &excl0, &de, L.scratch, &tot0, &dt);
+  const uint64_t kb_tot = block_sum_u64(my_kb, L.red);  // (syncs; also orders L.bad)
+  (void)excl0;
+  if (t == 0 && P.status == PBL_OK) {
+    if (L.bad) P.status = PBL_CORRUPT_BOUNDS;
+    else if (kb_tot > 0xffffffffull || uint64_t(d.v_hi - d.v_lo) > 0xffffffffull) P.status = PBL_UNSUPPORTED;
+  }
+  __syncthreads();
+  const bool ok = P.status == PBL_OK;
+  const uint64_t agg[kNumComp] = {ok ? rows : 0u, ok ? kb_tot : 0ull, ok ? uint64_t(d.v_hi - d.v_lo) : 0ull, 0ull};
+  if (wave_id() == 0) lb_publish(lb_state, nb, P.b, agg);
+  if (t == 0) {
+#pragma unroll
+    for (int c = 0; c < kNumComp; c++) P.agg[c] = agg[c];
+    P.tot0 = tot0;
+    P.mode = ok ? kFast : kErr;
+  }
+}
+
+__device__ __forceinline__ void col_parse(CLds& L, Slot& P, const Args& A, uint32_t schema) {
+  const Src S = slot_src(P, A);
+  CSTAMP(A, P.b, 0);
+  if (wave_id() == 0) {
+    const uint32_t st = parse_block_wave(S, schema, &P.d);
+    if (lane_id() == 0) {
+      L.bad = 0;
+      P.status = st;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) P.fast = P.status == PBL_OK && P.d.key_end <= P.nhead;
+  CSTAMP(A, P.b, 1);
+  if (P.status == PBL_OK && P.d.key_end <= P.nhead) col_parse_rows<true>(L, P, A, schema, S);
+  else col_parse_rows<false>(L, P, A, schema, S);
+  CSTAMP(A, P.b, 2);
+}
+
+// ---- emit phase (whole workgroup) --------------------------------------------------
+template <bool F>
+__device__ __forceinline__ void col_emit_rows(CLds& L, const Slot& E, const Args& A, uint32_t schema, const Src& S) {
+  const int t = threadIdx.x;
+  const pbl_decode_out& O = A.out;
+  const uint32_t b = E.b;
+  const Desc& d = E.d;
+  const uint32_t rows = d.rows;
+  const uint32_t nch = (rows + kChunk - 1) / kChunk;
+  const uint64_t kvb = L.bases[0], kbb = L.bases[1], vbb = L.bases[2];
+  const gptr<uint32_t> key_off = to_glb(O.key_off), val_off = to_glb(O.val_off);
+  const gptr<uint64_t> trailer = to_glb(O.trailer);
+  const gptr<uint8_t> kv_flags = to_glb(O.kv_flags);
+  const gptr<uint32_t> entry_off = to_glb(O.entry_off);
+
+  // per-row arrays
+  const UCol& vo = d.v_off;
+  for (uint32_t r = t; r <= rows; r += kTPB) {
+    const uint32_t v = vo.w ? uint32_t(S.le(vo.at + r * vo.w, vo.w)) : 0;
+    val_off[kvb + b + r] = v - d.v_lo;
+    if (r < rows) {
+      trailer[kvb + r] = u_at<F>(S, d.trailers, r);
+      if (O.kv_flags) {
+        uint8_t fl = 0;
+        if (d.pc_at && ((S.le(d.pc_at + 8 * (r >> 6), 8) >> (r & 63)) & 1)) fl |= PBL_KV_PREFIX_CHANGED;
+        if (d.obs_at && ((S.le(d.obs_at + 8 * (r >> 6), 8) >> (r & 63)) & 1)) fl |= PBL_KV_OBSOLETE;
+        if (d.ext_at && ((S.le(d.ext_at + 8 * (r >> 6), 8) >> (r & 63)) & 1)) {
+          const uint32_t v1 = vo.w ? uint32_t(S.le(vo.at + (r + 1) * vo.w, vo.w)) : 0;
+          const bool vb = v1 > v && (S.byte(d.v_data + v) & 0xC0) == 0x80;
+          fl |= vb ? PBL_KV_VALBLK_HANDLE : PBL_KV_BLOB_HANDLE;
+        }
+        kv_flags[kvb + r] = fl;
+      }
+      if (O.entry_off) entry_off[kvb + r] = r;
+    }
+  }
+
+  CSTAMP(A, b, 5);
+  // key bytes: chunks of 256 rows built in the LDS key buffer, copied out as
+  // aligned 16-B granules (keys past the buffer go straight to global memory)
+  lds_u8 kb8 = (lds_u8)to_lds(L.key4);
+  uint32_t cbase = 0;
+  for (uint32_t c = 0; c < nch; c++) {
+    const uint32_t r = c * kChunk + t;
+    RowParts p;
+    p.klen = 0;
+    if (r < rows) p = row_parts<F>(S, d, schema, r);
+    uint32_t ex, tot, de, dt;
+    block_excl_scan2(p.klen, 0u, &ex, &de, L.scratch, &tot, &dt);
+    if (r < rows) key_off[kvb + b + r] = cbase + ex;
+    if (tot <= kKeyBuf) {
+      if (r < rows) build_key<F>(S, d, schema, p, kb8, kKeyPad + ex);
+      __syncthreads();
+      const uint64_t lo = kbb + cbase, hi = lo + tot;
+      const lds_cu32 W = (lds_cu32)to_lds(L.key4);
+      for (uint64_t ga = (lo & ~uint64_t(15)) + 16ull * t; ga < hi; ga += 16ull * kTPB)
+        store16(O.key_bytes, ga, lo, hi, lds_bytes16(W, uint32_t(kKeyPad + ga - lo)));
+    } else if (r < rows) {
+      build_key_global<F>(S, d, schema, p, O.key_bytes + kbb + cbase + ex);
+    }
+    cbase += tot;
+    __syncthreads();
+  }
+  if (t == 0) key_off[kvb + b + rows] = cbase;
+  CSTAMP(A, b, 6);
+
+  // value bytes: one contiguous range, global -> global; four output granules
+  // per thread per step so their source loads are in flight together
+  {
+    const uint64_t src_lo = E.boff + d.v_data + d.v_lo;
+    const uint64_t n = d.v_hi - d.v_lo;
+    const uint64_t lo = vbb, hi = vbb + n;
+    const gptr<const uint8_t> G = to_glb(A.in.blocks);
+    const int64_t s_end = int64_t(src_lo + n);
+    constexpr int U = 4;
+    for (uint64_t g0 = (lo & ~uint64_t(15)) + 16ull * t; g0 < hi; g0 += 16ull * kTPB * U) {
+      u32x4 x[U], y[U];
+      uint32_t sh[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t ga = g0 + 16ull * kTPB * u;
+        const int64_t sx = int64_t(src_lo) + int64_t(ga) - int64_t(lo);
+        const int64_t sa = sx & ~int64_t(15);
+        sh[u] = uint32_t(sx - sa);
+        const bool live = ga < hi;
+        x[u] = u32x4{0, 0, 0, 0};
+        y[u] = u32x4{0, 0, 0, 0};
+        if (live && sa + 16 > int64_t(src_lo) && sa < s_end) x[u] = *(gptr<const u32x4>)(G + sa);
+        if (live && sh[u] && sa + 32 > int64_t(src_lo) && sa + 16 < s_end) y[u] = *(gptr<const u32x4>)(G + sa + 16);
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t ga = g0 + 16ull * kTPB * u;
+        if (ga >= hi) continue;
+        const uint4 xx = make_uint4(x[u].x, x[u].y, x[u].z, x[u].w);
+        const uint4 yy = make_uint4(y[u].x, y[u].y, y[u].z, y[u].w);
+        store16(O.val_bytes, ga, lo, hi, sh[u] ? funnel16(xx, yy, sh[u]) : xx);
+      }
+    }
+  }
+  CSTAMP(A, b, 7);
+}
+
+__device__ __forceinline__ void col_emit(CLds& L, const Slot& E, const Args& A, uint32_t schema) {
+  const uint32_t nb = A.in.n_blocks;
+  const pbl_decode_out& O = A.out;
+  uint8_t* ws = reinterpret_cast<uint8_t*>(O.workspace);
+  uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
+  const uint32_t b = E.b;
+  CSTAMP(A, b, 3);
+  if (wave_id() == 0) {
+    const uint64_t agg[kNumComp] = {E.agg[0], E.agg[1], E.agg[2], E.agg[3]};
+    uint64_t excl[kNumComp];
+    lb_resolve(lb_state, nb, b, agg, excl, &O.totals->status_mask);
+    if (lane_id() == 0) {
+      uint32_t status = E.status;
+      if (status == PBL_OK && overflows(O, excl, agg)) status = PBL_OVERFLOW;
+      L.st = status;
+#pragma unroll
+      for (int c = 0; c < kNumComp; c++) L.bases[c] = excl[c];
+      if (status != PBL_OK && excl[0] + b < O.kv_cap + nb) {
+        to_glb(O.key_off)[excl[0] + b] = 0;
+        to_glb(O.val_off)[excl[0] + b] = 0;
+      }
+      write_block_meta(O, b, nb, status, excl, agg, !E.fast);
+    }
+  }
+  __syncthreads();
+  CSTAMP(A, b, 4);
+  if (L.st != PBL_OK) return;
+  const Src S = slot_src(E, A);
+  if (E.fast) col_emit_rows<true>(L, E, A, schema, S);
+  else col_emit_rows<false>(L, E, A, schema, S);
+}
+
+// ---- the persistent kernel ----------------------------------------------------------
+__global__ void __launch_bounds__(kTPB, 4) colblk_pipe_kernel(Args A) {
+  __shared__ CLds L;
+  const int t = threadIdx.x;
+  const uint32_t nb = A.in.n_blocks;
+  const uint32_t schema = A.in.format;
+  uint32_t* tick = reinterpret_cast<uint32_t*>(A.out.workspace);
+  if (t == 0) {
+    const uint32_t t0 = g_atomic_add(tick, 1u);
+    L.s[1].mode = kNone;
+    L.s[1].b = nb;
+    if (t0 < nb) {
+      slot_setup(L.s[0], t0, to_glb(A.in.block_off)[t0], to_glb(A.in.block_len)[t0]);
+      L.nxt = g_atomic_add(tick, 1u);
+    } else {
+      L.s[0].b = nb;
+      L.s[0].mode = kNone;
+      L.nxt = nb;
+    }
+  }
+  __syncthreads();
+  if (L.s[0].b < nb) {
+    if (L.s[0].shift == (L.s[0].boff & 15)) {
+      ColPf pf;
+      pf.load(A.in.blocks, L.s[0].boff, L.s[0].blen);
+      pf.store(L.s[0], L.s[0].boff, L.s[0].blen);
+    } else {
+      slot_stage_funnel(L.s[0], A);
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = 0;; i++) {
+    Slot& P = L.s[i & 1];
+    Slot& E = L.s[(i + 1) & 1];
+    const uint32_t cb = P.b, nx = L.nxt;
+    if (cb >= nb && E.mode == kNone) break;
+    uint64_t nx_off = 0;
+    uint32_t nx_len = 0;
+    if (nx < nb) {
+      nx_off = to_glb(A.in.block_off)[nx];
+      nx_len = to_glb(A.in.block_len)[nx];
+    }
+    const bool pf_on = nx < nb && (nx_off & 7) == 0;
+    ColPf pf;
+    if (cb < nb) col_parse(L, P, A, schema);
+    __syncthreads();
+    if (pf_on) pf.load(A.in.blocks, nx_off, nx_len);  // lands during the emit
+    if (E.mode != kNone) col_emit(L, E, A, schema);
+    __syncthreads();
+    if (t == 0) slot_setup(E, nx < nb ? nx : nb, nx_off, nx_len);
+    if (pf_on) pf.store(E, nx_off, nx_len);
+    __syncthreads();
+    if (nx < nb && !pf_on) slot_stage_funnel(E, A);
+    if (t == 0) L.nxt = nx < nb ? g_atomic_add(tick, 1u) : nb;
+    __syncthreads();
+  }
+}
+
+}  // namespace cpipe
+}  // namespace col
+}  // namespace pbl

@@ -275,9 +275,10 @@ struct Args {
 
 // Store 16 bytes (w) covering global bytes [ga, ga+16) of which only [lo, hi)
 // belong to this block: one dwordx4 store when whole, byte stores at the edges.
-__device__ inline void store16(uint8_t* base, uint64_t ga, uint64_t lo, uint64_t hi, uint4 w) {
+__device__ inline void store16(uint8_t* base_, uint64_t ga, uint64_t lo, uint64_t hi, uint4 w) {
+  const gptr<uint8_t> base = to_glb(base_);
   if (ga >= lo && ga + 16 <= hi) {
-    *reinterpret_cast<uint4*>(base + ga) = w;
+    *(gptr<u32x4>)(base + ga) = u32x4{w.x, w.y, w.z, w.w};
     return;
   }
 #pragma unroll
