@@ -272,9 +272,31 @@ __device__ __forceinline__ uint32_t parse_block_wave(const Src& S, uint32_t sche
   if (l == 0) D->rows = rows;
   uint64_t s = 0, nx = 0, e = 0;
   bool ok = true;
-  uint32_t c = 0xffffffffu;  // this lane's column
-  if (uint32_t(l) < nsc + 5) c = uint32_t(l);
-  if (c == 0) {  // key column 0: PrefixBytes ("empty PrefixBytes" panics for 0 rows)
+  const uint32_t c = uint32_t(l);  // this lane's column (lanes >= nsc + 5 idle)
+  // one branch per column KIND (divergent lanes of one kind run together):
+  // Uint (crdb1 wall / logical, trailers), Bool (prefixChanged, isValueExternal,
+  // isObsolete), Bytes (untyped versions or suffixes, values), PrefixBytes
+  const bool is_uint = c == nsc || (schema == PBL_FMT_COL_CRDB1 && (c == 1 || c == 2));
+  const bool is_bool = c == nsc + 1 || c == nsc + 3 || c == nsc + 4;
+  const bool is_bytes = c == nsc - 1 || c == nsc + 2;
+  if (is_uint) {
+    UCol* u = c == nsc ? &D->trailers : c == 1 ? &D->wall : &D->logical;
+    ok = dir.column(S, c, kDtUint, &s, &nx) && dec_uints(S, s, rows, u, &e) && e == nx;
+  } else if (is_bool) {
+    uint32_t* at = c == nsc + 1 ? &D->pc_at : c == nsc + 3 ? &D->ext_at : &D->obs_at;
+    ok = dir.column(S, c, kDtBool, &s, &nx) && dec_bitmap(S, s, rows, at, &e) && e == nx;
+  } else if (is_bytes) {
+    const bool vals = c == nsc + 2;
+    UCol* o = vals ? &D->v_off : &D->rb_off;
+    uint32_t* data = vals ? &D->v_data : &D->rb_data;
+    ok = dir.column(S, c, kDtBytes, &s, &nx) && dec_rawbytes(S, s, rows, o, data, &e) && e == nx;
+    if (ok && vals) {
+      D->key_end = uint32_t(s);
+      const UCol& vo = D->v_off;
+      D->v_lo = vo.w ? uint32_t(S.le_u(vo.at, vo.w)) : 0;
+      D->v_hi = vo.w ? uint32_t(S.le_u(vo.at + rows * vo.w, vo.w)) : 0;
+    }
+  } else if (c == 0) {  // key column 0: PrefixBytes ("empty PrefixBytes" panics for 0 rows)
     ok = dir.column(S, 0, kDtPrefix, &s, &nx) && rows != 0 && s < S.len;
     if (ok) {
       const uint32_t sh = S.byte(uint32_t(s));
@@ -290,26 +312,6 @@ __device__ __forceinline__ uint32_t parse_block_wave(const Src& S, uint32_t sche
         }
       }
     }
-  } else if (schema == PBL_FMT_COL_CRDB1 && (c == 1 || c == 2)) {
-    ok = dir.column(S, c, kDtUint, &s, &nx) && dec_uints(S, s, rows, c == 1 ? &D->wall : &D->logical, &e) && e == nx;
-  } else if (c == nsc - 1) {  // untyped versions (crdb1) / suffixes (default)
-    ok = dir.column(S, c, kDtBytes, &s, &nx) && dec_rawbytes(S, s, rows, &D->rb_off, &D->rb_data, &e) && e == nx;
-  } else if (c == nsc) {
-    ok = dir.column(S, c, kDtUint, &s, &nx) && dec_uints(S, s, rows, &D->trailers, &e) && e == nx;
-  } else if (c == nsc + 1) {
-    ok = dir.column(S, c, kDtBool, &s, &nx) && dec_bitmap(S, s, rows, &D->pc_at, &e) && e == nx;
-  } else if (c == nsc + 2) {
-    ok = dir.column(S, c, kDtBytes, &s, &nx) && dec_rawbytes(S, s, rows, &D->v_off, &D->v_data, &e) && e == nx;
-    if (ok) {
-      D->key_end = uint32_t(s);
-      const UCol& vo = D->v_off;
-      D->v_lo = vo.w ? uint32_t(S.le_u(vo.at, vo.w)) : 0;
-      D->v_hi = vo.w ? uint32_t(S.le_u(vo.at + rows * vo.w, vo.w)) : 0;
-    }
-  } else if (c == nsc + 3) {
-    ok = dir.column(S, c, kDtBool, &s, &nx) && dec_bitmap(S, s, rows, &D->ext_at, &e) && e == nx;
-  } else if (c == nsc + 4) {
-    ok = dir.column(S, c, kDtBool, &s, &nx) && dec_bitmap(S, s, rows, &D->obs_at, &e) && e == nx;
   }
   if (__ballot(!ok)) return PBL_CORRUPT_COLBLK_HEADER;
   wave_sync();

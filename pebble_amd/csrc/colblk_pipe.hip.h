@@ -189,7 +189,8 @@ __device__ __forceinline__ void col_parse(CLds& L, Slot& P, const Args& A, uint3
 
 // ---- emit phase (whole workgroup) --------------------------------------------------
 template <bool F>
-__device__ __forceinline__ void col_emit_rows(CLds& L, const Slot& E, const Args& A, uint32_t schema, const Src& S) {
+__device__ __forceinline__ void col_emit_rows(CLds& L, const Slot& E, const Args& A, uint32_t schema, const Src& S,
+                                              bool prebuilt, uint32_t ex0, uint32_t tot0) {
   const int t = threadIdx.x;
   const pbl_decode_out& O = A.out;
   const uint32_t b = E.b;
@@ -229,7 +230,16 @@ __device__ __forceinline__ void col_emit_rows(CLds& L, const Slot& E, const Args
   // aligned 16-B granules (keys past the buffer go straight to global memory)
   lds_u8 kb8 = (lds_u8)to_lds(L.key4);
   uint32_t cbase = 0;
-  for (uint32_t c = 0; c < nch; c++) {
+  if (prebuilt) {
+    // single chunk, built in LDS while wave 0 resolved the look-back
+    if (uint32_t(t) < rows) key_off[kvb + b + t] = ex0;
+    const uint64_t lo = kbb, hi = kbb + tot0;
+    const lds_cu32 W = (lds_cu32)to_lds(L.key4);
+    for (uint64_t ga = (lo & ~uint64_t(15)) + 16ull * t; ga < hi; ga += 16ull * kTPB)
+      store16(O.key_bytes, ga, lo, hi, lds_bytes16(W, uint32_t(kKeyPad + ga - lo)));
+    cbase = tot0;
+  }
+  for (uint32_t c = 0; c < (prebuilt ? 0u : nch); c++) {
     const uint32_t r = c * kChunk + t;
     RowParts p;
     p.klen = 0;
@@ -290,13 +300,30 @@ __device__ __forceinline__ void col_emit_rows(CLds& L, const Slot& E, const Args
   CSTAMP(A, b, 7);
 }
 
-__device__ __forceinline__ void col_emit(CLds& L, const Slot& E, const Args& A, uint32_t schema) {
+template <bool F>
+__device__ __forceinline__ void col_emit_t(CLds& L, const Slot& E, const Args& A, uint32_t schema) {
   const uint32_t nb = A.in.n_blocks;
   const pbl_decode_out& O = A.out;
   uint8_t* ws = reinterpret_cast<uint8_t*>(O.workspace);
   uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
   const uint32_t b = E.b;
+  const int t = threadIdx.x;
+  const Src S = slot_src(E, A);
   CSTAMP(A, b, 3);
+  // keys of a single-chunk block are built in LDS (base-independent) by waves
+  // 1-3 while wave 0 resolves the look-back; wave 0 builds its rows afterwards
+  const bool okb = E.status == PBL_OK;
+  const uint32_t rows = okb ? E.d.rows : 0;
+  const bool prebuilt = okb && rows <= kChunk && E.tot0 <= kKeyBuf;
+  RowParts p;
+  p.klen = 0;
+  uint32_t ex = 0, tot = 0;
+  if (prebuilt) {
+    if (uint32_t(t) < rows) p = row_parts<F>(S, E.d, schema, uint32_t(t));
+    uint32_t de, dt;
+    block_excl_scan2(p.klen, 0u, &ex, &de, L.scratch, &tot, &dt);
+    if (wave_id() != 0 && uint32_t(t) < rows) build_key<F>(S, E.d, schema, p, (lds_u8)to_lds(L.key4), kKeyPad + ex);
+  }
   if (wave_id() == 0) {
     const uint64_t agg[kNumComp] = {E.agg[0], E.agg[1], E.agg[2], E.agg[3]};
     uint64_t excl[kNumComp];
@@ -313,13 +340,17 @@ __device__ __forceinline__ void col_emit(CLds& L, const Slot& E, const Args& A, 
       }
       write_block_meta(O, b, nb, status, excl, agg, !E.fast);
     }
+    if (prebuilt && uint32_t(t) < rows) build_key<F>(S, E.d, schema, p, (lds_u8)to_lds(L.key4), kKeyPad + ex);
   }
   __syncthreads();
   CSTAMP(A, b, 4);
   if (L.st != PBL_OK) return;
-  const Src S = slot_src(E, A);
-  if (E.fast) col_emit_rows<true>(L, E, A, schema, S);
-  else col_emit_rows<false>(L, E, A, schema, S);
+  col_emit_rows<F>(L, E, A, schema, S, prebuilt, ex, tot);
+}
+
+__device__ __forceinline__ void col_emit(CLds& L, const Slot& E, const Args& A, uint32_t schema) {
+  if (E.fast) col_emit_t<true>(L, E, A, schema);
+  else col_emit_t<false>(L, E, A, schema);
 }
 
 // ---- the persistent kernel ----------------------------------------------------------
