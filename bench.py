@@ -103,7 +103,7 @@ def main():
     elif a.workload == "col":
         fmt = N.PBL_FMT_COL_CRDB1
         buf, off, lens, n_kv = gen_col_blocks(seed, nb, a.block_size, n_threads=16)
-        kernel = "colblk_decode_kernel"
+        kernel = "colblk_decode_kernel" if os.environ.get("PBL_COL_KERNEL") == "single" else "colblk_pipe_kernel"
         wl = (f"config3: {nb} x {a.block_size // 1024} KiB colblk blocks per GPU, cockroachkvs crdb1 schema "
               f"(KeyGenConfig alphabet 26, RoachKeyLen 12, PrefixLenShared 4, 1 key/prefix), 128 B values")
     else:
@@ -185,7 +185,7 @@ def main():
     ab = alg_bytes(hres, nb, input_bytes)
     achieved = ab / (kern_ms * 1e-3) / 1e9
     traffic = None
-    tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    tp = os.path.join(ROOT, "profiles", "pmc_traffic.json" if a.workload == "row" else f"pmc_traffic_{a.workload}.json")
     if os.path.exists(tp):
         try:
             with open(tp) as f:

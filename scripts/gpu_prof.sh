@@ -2,7 +2,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/prof
 R="rocprofv3 --output-format csv"
-P="python3 scripts/prof_decode.py 65536 5"
+P="python3 scripts/prof_decode.py 65536 5 ${PROF_WORKLOAD:-row}"
 timeout -k 10 300 rocprofv3 -L > gpurun_out/prof/counters_list.txt 2>&1; \
 timeout -k 10 300 $R --kernel-trace --stats -d gpurun_out/prof/trace -o trace -- $P > gpurun_out/prof/trace.log 2>&1 && \
 timeout -k 10 300 $R --pmc FETCH_SIZE -d gpurun_out/prof/fetch -o fetch -- $P > gpurun_out/prof/fetch.log 2>&1 && \

@@ -17,11 +17,12 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
-src = os.path.join(ROOT, "gpurun_out", "prof")
+src = os.environ.get("PROF_SRC", os.path.join(ROOT, "gpurun_out", "prof"))
 dst = os.path.join(ROOT, "profiles")
 os.makedirs(dst, exist_ok=True)
 KERNEL = sys.argv[2] if len(sys.argv) > 2 else "rowblk_pipe_kernel"
 NB = int(sys.argv[3]) if len(sys.argv) > 3 else 65536
+WORKLOAD = sys.argv[4] if len(sys.argv) > 4 else "row"
 
 shutil.copy(os.path.join(src, "trace", "trace_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
 pmc = collections.defaultdict(list)
@@ -40,11 +41,11 @@ if "FETCH_SIZE" in means and "WRITE_SIZE" in means:
     fetch = means["FETCH_SIZE"] * 2 * 1024
     write = means["WRITE_SIZE"] * 1024
     out["hbm_bytes_per_launch"] = fetch + write
-    json.dump({"kernel": KERNEL, "workload_blocks": NB, "block_size": 32768,
+    json.dump({"kernel": KERNEL, "workload": WORKLOAD, "workload_blocks": NB, "block_size": 32768,
                "fetch_bytes_corrected": fetch, "write_bytes": write,
                "hbm_bytes_per_launch": fetch + write,
                "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes; FETCH_SIZE(KiB)x2x1024 "
                          "(gfx950 16-B/lane streaming-read correction), WRITE_SIZE(KiB)x1024",
-               "source": f"profiles/{tag}_pmc.json"}, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
+               "source": f"profiles/{tag}_pmc.json"}, open(os.path.join(dst, "pmc_traffic.json" if WORKLOAD == "row" else f"pmc_traffic_{WORKLOAD}.json"), "w"), indent=1)
 json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
