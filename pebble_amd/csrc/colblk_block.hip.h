@@ -255,65 +255,144 @@ __device__ __forceinline__ uint32_t parse_block(const Src& S, uint32_t schema, D
   return PBL_OK;
 }
 
-// Same decode, one lane per column (wave 0, all 64 lanes call it): each lane
-// reads its directory entry and decodes its column's encoding; the statuses
-// combine by ballot exactly as the serial order would (every header failure is
-// PBL_CORRUPT_COLBLK_HEADER; the final bounds check is PBL_CORRUPT_BOUNDS).
-// Lane 0 writes the shared fields; each column lane writes its own fields.
+// Same decode, one lane per column (wave 0, all 64 lanes call it), in uniform
+// stages so that every lane issues the same reads: (1) its directory entry
+// (Dir::column), (2) the encoding bytes at its column's start, (3) per-kind
+// arithmetic restating dec_uints / dec_bitmap / dec_rawbytes, (4) the first and
+// last offsets of offset-bearing columns.  Every read is bounds-guarded; the
+// statuses combine by ballot exactly as the serial order would (every header
+// failure is PBL_CORRUPT_COLBLK_HEADER; the final bounds check is
+// PBL_CORRUPT_BOUNDS).  Lane 0 writes the shared fields; each column lane its own.
+__device__ __forceinline__ uint32_t sbyte(const Src& S, uint64_t o) { return o < S.len ? S.byte(uint32_t(o)) : 0u; }
+__device__ __forceinline__ uint64_t sle(const Src& S, uint64_t o, uint32_t w) {
+  return (w && o + w <= S.len) ? S.le_u(uint32_t(o), w) : 0ull;
+}
+__device__ __forceinline__ bool uint_width_ok(uint32_t w, bool delta) {
+  return w == 0 || w == 1 || w == 2 || w == 4 || (w == 8 && !delta);
+}
+
 __device__ __forceinline__ uint32_t parse_block_wave(const Src& S, uint32_t schema, Desc* D) {
   const int l = lane_id();
   if (schema != PBL_FMT_COL_DEFAULT && schema != PBL_FMT_COL_CRDB1) return PBL_UNSUPPORTED;
   const uint32_t nsc = schema == PBL_FMT_COL_CRDB1 ? 4 : 2;
-  Dir dir;
-  dir.custom = 4 + (schema == PBL_FMT_COL_CRDB1 ? 1 : 0);
-  if (S.len < dir.custom + 7) return PBL_CORRUPT_COLBLK_HEADER;
-  dir.ncols = uint32_t(S.le_u(dir.custom + 1, 2));
-  const uint32_t rows = uint32_t(S.le_u(dir.custom + 3, 4));
+  const uint32_t custom = 4 + (schema == PBL_FMT_COL_CRDB1 ? 1 : 0);
+  if (S.len < custom + 7) return PBL_CORRUPT_COLBLK_HEADER;
+  const uint32_t ncols = uint32_t(S.le_u(custom + 1, 2));
+  const uint32_t rows = uint32_t(S.le_u(custom + 3, 4));
   if (l == 0) D->rows = rows;
-  uint64_t s = 0, nx = 0, e = 0;
-  bool ok = true;
-  const uint32_t c = uint32_t(l);  // this lane's column (lanes >= nsc + 5 idle)
-  // one branch per column KIND (divergent lanes of one kind run together):
-  // Uint (crdb1 wall / logical, trailers), Bool (prefixChanged, isValueExternal,
-  // isObsolete), Bytes (untyped versions or suffixes, values), PrefixBytes
-  const bool is_uint = c == nsc || (schema == PBL_FMT_COL_CRDB1 && (c == 1 || c == 2));
-  const bool is_bool = c == nsc + 1 || c == nsc + 3 || c == nsc + 4;
-  const bool is_bytes = c == nsc - 1 || c == nsc + 2;
-  if (is_uint) {
-    UCol* u = c == nsc ? &D->trailers : c == 1 ? &D->wall : &D->logical;
-    ok = dir.column(S, c, kDtUint, &s, &nx) && dec_uints(S, s, rows, u, &e) && e == nx;
-  } else if (is_bool) {
-    uint32_t* at = c == nsc + 1 ? &D->pc_at : c == nsc + 3 ? &D->ext_at : &D->obs_at;
-    ok = dir.column(S, c, kDtBool, &s, &nx) && dec_bitmap(S, s, rows, at, &e) && e == nx;
-  } else if (is_bytes) {
-    const bool vals = c == nsc + 2;
-    UCol* o = vals ? &D->v_off : &D->rb_off;
-    uint32_t* data = vals ? &D->v_data : &D->rb_data;
-    ok = dir.column(S, c, kDtBytes, &s, &nx) && dec_rawbytes(S, s, rows, o, data, &e) && e == nx;
-    if (ok && vals) {
-      D->key_end = uint32_t(s);
-      const UCol& vo = D->v_off;
-      D->v_lo = vo.w ? uint32_t(S.le_u(vo.at, vo.w)) : 0;
-      D->v_hi = vo.w ? uint32_t(S.le_u(vo.at + rows * vo.w, vo.w)) : 0;
+  const uint32_t c = uint32_t(l);
+  const bool active = c < nsc + 5;
+  // column kinds: 0 Uint, 1 Bool, 2 Bytes, 3 PrefixBytes
+  const bool crdb = schema == PBL_FMT_COL_CRDB1;
+  const uint32_t kind = c == 0 ? 3u
+                        : (c == nsc || (crdb && (c == 1 || c == 2))) ? 0u
+                        : (c == nsc + 1 || c == nsc + 3 || c == nsc + 4) ? 1u
+                        : 2u;
+  const uint32_t want = kind == 0 ? uint32_t(kDtUint) : kind == 1 ? uint32_t(kDtBool)
+                        : kind == 2 ? uint32_t(kDtBytes) : uint32_t(kDtPrefix);
+  // (1) directory entry: Dir::column
+  const uint64_t h = uint64_t(custom) + 7 + 5ull * c;
+  const uint32_t typ = sbyte(S, h);
+  const uint64_t start = sle(S, h + 1, 4);
+  const uint64_t nxt_raw = sle(S, h + 6, 4);
+  const bool last_col = c + 1 >= ncols;
+  const uint64_t nx = last_col ? uint64_t(S.len) - 1 : nxt_raw;
+  bool ok = c < ncols && h + 5 <= S.len && typ == want && (last_col || h + 10 <= S.len) && nx <= S.len &&
+            start <= nx;
+  // (2) encoding bytes at the column start (PrefixBytes: its shift byte, then
+  // the offsets' Uint encoding one byte later)
+  const uint64_t u0 = kind == 3 ? start + 1 : start;   // Uint encoding byte of this column
+  const uint32_t b_shift = sbyte(S, start);
+  const uint32_t enc = sbyte(S, u0);
+  const uint64_t base8 = sle(S, u0 + 1, 8);
+  // (3) per kind
+  uint32_t cnt = rows;  // value count (Uint) / slice count (Bytes, Prefix)
+  uint32_t shift = 0, nbund = 0;
+  if (kind == 3) {
+    ok = ok && rows != 0 && start < S.len;
+    shift = b_shift;
+    ok = ok && shift <= 16;
+    nbund = ok ? 1 + ((rows - 1) >> shift) : 0;
+    cnt = rows + nbund;
+  }
+  uint64_t at = 0, end = 0, base = 0;
+  uint32_t w = 0;
+  if (kind == 1) {  // dec_bitmap
+    ok = ok && start < S.len;
+    if (enc == 1) {
+      at = 0;
+      end = start + 1;
+    } else {
+      const uint64_t off = (start + 1 + 7) & ~uint64_t(7);
+      const uint64_t nw = (uint64_t(rows) + 63) >> 6, ns = (nw + 63) >> 6;
+      at = off;
+      end = off + 8 * (nw + ns);
+      ok = ok && end <= S.len;
     }
-  } else if (c == 0) {  // key column 0: PrefixBytes ("empty PrefixBytes" panics for 0 rows)
-    ok = dir.column(S, 0, kDtPrefix, &s, &nx) && rows != 0 && s < S.len;
-    if (ok) {
-      const uint32_t sh = S.byte(uint32_t(s));
-      D->pb_shift = sh;
-      ok = sh <= 16;
-      if (ok) {
-        const uint32_t nbund = 1 + ((rows - 1) >> sh);
-        ok = dec_rawbytes(S, s + 1, rows + nbund, &D->pb_off, &D->pb_data, &e) && e == nx;
-        if (ok) {
-          const UCol& po = D->pb_off;
-          D->shared_len = po.w ? uint32_t(S.le_u(po.at, po.w)) : 0;
-          D->data_len = po.w ? uint32_t(S.le_u(po.at + (rows + nbund) * po.w, po.w)) : 0;
-        }
+  } else {  // dec_uints over cnt (+1 for offset columns) values at u0
+    const uint32_t nvals = kind == 0 ? cnt : cnt + 1;
+    if (nvals == 0) {
+      at = u0;
+      end = u0;
+    } else {
+      ok = ok && u0 < S.len;
+      w = enc & 0x7f;
+      const bool delta = (enc & 0x80) != 0;
+      ok = ok && uint_width_ok(w, delta);
+      uint64_t off = u0 + 1;
+      if (delta) {
+        ok = ok && off + 8 <= S.len;
+        base = base8;
+        off += 8;
       }
+      if (w) off = (off + w - 1) & ~uint64_t(w - 1);
+      at = off;
+      end = off + uint64_t(nvals) * w;
+      if (kind != 0) ok = ok && base == 0 && w != 8 && end <= S.len;  // DecodeUnsafeOffsets
     }
   }
-  if (__ballot(!ok)) return PBL_CORRUPT_COLBLK_HEADER;
+  // (4) first and last offsets of offset-bearing columns
+  const uint64_t first = (kind >= 2 && w) ? sle(S, at, w) : 0;
+  const uint64_t lastv = (kind >= 2 && w) ? sle(S, at + uint64_t(cnt) * w, w) : 0;
+  uint64_t data = 0;
+  if (kind >= 2) {
+    data = end;            // RawBytes data start
+    end = end + lastv;     // RawBytes end
+    ok = ok && end <= S.len;
+  }
+  ok = ok && end == nx;
+  if (active && ok) {
+    UCol u;
+    u.base = base;
+    u.w = w;
+    u.at = uint32_t(at);
+    if (kind == 3) {
+      D->pb_shift = shift;
+      D->pb_off = u;
+      D->pb_data = uint32_t(data);
+      D->shared_len = uint32_t(first);
+      D->data_len = uint32_t(lastv);
+    } else if (kind == 0) {
+      if (c == nsc) D->trailers = u;
+      else if (c == 1) D->wall = u;
+      else D->logical = u;
+    } else if (kind == 1) {
+      const uint32_t a32 = uint32_t(at);
+      if (c == nsc + 1) D->pc_at = a32;
+      else if (c == nsc + 3) D->ext_at = a32;
+      else D->obs_at = a32;
+    } else if (c == nsc + 2) {
+      D->v_off = u;
+      D->v_data = uint32_t(data);
+      D->key_end = uint32_t(start);
+      D->v_lo = uint32_t(first);
+      D->v_hi = uint32_t(lastv);
+    } else {
+      D->rb_off = u;
+      D->rb_data = uint32_t(data);
+    }
+  }
+  if (__ballot(active && !ok)) return PBL_CORRUPT_COLBLK_HEADER;
   wave_sync();
   if (D->shared_len > D->data_len || D->v_lo > D->v_hi) return PBL_CORRUPT_BOUNDS;
   return PBL_OK;
