@@ -125,6 +125,32 @@ __device__ __forceinline__ void slot_stage_funnel(Slot& P, const Args& A) {
   stage((lds_u4)to_lds(P.tail4), A.in.blocks, P.boff, a1, P.tail_lo, P.blen - P.tail_lo);
 }
 
+// Resolve block E.b's exclusive prefix and write its block metadata (one wave:
+// wave 1, at the start of the iteration, concurrently with wave 0's header
+// decode of the next block).  Leaves the bases and the status in L.
+__device__ __forceinline__ void col_resolve(CLds& L, const Slot& E, const Args& A) {
+  const uint32_t nb = A.in.n_blocks;
+  const pbl_decode_out& O = A.out;
+  uint8_t* ws = reinterpret_cast<uint8_t*>(O.workspace);
+  uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
+  const uint32_t b = E.b;
+  const uint64_t agg[kNumComp] = {E.agg[0], E.agg[1], E.agg[2], E.agg[3]};
+  uint64_t excl[kNumComp];
+  lb_resolve(lb_state, nb, b, agg, excl, &O.totals->status_mask);
+  if (lane_id() == 0) {
+    uint32_t status = E.status;
+    if (status == PBL_OK && overflows(O, excl, agg)) status = PBL_OVERFLOW;
+    L.st = status;
+#pragma unroll
+    for (int c = 0; c < kNumComp; c++) L.bases[c] = excl[c];
+    if (status != PBL_OK && excl[0] + b < O.kv_cap + nb) {
+      to_glb(O.key_off)[excl[0] + b] = 0;
+      to_glb(O.val_off)[excl[0] + b] = 0;
+    }
+    write_block_meta(O, b, nb, status, excl, agg, !E.fast);
+  }
+}
+
 // ---- parse phase (whole workgroup) ------------------------------------------------
 template <bool F>
 __device__ __forceinline__ void col_parse_rows(CLds& L, Slot& P, const Args& A, uint32_t schema, const Src& S) {
@@ -169,10 +195,11 @@ __device__ __forceinline__ void col_parse_rows(CLds& L, Slot& P, const Args& A, 
   }
 }
 
-__device__ __forceinline__ void col_parse(CLds& L, Slot& P, const Args& A, uint32_t schema) {
+__device__ __forceinline__ void col_parse(CLds& L, Slot& P, const Slot& E, const Args& A, uint32_t schema) {
   const Src S = slot_src(P, A);
   CSTAMP(A, P.b, 0);
-  if (wave_id() == 0) {
+  if (wave_id() == 1 && E.mode != kNone) col_resolve(L, E, A);
+  if (wave_id() == 0 && P.b < A.in.n_blocks) {
     const uint32_t st = parse_block_wave(S, schema, &P.d);
     if (lane_id() == 0) {
       L.bad = 0;
@@ -180,6 +207,7 @@ __device__ __forceinline__ void col_parse(CLds& L, Slot& P, const Args& A, uint3
     }
   }
   __syncthreads();
+  if (P.b >= A.in.n_blocks) return;
   if (threadIdx.x == 0) P.fast = P.status == PBL_OK && P.d.key_end <= P.nhead;
   CSTAMP(A, P.b, 1);
   if (P.status == PBL_OK && P.d.key_end <= P.nhead) col_parse_rows<true>(L, P, A, schema, S);
@@ -300,21 +328,17 @@ __device__ __forceinline__ void col_emit_rows(CLds& L, const Slot& E, const Args
   CSTAMP(A, b, 7);
 }
 
+// Emit (whole workgroup) of block E.b, whose prefix col_resolve left in L.
 template <bool F>
 __device__ __forceinline__ void col_emit_t(CLds& L, const Slot& E, const Args& A, uint32_t schema) {
-  const uint32_t nb = A.in.n_blocks;
-  const pbl_decode_out& O = A.out;
-  uint8_t* ws = reinterpret_cast<uint8_t*>(O.workspace);
-  uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
   const uint32_t b = E.b;
   const int t = threadIdx.x;
   const Src S = slot_src(E, A);
   CSTAMP(A, b, 3);
-  // keys of a single-chunk block are built in LDS (base-independent) by waves
-  // 1-3 while wave 0 resolves the look-back; wave 0 builds its rows afterwards
-  const bool okb = E.status == PBL_OK;
-  const uint32_t rows = okb ? E.d.rows : 0;
-  const bool prebuilt = okb && rows <= kChunk && E.tot0 <= kKeyBuf;
+  if (L.st != PBL_OK) return;
+  // keys of a single-chunk block are built in LDS first (one scan + one barrier)
+  const uint32_t rows = E.d.rows;
+  const bool prebuilt = rows <= kChunk && E.tot0 <= kKeyBuf;
   RowParts p;
   p.klen = 0;
   uint32_t ex = 0, tot = 0;
@@ -322,29 +346,10 @@ __device__ __forceinline__ void col_emit_t(CLds& L, const Slot& E, const Args& A
     if (uint32_t(t) < rows) p = row_parts<F>(S, E.d, schema, uint32_t(t));
     uint32_t de, dt;
     block_excl_scan2(p.klen, 0u, &ex, &de, L.scratch, &tot, &dt);
-    if (wave_id() != 0 && uint32_t(t) < rows) build_key<F>(S, E.d, schema, p, (lds_u8)to_lds(L.key4), kKeyPad + ex);
+    if (uint32_t(t) < rows) build_key<F>(S, E.d, schema, p, (lds_u8)to_lds(L.key4), kKeyPad + ex);
+    __syncthreads();
   }
-  if (wave_id() == 0) {
-    const uint64_t agg[kNumComp] = {E.agg[0], E.agg[1], E.agg[2], E.agg[3]};
-    uint64_t excl[kNumComp];
-    lb_resolve(lb_state, nb, b, agg, excl, &O.totals->status_mask);
-    if (lane_id() == 0) {
-      uint32_t status = E.status;
-      if (status == PBL_OK && overflows(O, excl, agg)) status = PBL_OVERFLOW;
-      L.st = status;
-#pragma unroll
-      for (int c = 0; c < kNumComp; c++) L.bases[c] = excl[c];
-      if (status != PBL_OK && excl[0] + b < O.kv_cap + nb) {
-        to_glb(O.key_off)[excl[0] + b] = 0;
-        to_glb(O.val_off)[excl[0] + b] = 0;
-      }
-      write_block_meta(O, b, nb, status, excl, agg, !E.fast);
-    }
-    if (prebuilt && uint32_t(t) < rows) build_key<F>(S, E.d, schema, p, (lds_u8)to_lds(L.key4), kKeyPad + ex);
-  }
-  __syncthreads();
   CSTAMP(A, b, 4);
-  if (L.st != PBL_OK) return;
   col_emit_rows<F>(L, E, A, schema, S, prebuilt, ex, tot);
 }
 
@@ -366,11 +371,9 @@ __global__ void __launch_bounds__(kTPB, 4) colblk_pipe_kernel(Args A) {
     L.s[1].b = nb;
     if (t0 < nb) {
       slot_setup(L.s[0], t0, to_glb(A.in.block_off)[t0], to_glb(A.in.block_len)[t0]);
-      L.nxt = g_atomic_add(tick, 1u);
     } else {
       L.s[0].b = nb;
       L.s[0].mode = kNone;
-      L.nxt = nb;
     }
   }
   __syncthreads();
@@ -387,8 +390,15 @@ __global__ void __launch_bounds__(kTPB, 4) colblk_pipe_kernel(Args A) {
   for (uint32_t i = 0;; i++) {
     Slot& P = L.s[i & 1];
     Slot& E = L.s[(i + 1) & 1];
-    const uint32_t cb = P.b, nx = L.nxt;
+    const uint32_t cb = P.b;
     if (cb >= nb && E.mode == kNone) break;
+    // the next ticket is taken now (its latency overlaps the parse): tickets are
+    // held for one iteration only, which keeps the look-back distance short
+    if (t == 0) L.nxt = cb < nb ? g_atomic_add(tick, 1u) : nb;
+    ColPf pf;
+    col_parse(L, P, E, A, schema);  // (wave 1 first resolves E's prefix)
+    __syncthreads();
+    const uint32_t nx = L.nxt;
     uint64_t nx_off = 0;
     uint32_t nx_len = 0;
     if (nx < nb) {
@@ -396,9 +406,6 @@ __global__ void __launch_bounds__(kTPB, 4) colblk_pipe_kernel(Args A) {
       nx_len = to_glb(A.in.block_len)[nx];
     }
     const bool pf_on = nx < nb && (nx_off & 7) == 0;
-    ColPf pf;
-    if (cb < nb) col_parse(L, P, A, schema);
-    __syncthreads();
     if (pf_on) pf.load(A.in.blocks, nx_off, nx_len);  // lands during the emit
     if (E.mode != kNone) col_emit(L, E, A, schema);
     __syncthreads();
@@ -406,7 +413,6 @@ __global__ void __launch_bounds__(kTPB, 4) colblk_pipe_kernel(Args A) {
     if (pf_on) pf.store(E, nx_off, nx_len);
     __syncthreads();
     if (nx < nb && !pf_on) slot_stage_funnel(E, A);
-    if (t == 0) L.nxt = nx < nb ? g_atomic_add(tick, 1u) : nb;
     __syncthreads();
   }
 }

@@ -176,7 +176,7 @@ __device__ inline uint64_t lb_poll(uint64_t* p, uint64_t want, uint32_t* spins, 
 }
 
 __device__ inline void lb_resolve(uint64_t* st, uint32_t n_blocks, uint32_t v, const uint64_t agg[kNumComp],
-                                  uint64_t excl[kNumComp], uint32_t* timeout_flag) {
+                                  uint64_t excl[kNumComp], uint32_t* timeout_flag, uint32_t* stats = nullptr) {
   const int l = lane_id();
   uint64_t* word = st;
   uint64_t* pfx = st + n_blocks;
@@ -186,7 +186,9 @@ __device__ inline void lb_resolve(uint64_t* st, uint32_t n_blocks, uint32_t v, c
   bool done = v == 0;
   uint32_t spins = 0;
   bool timed_out = false;
+  uint32_t rounds = 0;
   while (!done && !timed_out) {
+    rounds++;
     uint64_t g[kLbWin];
 #pragma unroll
     for (int k = 0; k < kLbWin; k++) {
@@ -244,6 +246,10 @@ __device__ inline void lb_resolve(uint64_t* st, uint32_t n_blocks, uint32_t v, c
     }
   }
   if (timed_out && l == 0) g_atomic_or(timeout_flag, 1u << PBL_TIMEOUT);
+  if (stats) {
+    stats[0] = rounds;
+    stats[1] = spins;
+  }
 #pragma unroll
   for (int q = 0; q < kNumComp; q++) excl[q] = wave_sum(acc[q]);
   if (v > 0) {

@@ -30,3 +30,7 @@ for nm, a, z in [("parse: header", 0, 1), ("parse: rows + publish", 1, 2), ("par
     d = (st[m, z] - st[m, a]).astype(np.float64)
     if d.size:
         print(f"{nm:24s} median {np.median(d):9.0f} mean {np.mean(d):9.0f} p90 {np.percentile(d, 90):9.0f} cycles")
+r = st[:, 10]
+sp = st[:, 11]
+print("look-back rounds: median", np.median(r), "mean", r.mean(), "max", r.max(), "| spins: median", np.median(sp),
+      "mean", sp.mean(), "p90", np.percentile(sp, 90))
