@@ -7,7 +7,10 @@ BASELINE.json config 2 per GPU: 64 Ki x 32 KiB row-format blocks, restart
 interval 16, 16 B user keys / 100 B values.  `--workload col` is config 3
 (64 Ki x 32 KiB colblk blocks, cockroachkvs crdb1 schema, 22 B keys / 128 B
 values); `--workload mixed` is config 4's per-GPU shard (128 Ki blocks, even
-ids row / odd ids colblk, 1 Mi blocks over 8 GPUs).  With
+ids row / odd ids colblk, 1 Mi blocks over 8 GPUs); `--workload zipf` is
+config 5 per GPU (64 Ki variable-length blocks targeting 32 KiB, Zipf(1.1) key
+lengths 8-1024 B and value lengths 0-64 KiB, `--restart-interval` 1/16/32,
+`--zipf-format row|col`).  With
 N > 1 (torch.distributed.run, one rank per GPU, RCCL) every rank decodes its own
 64 Ki-block shard (weak scaling) and each step also performs the offset concat:
 an all-gather of per-rank totals and the rebase of the per-block bases.
@@ -40,13 +43,15 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", choices=["row", "col", "mixed"], default="row")
+    p.add_argument("--workload", choices=["row", "col", "mixed", "zipf"], default="row")
     p.add_argument("--blocks", type=int, default=0, help="blocks per GPU (0 = the workload's config)")
     p.add_argument("--block-size", type=int, default=32768)
     p.add_argument("--restart-interval", type=int, default=16)
     p.add_argument("--key-len", type=int, default=16)
     p.add_argument("--val-len", type=int, default=100)
     p.add_argument("--value-prefix", action="store_true")
+    p.add_argument("--zipf-format", choices=["row", "col"], default="row",
+                   help="config 5 block format (col = colblk DefaultKeySchema)")
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     p.add_argument("--cpu-threads", type=int, default=16)
@@ -106,6 +111,15 @@ def main():
         kernel = "colblk_decode_kernel" if os.environ.get("PBL_COL_KERNEL") == "single" else "colblk_pipe_kernel"
         wl = (f"config3: {nb} x {a.block_size // 1024} KiB colblk blocks per GPU, cockroachkvs crdb1 schema "
               f"(KeyGenConfig alphabet 26, RoachKeyLen 12, PrefixLenShared 4, 1 key/prefix), 128 B values")
+    elif a.workload == "zipf":
+        from pebble_amd.batch import gen_zipf_blocks
+        fmt = N.PBL_FMT_ROW if a.zipf_format == "row" else N.PBL_FMT_COL_DEFAULT
+        buf, off, lens, n_kv = gen_zipf_blocks(seed, nb, fmt, a.restart_interval, a.block_size, n_threads=16)
+        kernel = "rowblk_pipe_kernel" if fmt == N.PBL_FMT_ROW else "colblk_pipe_kernel"
+        wl = (f"config5: {nb} variable-length blocks per GPU targeting {a.block_size // 1024} KiB, "
+              + (f"row format, restart interval {a.restart_interval}" if fmt == N.PBL_FMT_ROW
+                 else "colblk DefaultKeySchema")
+              + ", Zipf(1.1) key lengths 8-1024 B / value lengths 0-64 KiB")
     else:
         fmt = N.PBL_FMT_ROW
         h = nb // 2
@@ -234,7 +248,8 @@ def main():
             m_bytes += float(pl.astype(np.int64).sum()) * mr
             reps_used.append(reps)
         src = {N.PBL_FMT_ROW: "oracle/rowblk_oracle.c (rowblk.Iter)",
-               N.PBL_FMT_COL_CRDB1: "oracle/colblk_oracle.c (colblk.DataBlockIter, crdb1)"}
+               N.PBL_FMT_COL_CRDB1: "oracle/colblk_oracle.c (colblk.DataBlockIter, crdb1)",
+               N.PBL_FMT_COL_DEFAULT: "oracle/colblk_oracle.c (colblk.DataBlockIter, DefaultKeySchema)"}
         res["cpu_baseline"] = {
             "value": round(it_bytes / it_sec / 2**30, 2), "unit": "GiB/s", "cores": th, "kind": "port",
             "sample": f"first {ns} blocks of each format in the batch x {reps_used} passes "
@@ -245,7 +260,7 @@ def main():
             "host_cpu": _cpu_model(), "seconds": round(it_sec, 2),
         }
 
-    if a.e2e and rank == 0:
+    if a.e2e and rank == 0 and a.workload != "zipf":  # (fixed-stride chunking only)
         res["e2e_pcie"] = e2e_rate(buf, off, lens, flags, dev, cap, fmt, block_fmt)
 
     res["gen_seconds"] = round(gen_s, 2)

@@ -255,6 +255,30 @@ uint64_t pbl_gen_col_blocks(const pbl_colgen_config* cfg, uint32_t schema, uint3
                             uint32_t block_size, uint8_t* dst, uint64_t* block_off,
                             uint32_t* block_len, int n_threads);
 
+/* Config 5 (BASELINE.json configs[4]): Zipf(s)-skewed key and value lengths. */
+typedef struct pbl_zipf_config {
+  uint64_t seed;
+  uint32_t key_min, key_max;   /* user-key length range, key_min >= 8 (8, 1024)  */
+  uint32_t val_min, val_max;   /* value length range (0, 65536)                   */
+  double s;                    /* Zipf exponent (1.1)                             */
+  uint32_t block_size;         /* target block size; a block always takes its
+                                  first KV, so one large KV may exceed it         */
+  int32_t restart_interval;    /* row format only (1, 16, 32)                     */
+} pbl_zipf_config;
+
+/*
+ * Synthetic config-5 batch in host memory: format PBL_FMT_ROW (rowblk.Writer)
+ * or PBL_FMT_COL_DEFAULT (DataBlockEncoder + DefaultKeySchema).  Key of row k of
+ * block b: 8 base-26 letters of (b << 20) + k, then random letters to its Zipf
+ * length; trailer MakeTrailer((b << 20) + k, SET); random value bytes.  Blocks
+ * are variable-length, packed at 8-B alignment into dst; *bytes_used is the
+ * packed size.  Returns total KVs, or UINT64_MAX on a bad config or when
+ * dst_cap < *bytes_used (nothing copied).
+ */
+uint64_t pbl_gen_zipf_blocks(const pbl_zipf_config* cfg, uint32_t format, uint32_t n_blocks,
+                             uint8_t* dst, uint64_t dst_cap, uint64_t* block_off, uint32_t* block_len,
+                             uint64_t* bytes_used, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -70,6 +70,14 @@ class ColGenConfigC(ctypes.Structure):
     ]
 
 
+class ZipfConfigC(ctypes.Structure):
+    _fields_ = [
+        ("seed", ctypes.c_uint64), ("key_min", ctypes.c_uint32), ("key_max", ctypes.c_uint32),
+        ("val_min", ctypes.c_uint32), ("val_max", ctypes.c_uint32), ("s", ctypes.c_double),
+        ("block_size", ctypes.c_uint32), ("restart_interval", ctypes.c_int32),
+    ]
+
+
 class TotalsC(ctypes.Structure):
     _fields_ = [
         ("n_kv", ctypes.c_uint64), ("key_bytes", ctypes.c_uint64),
@@ -125,6 +133,8 @@ SIGNATURES = {
     "pbl_colblk_writer_finish": (ctypes.c_size_t, [_vp, ctypes.c_uint32, _vp, ctypes.c_size_t]),
     "pbl_gen_col_blocks": (ctypes.c_uint64, [ctypes.POINTER(ColGenConfigC), ctypes.c_uint32, ctypes.c_uint32,
                                              ctypes.c_uint32, _vp, _vp, _vp, ctypes.c_int]),
+    "pbl_gen_zipf_blocks": (ctypes.c_uint64, [ctypes.POINTER(ZipfConfigC), ctypes.c_uint32, ctypes.c_uint32,
+                                              _vp, ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_int]),
 }
 
 _lib = None

@@ -236,3 +236,29 @@ def offset_concat(out: DecodedBatch, rank_totals: torch.Tensor, rank: int, strea
                                _stream_handle(stream))
     if rc != N.PBL_OK:
         raise DecodeError(f"pbl_offset_concat failed: {N.STATUS_NAMES.get(rc, rc)}")
+
+
+def gen_zipf_blocks(seed: int, n_blocks: int, fmt: int = 0, restart_interval: int = 16, block_size: int = 32768,
+                    key_min: int = 8, key_max: int = 1024, val_min: int = 0, val_max: int = 65536, s: float = 1.1,
+                    n_threads: int = 0):
+    """Config 5 (BASELINE.json configs[4]): Zipf(s) key lengths in [key_min, key_max]
+    and value lengths in [val_min, val_max], variable-length blocks packed at 8-B
+    alignment (`pbl_gen_zipf_blocks`).  fmt is PBL_FMT_ROW or PBL_FMT_COL_DEFAULT.
+    Returns (buf, off, lens, n_kv) with buf padded by 16 zero bytes."""
+    import ctypes
+    import os
+    cfg = N.ZipfConfigC(seed, key_min, key_max, val_min, val_max, s, block_size, restart_interval)
+    nt = n_threads or min(16, os.cpu_count() or 1)
+    off = np.empty(n_blocks, np.uint64)
+    lens = np.empty(n_blocks, np.uint32)
+    used = ctypes.c_uint64(0)
+    # worst case: every block is its target plus one maximal KV
+    cap = n_blocks * (block_size + key_max + val_max + 64)
+    buf = np.empty(cap + 16, np.uint8)
+    n = N.lib().pbl_gen_zipf_blocks(ctypes.byref(cfg), fmt, n_blocks, buf.ctypes.data, cap, off.ctypes.data,
+                                    lens.ctypes.data, ctypes.byref(used), nt)
+    if n == (1 << 64) - 1:
+        raise ValueError(f"pbl_gen_zipf_blocks: bad config or capacity ({used.value} > {cap})")
+    buf = buf[: used.value + 16].copy()
+    buf[used.value:] = 0
+    return buf, off, lens, int(n)

@@ -24,6 +24,7 @@
 // Blocks whose restart table is inconsistent with a per-run walk, or that do
 // not fit the LDS limits, take the general path (rowblk_general.hip.h): a
 // wave-serial restatement of Iter.First/Next, bit-identical by construction.
+#include <algorithm>
 #include <stdlib.h>
 #include <string.h>
 
@@ -561,7 +562,7 @@ __device__ __forceinline__ void row_process(Lds& s, const Args& A, const uint32_
     uint32_t status = PBL_OK;
     if (wave_id() == 0) {
       uint64_t dummy[kNumComp] = {0, 0, 0, 0};
-      slow_walk(src, blen, flags, keybuf, keycap, 0, A.out, b, dummy, &ss);
+      slow_walk(src, fits, blen, flags, keybuf, keycap, 0, A.out, b, dummy, &ss);
       bool ok = ss.status == PBL_OK;
       agg[0] = ok ? ss.nkv : 0;
       agg[1] = ok ? ss.kb : 0;
@@ -579,7 +580,7 @@ __device__ __forceinline__ void row_process(Lds& s, const Args& A, const uint32_
     }
     if (wave_id() != 0) return;
     if (status == PBL_OK) {
-      slow_walk(src, blen, flags, keybuf, keycap, 1, A.out, b, excl, &ss);
+      slow_walk(src, fits, blen, flags, keybuf, keycap, 1, A.out, b, excl, &ss);
     } else if (lane_id() == 0 && excl[0] + b < O.kv_cap + nb) {
       O.key_off[excl[0] + b] = 0;
       O.val_off[excl[0] + b] = 0;
@@ -857,8 +858,15 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
     if (grid > batch->n_blocks) grid = batch->n_blocks;
     if (single)
       hipLaunchKernelGGL(pbl::row::rowblk_decode_kernel, dim3(uint32_t(grid)), dim3(pbl::kTPB), 0, st, a);
-    else
+    else {
+      // sizes of the blocks past the LDS stage first (one wave each, all at once)
+      hipLaunchKernelGGL(pbl::row::pipe::big_block_sizes_kernel, dim3(uint32_t(std::min<uint64_t>(
+                             batch->n_blocks, uint64_t(cus > 0 ? cus : 1) * 4))), dim3(pbl::kWave), 0, st, a);
       hipLaunchKernelGGL(pbl::row::pipe::rowblk_pipe_kernel, dim3(uint32_t(grid)), dim3(pbl::kTPB), 0, st, a);
+      // then their value bytes (all big blocks at once, bandwidth-bound)
+      hipLaunchKernelGGL(pbl::row::pipe::big_block_values_kernel, dim3(uint32_t(std::min<uint64_t>(
+                             batch->n_blocks, uint64_t(cus > 0 ? cus : 1) * 4))), dim3(pbl::kWave), 0, st, a);
+    }
   }
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }

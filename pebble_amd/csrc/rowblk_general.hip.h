@@ -31,35 +31,115 @@ __device__ inline uint32_t g_le32(const uint8_t* p) {
   return uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 | uint32_t(p[3]) << 24;
 }
 
-// pass 0 counts; pass 1 writes outputs at the given bases.
-__device__ __noinline__ void slow_walk(const uint8_t* blk, uint64_t len, uint32_t flags, uint8_t* keybuf,
-                          uint32_t keycap, int pass, const pbl_decode_out O, uint32_t b,
-                          const uint64_t* bases, SlowState* st) {
+// Block sources of the general path.  Both read bytes, LE32 words and 16-byte
+// windows at block offsets; an ld16 window may start up to 15 bytes before the
+// block or end past it (those bytes are don't-cares; nothing outside the
+// block's 16-B granules is touched).  Typed address spaces throughout: a
+// generic (FLAT) LDS read would wait for every outstanding global store.
+struct SlowLds {  // block staged in LDS (byte 0 at B[base])
+  View V;
+  __device__ __forceinline__ uint32_t byte(uint64_t i) const { return V.byte(uint32_t(i)); }
+  __device__ __forceinline__ uint32_t le32(uint64_t i) const { return V.le32(uint32_t(i)); }
+  __device__ __forceinline__ uint4 ld16(int64_t i) const { return V.ld16(int32_t(i)); }
+};
+struct SlowGlb {  // block in global memory
+  gptr<const uint8_t> g;
+  uint64_t len;
+  __device__ __forceinline__ uint32_t byte(uint64_t i) const { return g[i]; }
+  __device__ __forceinline__ uint32_t le32(uint64_t i) const {
+    return uint32_t(g[i]) | uint32_t(g[i + 1]) << 8 | uint32_t(g[i + 2]) << 16 | uint32_t(g[i + 3]) << 24;
+  }
+  __device__ __forceinline__ uint4 ld16(int64_t i) const {
+    const uint64_t s0 = uint64_t(g), s1 = s0 + len, sx = s0 + uint64_t(i), sa = sx & ~uint64_t(15);
+    const uint32_t sh = uint32_t(sx - sa);
+    uint4 x = make_uint4(0, 0, 0, 0), y = make_uint4(0, 0, 0, 0);
+    if (sa + 16 > s0 && sa < s1) {
+      const u32x4 v = *(gptr<const u32x4>)(sa);
+      x = make_uint4(v.x, v.y, v.z, v.w);
+    }
+    if (sh && sa + 32 > s0 && sa + 16 < s1) {
+      const u32x4 v = *(gptr<const u32x4>)(sa + 16);
+      y = make_uint4(v.x, v.y, v.z, v.w);
+    }
+    return sh ? col::funnel16(x, y, sh) : x;
+  }
+};
+
+// byte k (< 16) of a 16-byte window, by shifts (a runtime-indexed register
+// array would live in scratch)
+__device__ __forceinline__ uint32_t win_byte(const uint4& w, uint32_t k) {
+  const uint64_t q = k < 8 ? (uint64_t(w.x) | uint64_t(w.y) << 32) : (uint64_t(w.z) | uint64_t(w.w) << 32);
+  return uint32_t(q >> (8 * (k & 7))) & 0xffu;
+}
+
+// varint at window bytes [i0, n) (g_varint's rules: 5th byte << 28, none past n)
+__device__ __forceinline__ uint32_t w_varint(const uint4& w, uint32_t i0, uint32_t n, uint32_t* v) {
+  uint32_t r = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 5; i++) {
+    if (i0 + i >= n) return 0;
+    const uint32_t b = win_byte(w, i0 + i);
+    if (i == 4) { *v = r | (b << 28); return 5; }
+    if (b < 128) { *v = r | (b << (7 * i)); return i + 1; }
+    r |= (b & 0x7f) << (7 * i);
+  }
+  return 0;
+}
+
+// Key buffer: LDS bytes with a 16-B front pad and a 32-B tail so that 16-B
+// gathers around the key stay inside it.
+constexpr uint32_t kKeyBufPad = 16, kKeyBufSlack = 48;
+
+// Walk passes: kPassCount counts; kPassAll writes every output at the given bases.
+enum { kPassCount = 0, kPassAll = 1 };
+
+#ifndef PBL_SLOW_U
+#define PBL_SLOW_U 1
+#endif
+
+// U: value granules per lane in flight.
+template <class Src, int U>
+__device__ __forceinline__ void slow_walk_t(const Src S, uint64_t len, uint32_t flags, lptr<uint8_t> kbuf,
+                                            uint32_t keycap, int pass, const pbl_decode_out& O, uint32_t b,
+                                            const uint64_t bases[kNumComp], SlowState* st) {
   const int l = lane_id();
-  const uint8_t* end = blk + len;
-  int32_t nr = int32_t(g_le32(blk + len - 4));
-  int64_t restarts = int64_t(len) - 4 * (1 + int64_t(nr));
-  const uint8_t* rtab = blk + restarts;
+  lptr<uint8_t> keybuf = kbuf + kKeyBufPad;
+  const lptr<const uint32_t> KW = (lptr<const uint32_t>)kbuf;
+  keycap = keycap > kKeyBufSlack ? keycap - kKeyBufSlack : 0;
+  const gptr<uint64_t> o_trailer = to_glb(O.trailer);
+  const gptr<uint8_t> o_flags = to_glb(O.kv_flags);
+  const gptr<uint32_t> o_entry = to_glb(O.entry_off), o_koff = to_glb(O.key_off), o_voff = to_glb(O.val_off);
+  const int32_t nr = int32_t(S.le32(len - 4));
+  const int64_t restarts = int64_t(len) - 4 * (1 + int64_t(nr));
   uint64_t nkv = 0, kb = 0, vb = 0, full_len = 0;
   int64_t offset = 0;
   uint32_t ri = 0;
   uint32_t status = PBL_OK;
   while (offset >= 0 && offset < restarts) {
-    const uint8_t* p = blk + offset;
+    // the header's bytes in one window, the three varints from registers
+    const uint4 hw = S.ld16(offset);
+    const uint32_t hn = uint32_t(min<int64_t>(15, int64_t(len) - offset));
     uint32_t shared, unshared, vlen;
-    uint32_t a = g_varint(p, end, &shared);
-    uint32_t bb = a ? g_varint(p + a, end, &unshared) : 0;
-    uint32_t c = bb ? g_varint(p + a + bb, end, &vlen) : 0;
+    const uint32_t a = w_varint(hw, 0, hn, &shared);
+    const uint32_t bb = a ? w_varint(hw, a, hn, &unshared) : 0;
+    const uint32_t c = bb ? w_varint(hw, a + bb, hn, &vlen) : 0;
     if (!c) { status = PBL_CORRUPT_BOUNDS; break; }
-    const uint8_t* kp = p + a + bb + c;
-    if (uint64_t(end - kp) < unshared) { status = PBL_CORRUPT_BOUNDS; break; }
-    const uint8_t* vp = kp + unshared;
-    if (uint64_t(end - vp) < vlen) { status = PBL_CORRUPT_BOUNDS; break; }
+    const uint64_t kp = uint64_t(offset) + a + bb + c;
+    if (len - kp < unshared) { status = PBL_CORRUPT_BOUNDS; break; }
+    const uint64_t vp = kp + unshared;
+    if (len - vp < vlen) { status = PBL_CORRUPT_BOUNDS; break; }
     if (shared > full_len) { status = PBL_CORRUPT_BOUNDS; break; }
-    uint64_t klen = uint64_t(shared) + unshared;
+    const uint64_t klen = uint64_t(shared) + unshared;
     if (klen > keycap) { status = PBL_UNSUPPORTED; break; }
     wave_sync();
-    for (uint32_t i = l; i < unshared; i += kWave) keybuf[shared + i] = kp[i];
+    // unshared key bytes -> keybuf[shared, klen): one 16-B window per lane step
+    for (uint32_t i0 = 16u * l; i0 < unshared; i0 += 16u * kWave) {
+      const uint4 w = S.ld16(int64_t(kp + i0));
+      const uint32_t n = min(16u, unshared - i0);
+#pragma unroll
+      for (uint32_t k = 0; k < 16; k++)
+        if (k < n) keybuf[shared + i0 + k] = uint8_t(win_byte(w, k));
+    }
     wave_sync();
     full_len = klen;
     uint64_t trailer, ukl;
@@ -69,6 +149,7 @@ __device__ __noinline__ void slow_walk(const uint8_t* blk, uint64_t len, uint32_
       ukl = klen;
     } else if (klen >= 8) {
       uint64_t raw = 0;
+#pragma unroll
       for (int i = 0; i < 8; i++) raw |= uint64_t(keybuf[klen - 8 + i]) << (8 * i);
       if (raw & 64u) fl |= PBL_KV_OBSOLETE;
       trailer = raw & kTrailerObsoleteMask;
@@ -78,51 +159,93 @@ __device__ __noinline__ void slow_walk(const uint8_t* blk, uint64_t len, uint32_
       ukl = 0;
       fl |= PBL_KV_INVALID_KEY;
     }
-    const uint8_t* v = vp;
-    uint64_t vl = vlen;
+    uint64_t v = vp, vl = vlen;
     if ((flags & PBL_ROW_VALUE_PREFIX) && !(flags & PBL_ROW_RAW_KEYS) && (trailer & 0xff) == 1) {
       if (vl == 0) { status = PBL_CORRUPT_BOUNDS; break; }
-      uint8_t pre = v[0];
+      const uint32_t pre = S.byte(v);
       if ((pre & 0xC0) == 0 || (flags & PBL_ROW_NO_VALUER)) { v++; vl--; }
       else if ((pre & 0xC0) == 0x80) fl |= PBL_KV_VALBLK_HANDLE;
       else fl |= PBL_KV_BLOB_HANDLE;
     }
-    while (ri < uint32_t(nr) && int64_t(g_le32(rtab + 4 * ri) & kRestartMask) < offset) ri++;
-    if (ri < uint32_t(nr) && int64_t(g_le32(rtab + 4 * ri) & kRestartMask) == offset) {
-      fl |= PBL_KV_RESTART;
-      if (g_le32(rtab + 4 * ri) & 0x80000000u) fl |= PBL_KV_RESTART_SAMEPFX;
-    }
-    if (pass == 1) {
-      uint64_t kv = bases[0] + nkv, o = bases[0] + b + nkv;
-      if (l == 0) {
-        O.trailer[kv] = trailer;
-        if (O.kv_flags) O.kv_flags[kv] = fl;
-        if (O.entry_off) O.entry_off[kv] = uint32_t(offset);
-        O.key_off[o] = uint32_t(kb);
-        O.val_off[o] = uint32_t(vb);
+    if (pass == kPassAll) {
+      while (ri < uint32_t(nr) && int64_t(S.le32(uint64_t(restarts) + 4 * ri) & kRestartMask) < offset) ri++;
+      if (ri < uint32_t(nr)) {
+        const uint32_t rw = S.le32(uint64_t(restarts) + 4 * ri);
+        if (int64_t(rw & kRestartMask) == offset) {
+          fl |= PBL_KV_RESTART;
+          if (rw & 0x80000000u) fl |= PBL_KV_RESTART_SAMEPFX;
+        }
       }
-      uint8_t* kd = O.key_bytes + bases[1] + kb;
-      for (uint64_t i = l; i < ukl; i += kWave) kd[i] = keybuf[i];
-      uint8_t* vd = O.val_bytes + bases[2] + vb;
-      for (uint64_t i = l; i < vl; i += kWave) vd[i] = v[i];
+      const uint64_t kv = bases[0] + nkv, o = bases[0] + b + nkv;
+      if (l == 0) {
+        o_trailer[kv] = trailer;
+        if (O.kv_flags) o_flags[kv] = fl;
+        if (O.entry_off) o_entry[kv] = uint32_t(offset);
+        o_koff[o] = uint32_t(kb);
+        o_voff[o] = uint32_t(vb);
+      }
+      // user key: 16-B destination granules gathered from the key buffer
+      {
+        const uint64_t lo = bases[1] + kb, hi = lo + ukl;
+        for (uint64_t ga = (lo & ~uint64_t(15)) + 16ull * l; ga < hi; ga += 16ull * kWave)
+          store16(O.key_bytes, ga, lo, hi, lds_gather16(KW, uint32_t(int64_t(kKeyBufPad) + int64_t(ga - lo))));
+      }
+    }
+    if (pass == kPassAll) {
+      // value: 16-B destination granules from source windows, U per lane in flight
+      const uint64_t lo = bases[2] + vb, hi = lo + vl;
+      for (uint64_t g0 = (lo & ~uint64_t(15)) + 16ull * l; g0 < hi; g0 += 16ull * kWave * U) {
+        uint4 w[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const uint64_t ga = g0 + 16ull * kWave * u;
+          w[u] = ga < hi ? S.ld16(int64_t(v) + int64_t(ga - lo)) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const uint64_t ga = g0 + 16ull * kWave * u;
+          if (ga < hi) store16(O.val_bytes, ga, lo, hi, w[u]);
+        }
+      }
     }
     nkv++;
     kb += ukl;
     vb += vl;
-    offset = int64_t(vp - blk) + vlen;
+    offset = int64_t(vp) + vlen;
   }
   if (status == PBL_OK && (kb >> 32 || vb >> 32)) status = PBL_UNSUPPORTED;
-  if (pass == 1 && status == PBL_OK) {
-    uint64_t o = bases[0] + b + nkv;
-    if (l == 0) { O.key_off[o] = uint32_t(kb); O.val_off[o] = uint32_t(vb); }
-    if (O.restarts)
-      for (int32_t r = l; r < nr; r += kWave) O.restarts[bases[3] + r] = g_le32(rtab + 4 * r);
+  if (pass == kPassAll && status == PBL_OK) {
+    const uint64_t o = bases[0] + b + nkv;
+    if (l == 0) { o_koff[o] = uint32_t(kb); o_voff[o] = uint32_t(vb); }
+    if (O.restarts) {
+      const gptr<uint32_t> o_rst = to_glb(O.restarts);
+      for (int32_t r = l; r < nr; r += kWave) o_rst[bases[3] + r] = S.le32(uint64_t(restarts) + 4ull * r);
+    }
   }
   st->status = status;
   st->nkv = nkv;
   st->kb = kb;
   st->vb = vb;
   st->nr = uint64_t(nr);
+}
+
+// blk: the block's first byte, in LDS (staged, blk_lds) or global memory;
+// keybuf: LDS (dword aligned) of keycap bytes.
+__device__ __noinline__ void slow_walk(const uint8_t* blk, bool blk_lds, uint64_t len, uint32_t flags,
+                                       uint8_t* keybuf, uint32_t keycap, int pass, const pbl_decode_out O,
+                                       uint32_t b, const uint64_t* bases_p, SlowState* st) {
+  const uint64_t bases[kNumComp] = {bases_p[0], bases_p[1], bases_p[2], bases_p[3]};
+  const lptr<uint8_t> kbuf = to_lds_ptr(keybuf);
+  if (blk_lds) {
+    // View base: the 16-B granule below the block's own granule (ld16 windows
+    // start up to 15 bytes early; the staging buffers carry a 16-B front pad)
+    const uint32_t a = uint32_t(uint64_t(to_lds_ptr(blk)));
+    const uint32_t base = 16u + (a & 15u);
+    slow_walk_t<SlowLds, PBL_SLOW_U>(SlowLds{lds_view(reinterpret_cast<const void*>(blk - base), base)}, len, flags,
+                                     kbuf, keycap, pass, O, b, bases, st);
+  } else {
+    slow_walk_t<SlowGlb, PBL_SLOW_U>(SlowGlb{to_glb(blk), len}, len, flags, kbuf, keycap, pass, O, b, bases, st);
+  }
 }
 
 

@@ -48,7 +48,7 @@ namespace pipe {
 #endif
 
 constexpr int kKv = 400;                       // KVs (and runs) per block on the pipelined path
-constexpr uint32_t kKeyCap = 16384;            // user-key bytes per block on the pipelined path
+constexpr uint32_t kKeyCap = 32768;            // user-key bytes per block on the pipelined path
 constexpr int kBs = 7;                         // output bucket = 128 bytes
 constexpr int kKBkt = kKeyCap >> kBs;          // key buckets
 constexpr int kVBkt = kMaxFastLen >> kBs;      // value buckets (values <= block length)
@@ -90,6 +90,30 @@ static_assert(sizeof(PLds) <= 163840 / 2, "two pipelined workgroups per CU");
 // Entry header (rowblk_iter.go:345-398: three uint32 varints) decoded without
 // branches from the 8 bytes at the entry: each varint 1 or 2 bytes.  Returns
 // false if any needs 3+ bytes (value >= 16384: the block takes the general path).
+// Entry header: three uint32 varints decoded from one 8-byte window.  The
+// common 1-2 byte form is decoded inline; a 3-byte varint (values of 16 KiB and
+// more, config 5) takes hdr3 on the lanes that need it.  Anything longer takes
+// the general path.
+__device__ __forceinline__ bool hdr3(uint64_t w, uint32_t* sh, uint32_t* un, uint32_t* vl, uint32_t* h) {
+  uint32_t p = 0, v[3];
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const uint32_t x = uint32_t(w >> (8 * p));  // p <= 6 here
+    const uint32_t b0 = x & 0xff, b1 = (x >> 8) & 0xff, b2 = (x >> 16) & 0xff;
+    const bool c0 = (b0 & 0x80) != 0, c1 = c0 && (b1 & 0x80) != 0;
+    v[k] = c1 ? ((b0 & 0x7f) | ((b1 & 0x7f) << 7) | (b2 << 14)) : c0 ? ((b0 & 0x7f) | (b1 << 7)) : b0;
+    ok = ok && !(c1 && (b2 & 0x80));
+    p += c1 ? 3 : c0 ? 2 : 1;
+  }
+  *sh = v[0];
+  *un = v[1];
+  *vl = v[2];
+  *h = p;
+  // RunBuf packs unshared in 14 bits and the header length in 3
+  return ok && p <= 7 && v[1] < 16384u;
+}
+
 __device__ __forceinline__ bool hdr2(uint64_t w, uint32_t* sh, uint32_t* un, uint32_t* vl, uint32_t* h) {
   uint32_t p = 0, v[3];
   bool ok = true;
@@ -106,6 +130,7 @@ __device__ __forceinline__ bool hdr2(uint64_t w, uint32_t* sh, uint32_t* un, uin
   *un = v[1];
   *vl = v[2];
   *h = p;
+  if (__builtin_expect(!ok, 0)) ok = hdr3(w, sh, un, vl, h);
   return ok;
 }
 
@@ -126,7 +151,7 @@ __device__ __forceinline__ void run_count(const View& V, uint32_t r, uint32_t nr
   while (pos < e0) {
     uint32_t sh, un, vl, h;
     const bool hok = hdr2(V.ld8(pos), &sh, &un, &vl, &h);
-    const uint32_t np = pos + h + un + vl;  // < 2^18: no overflow
+    const uint32_t np = pos + h + un + vl;  // < 2^23: no overflow
     if (!hok || (cnt == 0 && sh != 0) || np > e0) { ok = false; return; }
     bad = bad || (cnt > 0 && sh > prev_kl);
     const uint32_t kl = sh + un;
@@ -363,31 +388,55 @@ __device__ __noinline__ void parse_slow(Meta& M, uint4* X, const Args A) {
   uint8_t* ws = reinterpret_cast<uint8_t*>(A.out.workspace);
   uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
     // ---- general path (wave-serial Iter.Next), resolving its own look-back --------
-    // key buffer: the meta slot's per-KV arrays; if a key outgrows it, re-run
-    // from global memory with the whole staging buffer as the key buffer
-    bool from_lds = fits;
-    uint8_t* keybuf = reinterpret_cast<uint8_t*>(&M);
-    uint32_t keycap = uint32_t(offsetof(Meta, boff));
-    const uint8_t* src = fits ? reinterpret_cast<const uint8_t*>(X) + kPad + (boff & 15) : gblk;
-    if (!fits) { keybuf = reinterpret_cast<uint8_t*>(X); keycap = uint32_t(kLdsBlkBytes); }
     SlowState ss;
-    uint64_t dummy[kNumComp] = {0, 0, 0, 0};
-    slow_walk(src, blen, flags, keybuf, keycap, 0, A.out, b, dummy, &ss);
-    if (ss.status == PBL_UNSUPPORTED && from_lds) {
-      from_lds = false;
-      src = gblk;
-      keybuf = reinterpret_cast<uint8_t*>(X);
-      keycap = uint32_t(kLdsBlkBytes);
-      slow_walk(src, blen, flags, keybuf, keycap, 0, A.out, b, dummy, &ss);
+    uint64_t excl[kNumComp];
+    if (!fits) {
+      // a block past the LDS stage: big_block_sizes_kernel walked it, published
+      // its aggregate and left {status, counts} in its block-metadata slots;
+      // big_block_values_kernel writes its outputs after this launch
+      ss.status = to_glb(A.out.blk_status)[b];
+      ss.nkv = to_glb(A.out.blk_kv_base)[b];
+      ss.kb = to_glb(A.out.blk_key_base)[b];
+      ss.vb = to_glb(A.out.blk_val_base)[b];
+      ss.nr = ss.status == PBL_OK ? SlowGlb{to_glb(gblk), blen}.le32(blen - 4) : 0;
+    } else {
+      // key buffer: the meta slot's per-KV arrays; if a key outgrows it, re-run
+      // from global memory with the whole staging buffer as the key buffer
+      const uint8_t* src = reinterpret_cast<const uint8_t*>(X) + kPad + (boff & 15);
+      uint64_t dummy[kNumComp] = {0, 0, 0, 0};
+      bool from_lds = true;
+      uint8_t* keybuf = reinterpret_cast<uint8_t*>(&M);
+      uint32_t keycap = uint32_t(offsetof(Meta, boff));
+      slow_walk(src, true, blen, flags, keybuf, keycap, kPassCount, A.out, b, dummy, &ss);
+      if (ss.status == PBL_UNSUPPORTED) {
+        from_lds = false;
+        src = gblk;
+        keybuf = reinterpret_cast<uint8_t*>(X);
+        keycap = uint32_t(kLdsBlkBytes);
+        slow_walk(src, false, blen, flags, keybuf, keycap, kPassCount, A.out, b, dummy, &ss);
+      }
+      const bool okk = ss.status == PBL_OK;
+      const uint64_t agg[kNumComp] = {okk ? ss.nkv : 0, okk ? ss.kb : 0, okk ? ss.vb : 0, okk ? ss.nr : 0};
+      lookback(lb_state, nb, b, agg, excl, &A.out.totals->status_mask);
+      uint32_t st2 = ss.status;
+      if (okk && overflows(A.out, excl, agg)) st2 = PBL_OVERFLOW;
+      if (st2 == PBL_OK) slow_walk(src, from_lds, blen, flags, keybuf, keycap, kPassAll, A.out, b, excl, &ss);
+      else if (l == 0 && excl[0] + b < A.out.kv_cap + nb) {
+        A.out.key_off[excl[0] + b] = 0;
+        A.out.val_off[excl[0] + b] = 0;
+      }
+      if (l == 0) {
+        write_block_meta(A.out, b, nb, st2, excl, agg, true);
+        M.mode = kModeDone;
+      }
+      return;
     }
     const bool okk = ss.status == PBL_OK;
-    uint64_t agg[kNumComp] = {okk ? ss.nkv : 0, okk ? ss.kb : 0, okk ? ss.vb : 0, okk ? ss.nr : 0};
-    uint64_t excl[kNumComp];
-    lookback(lb_state, nb, b, agg, excl, &A.out.totals->status_mask);
+    const uint64_t agg[kNumComp] = {okk ? ss.nkv : 0, okk ? ss.kb : 0, okk ? ss.vb : 0, okk ? ss.nr : 0};
+    lb_resolve(lb_state, nb, b, agg, excl, &A.out.totals->status_mask);
     uint32_t st2 = ss.status;
     if (okk && overflows(A.out, excl, agg)) st2 = PBL_OVERFLOW;
-    if (st2 == PBL_OK) slow_walk(src, blen, flags, keybuf, keycap, 1, A.out, b, excl, &ss);
-    else if (l == 0 && excl[0] + b < A.out.kv_cap + nb) {
+    if (st2 != PBL_OK && l == 0 && excl[0] + b < A.out.kv_cap + nb) {
       A.out.key_off[excl[0] + b] = 0;
       A.out.val_off[excl[0] + b] = 0;
     }
@@ -395,6 +444,78 @@ __device__ __noinline__ void parse_slow(Meta& M, uint4* X, const Args A) {
       write_block_meta(A.out, b, nb, st2, excl, agg, true);
       M.mode = kModeDone;
     }
+}
+
+// Size pass for the blocks past the LDS stage (blen > kMaxFastLen), one wave
+// per block, launched ahead of rowblk_pipe_kernel on the same stream.  Their
+// count walk reads global memory entry by entry; inside the pipeline it would
+// hold back the look-back of every later ticket.  Here all of them walk at
+// once and publish their aggregates, so the pipeline's parse_slow only
+// resolves.  Same init checks and the same slow_walk as parse_slow, so the
+// aggregate is the one parse_slow computes.
+__global__ void __launch_bounds__(kWave) big_block_sizes_kernel(Args A) {
+  __shared__ uint4 keybuf4[kLdsBlkBytes / 16];
+  const uint32_t nb = A.in.n_blocks, flags = A.in.flags;
+  uint8_t* ws = reinterpret_cast<uint8_t*>(A.out.workspace);
+  uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
+  // 64 lengths per wave per round; the big blocks among them one after another
+  for (uint64_t base = uint64_t(blockIdx.x) * kWave; base < nb; base += uint64_t(gridDim.x) * kWave) {
+   const uint64_t bl = base + lane_id();
+   uint64_t big = __ballot(bl < nb && to_glb(A.in.block_len)[bl] > kMaxFastLen);
+   while (big) {
+    const uint32_t b = uint32_t(base) + uint32_t(__builtin_ctzll(big));
+    big &= big - 1;
+    const uint32_t blen = A.in.block_len[b];
+    const uint8_t* gblk = A.in.blocks + A.in.block_off[b];
+    uint32_t roff, nres;
+    if (init_checks(GlbRd{gblk}, blen, flags, &roff, &nres) != PBL_OK) continue;  // (parse_block's error path publishes)
+    SlowState ss;
+    uint64_t dummy[kNumComp] = {0, 0, 0, 0};
+    slow_walk(gblk, false, blen, flags, reinterpret_cast<uint8_t*>(keybuf4), uint32_t(kLdsBlkBytes), 0, A.out, b, dummy,
+              &ss);
+    const bool okk = ss.status == PBL_OK;
+    const uint64_t agg[kNumComp] = {okk ? ss.nkv : 0, okk ? ss.kb : 0, okk ? ss.vb : 0, okk ? ss.nr : 0};
+    lb_publish(lb_state, nb, b, agg);
+    if (lane_id() == 0) {  // for parse_slow (write_block_meta replaces them)
+      g_atomic_add(reinterpret_cast<uint32_t*>(ws) + kWsBigCount, 1u);
+      to_glb(A.out.blk_status)[b] = ss.status;
+      to_glb(A.out.blk_kv_base)[b] = agg[0];
+      to_glb(A.out.blk_key_base)[b] = agg[1];
+      to_glb(A.out.blk_val_base)[b] = agg[2];
+    }
+   }
+  }
+}
+
+// Outputs of the blocks past the LDS stage, launched after rowblk_pipe_kernel
+// on the same stream (which resolved their bases into blk_*_base).  One wave
+// per block, all big blocks at once, 8 value granules per lane in flight: a big
+// value is HBM-bandwidth work, which a single wave inside the pipeline (each
+// granule behind the previous store's vmcnt) turned into latency-bound work,
+// and its serial walk would hold the workgroup's pipeline.
+__global__ void __launch_bounds__(kWave) big_block_values_kernel(Args A) {
+  __shared__ uint4 keybuf4[kLdsBlkBytes / 16];
+  const uint32_t nb = A.in.n_blocks, flags = A.in.flags;
+  // (the size pass counted the big blocks; usually there are none)
+  if (__hip_atomic_load(to_glb(reinterpret_cast<uint32_t*>(A.out.workspace) + kWsBigCount), __ATOMIC_RELAXED,
+                        __HIP_MEMORY_SCOPE_AGENT) == 0)
+    return;
+  for (uint64_t base = uint64_t(blockIdx.x) * kWave; base < nb; base += uint64_t(gridDim.x) * kWave) {
+    const uint64_t bl = base + lane_id();
+    uint64_t big = __ballot(bl < nb && to_glb(A.in.block_len)[bl] > kMaxFastLen &&
+                            to_glb(A.out.blk_status)[bl] == PBL_OK);
+    while (big) {
+      const uint32_t b = uint32_t(base) + uint32_t(__builtin_ctzll(big));
+      big &= big - 1;
+      const uint32_t blen = A.in.block_len[b];
+      const uint64_t bases[kNumComp] = {A.out.blk_kv_base[b], A.out.blk_key_base[b], A.out.blk_val_base[b],
+                                        A.out.blk_rst_base ? A.out.blk_rst_base[b] : 0};
+      SlowState ss;
+      slow_walk_t<SlowGlb, 8>(SlowGlb{to_glb(A.in.blocks + A.in.block_off[b]), blen}, blen, flags,
+                              to_lds_ptr(reinterpret_cast<uint8_t*>(keybuf4)), uint32_t(kLdsBlkBytes), kPassAll,
+                              A.out, b, bases, &ss);
+    }
+  }
 }
 
 // Parse stage: wave 0, block M.b staged in X (if it fits).
