@@ -141,13 +141,12 @@ struct RunAcc {
 // Pass 1 over run r: count entries and output bytes; `ok` clears if the run is
 // not walkable per run (general path), `bad` sets on shared > len(previous key)
 // (rowblk_iter.go:403), `vbad` on a SET value without its prefix byte.
-__device__ __forceinline__ void run_count(const View& V, uint32_t r, uint32_t nres, uint32_t roff, uint32_t flags,
-                                          bool vprefix, RunAcc& acc, bool& ok, bool& bad, bool& vbad) {
-  const uint32_t st = roff + 4 * r;
-  const uint32_t s0 = V.le32(st) & kRestartMask;
-  const uint32_t e0 = (r + 1 < nres) ? (V.le32(st + 4) & kRestartMask) : roff;
-  if (!((r != 0 || s0 == 0) && s0 < e0 && e0 <= roff)) { ok = false; return; }
-  uint32_t pos = s0, cnt = 0, prev_kl = 0;
+// Count entries [pos, e0) of a run whose first `cnt` entries were already
+// counted (prev_kl = the length of the last one).
+__device__ __forceinline__ void run_count_span(const View& V, uint32_t pos, uint32_t e0, uint32_t cnt,
+                                               uint32_t prev_kl, uint32_t flags, bool vprefix, RunAcc& acc,
+                                               bool& ok, bool& bad, bool& vbad) {
+  const uint32_t cnt0 = cnt;
   while (pos < e0) {
     uint32_t sh, un, vl, h;
     const bool hok = hdr2(V.ld8(pos), &sh, &un, &vl, &h);
@@ -169,19 +168,30 @@ __device__ __forceinline__ void run_count(const View& V, uint32_t r, uint32_t nr
     prev_kl = kl;
     pos = np;
   }
-  acc.cnt += cnt;
+  acc.cnt += cnt - cnt0;
+}
+
+__device__ __forceinline__ void run_count(const View& V, uint32_t r, uint32_t nres, uint32_t roff, uint32_t flags,
+                                          bool vprefix, RunAcc& acc, bool& ok, bool& bad, bool& vbad) {
+  const uint32_t st = roff + 4 * r;
+  const uint32_t s0 = V.le32(st) & kRestartMask;
+  const uint32_t e0 = (r + 1 < nres) ? (V.le32(st + 4) & kRestartMask) : roff;
+  if (!((r != 0 || s0 == 0) && s0 < e0 && e0 <= roff)) { ok = false; return; }
+  run_count_span(V, s0, e0, 0, 0, flags, vprefix, acc, ok, bad, vbad);
 }
 
 // Pass 2 over run r (validated by pass 1): per-KV metadata at final indices.
-__device__ __forceinline__ void run_write(Meta& M, const View& V, uint32_t r, uint32_t nres, uint32_t roff,
-                                          uint32_t flags, bool vprefix, RunAcc& acc) {
-  const uint32_t st = roff + 4 * r;
-  const uint32_t rw = V.le32(st);
-  const uint32_t s0 = rw & kRestartMask;
-  const uint32_t e0 = (r + 1 < nres) ? (V.le32(st + 4) & kRestartMask) : roff;
-  uint32_t pos = s0, j = acc.cnt, kb = acc.kb, vb = acc.vb;
-  uint32_t prev_sh = 0, pp = 0, ppsh = 0;
-  bool first = true;
+// Prefix-parent chain state carried from one entry of a run to the next.
+struct ParState {
+  uint32_t prev_sh, pp, ppsh;
+};
+
+// Write entries [pos, e0) of a run at final indices acc.cnt.. (P = the chain
+// state after the entries before pos; `first` = pos is the restart point).
+__device__ __forceinline__ void run_write_span(Meta& M, const View& V, uint32_t pos, uint32_t e0, uint32_t rw,
+                                               bool first, ParState P, uint32_t flags, bool vprefix, RunAcc& acc) {
+  uint32_t j = acc.cnt, kb = acc.kb, vb = acc.vb;
+  uint32_t prev_sh = P.prev_sh, pp = P.pp, ppsh = P.ppsh;
   while (pos < e0) {
     uint32_t sh, un, vl, h;
     hdr2(V.ld8(pos), &sh, &un, &vl, &h);
@@ -231,6 +241,15 @@ __device__ __forceinline__ void run_write(Meta& M, const View& V, uint32_t r, ui
   acc.vb = vb;
 }
 
+// Pass 2 over run r (validated by pass 1): per-KV metadata at final indices.
+__device__ __forceinline__ void run_write(Meta& M, const View& V, uint32_t r, uint32_t nres, uint32_t roff,
+                                          uint32_t flags, bool vprefix, RunAcc& acc) {
+  const uint32_t st = roff + 4 * r;
+  const uint32_t rw = V.le32(st);
+  const uint32_t e0 = (r + 1 < nres) ? (V.le32(st + 4) & kRestartMask) : roff;
+  run_write_span(M, V, rw & kRestartMask, e0, rw, true, ParState{0, 0, 0}, flags, vprefix, acc);
+}
+
 // Single-walk form of passes 1+2 for runs of at most kRunBuf entries (every
 // run of a block written with restart interval <= 16): the run is walked once,
 // each entry's header parked in two packed registers (static indices: no
@@ -242,6 +261,7 @@ struct RunBuf {
   uint32_t ea[kRunBuf];  // pos | shared << 16
   uint32_t eb[kRunBuf];  // unshared | header length << 14 | value length << 17
   uint32_t cnt, s0, rw;
+  uint32_t pos, e0, prev_kl;  // continuation of a run longer than kRunBuf (over)
 };
 
 // Walk run r once.  `ok` clears as in run_count; `over` sets if the run has more
@@ -289,13 +309,16 @@ __device__ __forceinline__ void run_walk(const View& V, uint32_t r, uint32_t nre
     }
   }
   if (go && pos < e0) over = true;
+  B.pos = pos;
+  B.e0 = e0;
+  B.prev_kl = prev_kl;
   B.cnt = cnt;
   acc.cnt += cnt;
 }
 
 // Write the parked entries of one run at final indices (acc = the run's bases).
 __device__ __forceinline__ void run_emit_meta(Meta& M, const View& V, const RunBuf& B, uint32_t flags, bool vprefix,
-                                              RunAcc acc) {
+                                              RunAcc& acc, ParState& P) {
   uint32_t j = acc.cnt, kb = acc.kb, vb = acc.vb;
   uint32_t prev_sh = 0, pp = 0, ppsh = 0;
 #pragma unroll
@@ -341,6 +364,8 @@ __device__ __forceinline__ void run_emit_meta(Meta& M, const View& V, const RunB
       j++;
     }
   }
+  acc = RunAcc{j, kb, vb};
+  P = ParState{prev_sh, pp, ppsh};
 }
 
 // Init checks (Init :248-256, readFirstKey :418-485) evaluated by every lane.
@@ -550,7 +575,9 @@ __device__ __forceinline__ void parse_block(Meta& M, uint4* X, const Args& A) {
       if (r0 < nres) run_walk(V, r0, nres, roff, flags, vprefix, RB, acc, ok, bad, vbad, over);
       else RB.cnt = 0;
     }
-    const bool walked = single && !__ballot(over);
+    // a run longer than kRunBuf keeps its parked head and counts only its tail
+    if (single && over && ok) run_count_span(V, RB.pos, RB.e0, RB.cnt, RB.prev_kl, flags, vprefix, acc, ok, bad, vbad);
+    const bool walked = single;
     if (!walked) {
       acc = RunAcc{0, 0, 0};
       ok = true; bad = false; vbad = false;
@@ -570,7 +597,11 @@ __device__ __forceinline__ void parse_block(Meta& M, uint4* X, const Args& A) {
       lb_publish(lb_state, nb, b, agg);
       published = true;
       RunAcc w{ic - acc.cnt, ik - acc.kb, iv - acc.vb};
-      if (walked) run_emit_meta(M, V, RB, flags, vprefix, w);
+      if (walked) {
+        ParState P;
+        run_emit_meta(M, V, RB, flags, vprefix, w, P);
+        if (over) run_write_span(M, V, RB.pos, RB.e0, RB.rw, false, P, flags, vprefix, w);
+      }
       else
         for (uint32_t r = r0; r < r1; r++) run_write(M, V, r, nres, roff, flags, vprefix, w);
       PSTAMP(A, b, 2, l == 0);

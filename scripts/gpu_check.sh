@@ -7,3 +7,4 @@ echo "== smoke" && timeout -k 10 300 python __graft_entry__.py smoke 2>&1 | grep
 echo "== bench row" && timeout -k 10 300 python bench.py --steps 10 --warmup 2 --cpu-baseline-seconds 5 --e2e 2>&1 | grep -v amdgpu.ids && \
 echo "== bench col" && timeout -k 10 300 python bench.py --workload col --steps 10 --warmup 2 --no-cpu-baseline 2>&1 | grep -v amdgpu.ids && \
 echo "== bench mixed" && timeout -k 10 300 python bench.py --workload mixed --steps 10 --warmup 2 --no-cpu-baseline 2>&1 | grep -v amdgpu.ids
+echo "== bench zipf" && timeout -k 10 300 python bench.py --workload zipf --steps 10 --warmup 2 --no-cpu-baseline 2>/dev/null | cut -c1-400

@@ -18,6 +18,12 @@ if workload == "col":
     from pebble_amd.colblk import gen_col_blocks
     buf, off, lens, n = gen_col_blocks(42, nb, 32768, n_threads=16)
     b = BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_COL_CRDB1, 0)
+elif workload == "zipf":
+    # config 5, row format, restart interval 16 (bench.py --workload zipf)
+    from pebble_amd import _native as N
+    from pebble_amd.batch import gen_zipf_blocks
+    buf, off, lens, n = gen_zipf_blocks(42, nb, N.PBL_FMT_ROW, 16, 32768, n_threads=16)
+    b = BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, 0)
 else:
     buf, off, lens, n = gen_row_blocks(42, nb, 32768, 16, 16, 100, n_threads=16)
     b = BlockBatch.from_host(buf, off, lens, "cuda")

@@ -95,7 +95,7 @@ def test_rowblk_iter_datadriven_on_gpu(golden, ri):
             assert run_iter_cmds(it, case["input"]) == case["expected"], case
 
 
-@pytest.mark.parametrize("ri", [1, 2, 16, 32])
+@pytest.mark.parametrize("ri", [1, 2, 16, 17, 32, 64])
 @pytest.mark.parametrize("kl,vl", [(16, 100), (8, 0), (64, 7), (24, 1000)])
 @pytest.mark.parametrize("vp", [False, True])
 def test_synthetic_batches(ri, kl, vl, vp):
