@@ -204,8 +204,10 @@ def main():
         try:
             with open(tp) as f:
                 pt = json.load(f)
+            same_zipf = a.workload != "zipf" or (pt.get("restart_interval") == a.restart_interval
+                                                  and pt.get("zipf_format") == a.zipf_format)
             if (pt.get("workload_blocks") == nb and pt.get("block_size") == a.block_size
-                    and pt.get("workload", "row") == a.workload):
+                    and pt.get("workload", "row") == a.workload and same_zipf):
                 traffic = pt.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
