@@ -115,7 +115,10 @@ def main():
         from pebble_amd.batch import gen_zipf_blocks
         fmt = N.PBL_FMT_ROW if a.zipf_format == "row" else N.PBL_FMT_COL_DEFAULT
         buf, off, lens, n_kv = gen_zipf_blocks(seed, nb, fmt, a.restart_interval, a.block_size, n_threads=16)
-        kernel = "rowblk_pipe_kernel" if fmt == N.PBL_FMT_ROW else "colblk_pipe_kernel"
+        from pebble_amd.batch import varlen_hint
+        # (a Zipf colblk batch carries PBL_BATCH_VARLEN: one-block-per-workgroup kernel)
+        kernel = ("rowblk_pipe_kernel" if fmt == N.PBL_FMT_ROW
+                  else "colblk_decode_kernel" if varlen_hint(lens) else "colblk_pipe_kernel")
         wl = (f"config5: {nb} variable-length blocks per GPU targeting {a.block_size // 1024} KiB, "
               + (f"row format, restart interval {a.restart_interval}" if fmt == N.PBL_FMT_ROW
                  else "colblk DefaultKeySchema")

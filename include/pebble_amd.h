@@ -67,6 +67,12 @@ enum {
 #define PBL_ROW_RAW_KEYS 0x4u     /* rowblk.RawIter semantics (rowblk_iter.go:1743-1794):
                                      keys are emitted whole, no trailer split, no
                                      first-key check; trailer[] = 0              */
+#define PBL_BATCH_VARLEN 0x100u   /* scheduling hint, no effect on results: block
+                                     lengths vary widely (e.g. Zipf value sizes), so a
+                                     colblk batch takes the one-block-per-workgroup
+                                     kernel, whose look-back does not convoy behind
+                                     long blocks.  The caller knows the lengths on the
+                                     host (block handles carry them).              */
 
 /* per-KV flag byte (kv_flags[]) */
 #define PBL_KV_RESTART 0x01u       /* entry offset is a restart point            */

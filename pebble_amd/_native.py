@@ -39,6 +39,7 @@ PBL_FMT_COL_CRDB1 = 2
 PBL_ROW_VALUE_PREFIX = 0x1
 PBL_ROW_NO_VALUER = 0x2
 PBL_ROW_RAW_KEYS = 0x4
+PBL_BATCH_VARLEN = 0x100
 
 PBL_KV_RESTART = 0x01
 PBL_KV_RESTART_SAMEPFX = 0x02

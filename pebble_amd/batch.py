@@ -30,6 +30,15 @@ class DecodeError(RuntimeError):
     pass
 
 
+def varlen_hint(lens: np.ndarray) -> int:
+    """PBL_BATCH_VARLEN when block lengths vary widely (coefficient of variation
+    above 0.25): a scheduling hint only (include/pebble_amd.h)."""
+    l = np.asarray(lens, dtype=np.float64)
+    if l.size < 2 or l.mean() <= 0:
+        return 0
+    return N.PBL_BATCH_VARLEN if l.std() / l.mean() > 0.25 else 0
+
+
 @dataclass
 class BlockBatch:
     """Raw data blocks resident on one device (concatenated, 16-B readable slack)."""
@@ -58,6 +67,7 @@ class BlockBatch:
         b = torch.from_numpy(pad).to(device, non_blocking=non_blocking)
         o = torch.from_numpy(np.ascontiguousarray(off, dtype=np.uint64).view(np.int64)).to(device)
         l = torch.from_numpy(np.ascontiguousarray(lens, dtype=np.uint32).view(np.int32)).to(device)
+        flags |= varlen_hint(lens)
         bf = None
         if block_format is not None:
             bf = torch.from_numpy(np.ascontiguousarray(block_format, dtype=np.uint8)).to(device)

@@ -34,8 +34,11 @@ extern "C" int pbl_decode_batch_colblk(const pbl_block_batch* batch, pbl_decode_
   a.out = *out;
   // default: the persistent lagged-look-back kernel (colblk_pipe.hip.h);
   // PBL_COL_KERNEL=single selects the one-block-per-workgroup kernel (A/B)
+  // or PBL_BATCH_VARLEN (measured on config 5: 412 vs 245 GiB/s, the pipeline's
+  // one-iteration look-back lag convoys behind long blocks)
   const char* kv = getenv("PBL_COL_KERNEL");
-  if (kv && strcmp(kv, "single") == 0) {
+  const bool single = kv ? strcmp(kv, "single") == 0 : (batch->flags & PBL_BATCH_VARLEN) != 0;
+  if (single) {
     hipLaunchKernelGGL(pbl::col::colblk_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
   } else {
     int dev = 0, cus = 0, per_cu = 0;

@@ -16,8 +16,15 @@ from pebble_amd.batch import BlockBatch, decode  # noqa: E402
 from pebble_amd.colblk import gen_col_blocks  # noqa: E402
 
 nb = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
-buf, off, lens, n = gen_col_blocks(42, nb, 32768, n_threads=16)
-b = BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_COL_CRDB1, 0)
+if len(sys.argv) > 2 and sys.argv[2] == "zipf":
+    # config 5, colblk DefaultKeySchema (bench.py --workload zipf --zipf-format col)
+    from pebble_amd.batch import gen_zipf_blocks
+    buf, off, lens, n = gen_zipf_blocks(42, nb, N.PBL_FMT_COL_DEFAULT, 16, 32768, n_threads=16)
+    b = BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_COL_DEFAULT, 0)
+    print("blocks: len median", np.median(lens), "p99", np.percentile(lens, 99), "max", lens.max(), "kvs", n)
+else:
+    buf, off, lens, n = gen_col_blocks(42, nb, 32768, n_threads=16)
+    b = BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_COL_CRDB1, 0)
 for _ in range(3):
     out = decode(b)
 torch.cuda.synchronize()
@@ -32,5 +39,10 @@ for nm, a, z in [("parse: header", 0, 1), ("parse: rows + publish", 1, 2), ("par
         print(f"{nm:24s} median {np.median(d):9.0f} mean {np.mean(d):9.0f} p90 {np.percentile(d, 90):9.0f} cycles")
 r = st[:, 10]
 sp = st[:, 11]
+tot = st[:, 7] - st[:, 0]
+m = (st[:, 0] > 0) & (st[:, 7] > 0)
+if m.any():
+    print("per-block parse start -> values end: median", np.median(tot[m]), "p99", np.percentile(tot[m], 99),
+          "max", tot[m].max())
 print("look-back rounds: median", np.median(r), "mean", r.mean(), "max", r.max(), "| spins: median", np.median(sp),
       "mean", sp.mean(), "p90", np.percentile(sp, 90))

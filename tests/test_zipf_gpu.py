@@ -26,8 +26,14 @@ def test_zipf_row(ri, vp):
         assert g["n_slow_blocks"] >= int((lens > 32768).sum())
 
 
-def test_zipf_col():
-    buf, off, lens, n = gen_zipf_blocks(7, 400, N.PBL_FMT_COL_DEFAULT)
+@pytest.mark.parametrize("seed", [7, 8, 9])
+@pytest.mark.parametrize("kernel", ["auto", "pipe"])
+def test_zipf_col(seed, kernel, monkeypatch):
+    # auto: the batch carries PBL_BATCH_VARLEN -> one-block-per-workgroup kernel;
+    # pipe: the persistent pipeline forced on the same blocks
+    if kernel == "pipe":
+        monkeypatch.setenv("PBL_COL_KERNEL", "pipe")
+    buf, off, lens, n = gen_zipf_blocks(seed, 400, N.PBL_FMT_COL_DEFAULT)
     g = col_check(buf, off, lens, N.PBL_FMT_COL_DEFAULT, ctx="zipf col")
     assert g["n_kv"] == n
 

@@ -38,3 +38,13 @@ def test_zipf_generator_is_deterministic():
     a = gen_zipf_blocks(3, 16, N.PBL_FMT_ROW, 16)
     b = gen_zipf_blocks(3, 16, N.PBL_FMT_ROW, 16, n_threads=3)
     assert a[3] == b[3] and np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_varlen_hint():
+    """PBL_BATCH_VARLEN (a scheduling hint) is set for config 5's Zipf-sized
+    blocks and not for fixed-size batches (configs 2/3)."""
+    from pebble_amd.batch import varlen_hint
+    assert varlen_hint(np.full(100, 32768, np.uint32)) == 0
+    assert varlen_hint(np.r_[np.full(50, 8000), np.full(50, 60000)]) == N.PBL_BATCH_VARLEN
+    _, _, lens, _ = gen_zipf_blocks(7, 200, N.PBL_FMT_COL_DEFAULT)
+    assert varlen_hint(lens) == N.PBL_BATCH_VARLEN
