@@ -12,3 +12,6 @@ $B --workload zipf --restart-interval 1 --no-cpu-baseline > gpurun_out/final/ben
 $B --workload zipf --restart-interval 16 --cpu-baseline-seconds 5 > gpurun_out/final/bench_zipf_ri16.json 2>/dev/null && \
 $B --workload zipf --restart-interval 32 --no-cpu-baseline > gpurun_out/final/bench_zipf_ri32.json 2>/dev/null && \
 $B --workload zipf --zipf-format col --no-cpu-baseline > gpurun_out/final/bench_zipf_col.json 2>/dev/null && echo zipf ok
+echo "== trace zipf col" && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/final/trace_zipf_col -o t -- python3 bench.py --workload zipf --zipf-format col --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/final/trace_zipf_col.log 2>&1 && \
+find gpurun_out/final/trace_zipf_col -name "*kernel_stats.csv" | head -1
