@@ -23,8 +23,12 @@
  *   - `stream` is a hipStream_t passed as void* (0 = legacy default stream).  All
  *     device entry points are stream-ordered and asynchronous; they never
  *     synchronise and are safe to capture into a hipGraph.
- *   - The library holds no global mutable state; it is reentrant across
- *     streams and devices.
+ *   - A launch runs on the device of its `stream` (hipStreamGetDevice), whatever
+ *     the calling thread's current device.  The library is reentrant across
+ *     streams and devices; its only process-wide state is a per-device cache of
+ *     hardware properties (CU count, resident workgroups per kernel), written
+ *     once.  Kernel choice depends only on the batch (format, flags), never on
+ *     the environment.
  */
 #ifndef PEBBLE_AMD_H
 #define PEBBLE_AMD_H
@@ -36,7 +40,7 @@
 extern "C" {
 #endif
 
-#define PBL_ABI_VERSION 2
+#define PBL_ABI_VERSION 3
 
 /* ---- status codes (per block, and OR-ed as bit masks into totals) ---------- */
 enum {
@@ -73,6 +77,11 @@ enum {
                                      kernel, whose look-back does not convoy behind
                                      long blocks.  The caller knows the lengths on the
                                      host (block handles carry them).              */
+#define PBL_KERNEL_SINGLE 0x200u  /* A/B measurement, no effect on results: the
+                                     one-block-per-workgroup kernels instead of the
+                                     persistent pipelines                          */
+#define PBL_KERNEL_PIPE 0x400u    /* A/B measurement, no effect on results: the
+                                     pipelines even for a PBL_BATCH_VARLEN batch   */
 
 /* per-KV flag byte (kv_flags[]) */
 #define PBL_KV_RESTART 0x01u       /* entry offset is a restart point            */
@@ -159,6 +168,27 @@ uint64_t pbl_workspace_bytes(uint32_t n_blocks);
  * reported in out->blk_status and out->totals (read them after the stream syncs).
  */
 int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stream);
+
+/*
+ * Size pass: the same parse as pbl_decode_batch, writing only
+ * the per-block results: blk_{kv,key,val,rst}_base (n_blocks+1 entries, the last
+ * = batch totals), blk_status and totals.  Only those arrays, `totals` and the
+ * workspace are required in `out`; every other pointer and capacity is ignored
+ * and nothing else is written.  A caller without exact sizes runs this, then
+ * pbl_decode_batch into exactly sized buffers (instead of guessing capacities
+ * and re-running on PBL_OVERFLOW).  Statuses are those pbl_decode_batch reports,
+ * PBL_OVERFLOW excepted.
+ */
+int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stream);
+
+/*
+ * Layout of the ABI structs as this library was compiled, for binding checks
+ * (ctypes, cgo): writes up to `cap` u64 values and returns how many it has:
+ *   sizeof(pbl_block_batch), the offsets of its 8 fields in declaration order,
+ *   sizeof(pbl_totals), the offsets of its 8 fields,
+ *   sizeof(pbl_decode_out), the offsets of its 20 fields.
+ */
+size_t pbl_struct_layout(uint64_t* out, size_t cap);
 
 /*
  * Offset concat for a sharded batch: add this rank's global

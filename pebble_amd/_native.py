@@ -10,7 +10,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# PBL_LIB selects the diagnostic (phase-stamp) build for scripts/phase_stamps.py
+# PBL_LIB selects the diagnostic (phase-stamp) build for scripts/pipe_stamps.py
 LIB_PATH = os.environ.get("PBL_LIB") or os.path.join(_HERE, "libpebble_amd.so")
 
 # status codes (include/pebble_amd.h)
@@ -30,7 +30,7 @@ STATUS_NAMES = {
     8: "DEVICE_ERROR", 9: "TIMEOUT",
 }
 
-ABI_VERSION = 2  # include/pebble_amd.h PBL_ABI_VERSION
+ABI_VERSION = 3  # include/pebble_amd.h PBL_ABI_VERSION
 
 PBL_FMT_ROW = 0
 PBL_FMT_COL_DEFAULT = 1
@@ -40,6 +40,8 @@ PBL_ROW_VALUE_PREFIX = 0x1
 PBL_ROW_NO_VALUER = 0x2
 PBL_ROW_RAW_KEYS = 0x4
 PBL_BATCH_VARLEN = 0x100
+PBL_KERNEL_SINGLE = 0x200
+PBL_KERNEL_PIPE = 0x400
 
 PBL_KV_RESTART = 0x01
 PBL_KV_RESTART_SAMEPFX = 0x02
@@ -106,6 +108,8 @@ SIGNATURES = {
     "pbl_abi_version": (ctypes.c_int, []),
     "pbl_workspace_bytes": (ctypes.c_uint64, [ctypes.c_uint32]),
     "pbl_decode_batch": (ctypes.c_int, [ctypes.POINTER(BlockBatchC), ctypes.POINTER(DecodeOutC), _vp]),
+    "pbl_size_batch": (ctypes.c_int, [ctypes.POINTER(BlockBatchC), ctypes.POINTER(DecodeOutC), _vp]),
+    "pbl_struct_layout": (ctypes.c_size_t, [_vp, ctypes.c_size_t]),
     "pbl_rebase_blocks": (ctypes.c_int, [ctypes.POINTER(DecodeOutC), ctypes.c_uint32, ctypes.c_uint64,
                                          ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _vp]),
     "pbl_offset_concat": (ctypes.c_int, [ctypes.POINTER(DecodeOutC), ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]),

@@ -171,7 +171,7 @@ class DecodedBatch:
 
     # ---- host readouts ------------------------------------------------------------
     def read_totals(self) -> N.TotalsC:
-        raw = self.totals.cpu().numpy().tobytes()
+        raw = self.totals.cpu().numpy().tobytes()  # (a sync copy: call after the decode's stream)
         t = N.TotalsC.from_buffer_copy(raw)
         self._host_totals = t
         return t
@@ -210,20 +210,46 @@ def decode_into(batch: BlockBatch, out: DecodedBatch, stream=None) -> None:
         raise DecodeError(f"pbl_decode_batch failed: {N.STATUS_NAMES.get(rc, rc)}")
 
 
+def size_batch(batch: BlockBatch, stream=None) -> DecodedBatch:
+    """Size pass (`pbl_size_batch`): per-block bases, statuses and totals only,
+    in a DecodedBatch whose per-KV arrays are empty (Capacity 0)."""
+    st = stream if stream is not None else torch.cuda.current_stream(batch.device)
+    with torch.cuda.stream(st):
+        out = DecodedBatch.allocate(batch.n_blocks, Capacity(0, 0, 0, 0), batch.device)
+    b = batch.c_struct()
+    o = out.c_struct()
+    rc = N.lib().pbl_size_batch(ctypes.byref(b), ctypes.byref(o), ctypes.c_void_p(st.cuda_stream))
+    if rc != N.PBL_OK:
+        raise DecodeError(f"pbl_size_batch failed: {N.STATUS_NAMES.get(rc, rc)}")
+    return out
+
+
 def decode(batch: BlockBatch, cap: Optional[Capacity] = None, stream=None, entry_off: bool = True,
-           restarts: bool = True) -> DecodedBatch:
-    """Decode a batch; re-runs once with exact capacities on PBL_OVERFLOW."""
+           restarts: bool = True, exact: bool = False) -> DecodedBatch:
+    """Decode a batch.  Without `cap`, capacities are estimated and the decode
+    re-runs once with exact ones on PBL_OVERFLOW; `exact=True` runs the size
+    pass first instead (one parse more, never a second decode).  The outputs are
+    allocated on the launch stream, so the caching allocator never hands them to
+    other work while the kernel writes them."""
+    st = stream if stream is not None else torch.cuda.current_stream(batch.device)
+    if cap is None and exact:
+        sz = size_batch(batch, st)
+        st.synchronize()
+        t = sz.read_totals()
+        cap = Capacity(kv=int(t.n_kv), key=int(t.key_bytes), val=int(t.val_bytes), rst=int(t.n_restarts))
     cap = cap or Capacity.estimate(batch)
-    out = DecodedBatch.allocate(batch.n_blocks, cap, batch.device, entry_off, restarts)
-    decode_into(batch, out, stream)
-    torch.cuda.current_stream().synchronize() if stream is None else stream.synchronize()
+    with torch.cuda.stream(st):
+        out = DecodedBatch.allocate(batch.n_blocks, cap, batch.device, entry_off, restarts)
+    decode_into(batch, out, st)
+    st.synchronize()
     t = out.read_totals()
     if t.status_mask & (1 << N.PBL_OVERFLOW):
         cap = Capacity(kv=int(t.n_kv) + 1, key=int(t.key_bytes) + 1, val=int(t.val_bytes) + 1,
                        rst=int(t.n_restarts) + 1)
-        out = DecodedBatch.allocate(batch.n_blocks, cap, batch.device, entry_off, restarts)
-        decode_into(batch, out, stream)
-        torch.cuda.current_stream().synchronize() if stream is None else stream.synchronize()
+        with torch.cuda.stream(st):
+            out = DecodedBatch.allocate(batch.n_blocks, cap, batch.device, entry_off, restarts)
+        decode_into(batch, out, st)
+        st.synchronize()
         out.read_totals()
     return out
 

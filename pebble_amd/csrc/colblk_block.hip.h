@@ -648,7 +648,7 @@ __device__ __forceinline__ void col_rows(Lds& s, const Args& A, uint32_t b, uint
       s.status = status;
 #pragma unroll
       for (int c = 0; c < kNumComp; c++) s.bases[c] = excl[c];
-      if (status != PBL_OK && excl[0] + b < O.kv_cap + nb) {
+      if (status != PBL_OK && O.key_off && excl[0] + b < O.kv_cap + nb) {
         O.key_off[excl[0] + b] = 0;
         O.val_off[excl[0] + b] = 0;
       }

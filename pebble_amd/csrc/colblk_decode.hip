@@ -1,9 +1,6 @@
 // colblk_decode.hip — gfx950 decoder for batches of Pebble columnar (colblk)
 // data blocks (colblk.DefaultKeySchema / cockroachkvs "crdb1").  One 256-thread
 // workgroup per block in ticket order; per-block work in colblk_block.hip.h.
-#include <stdlib.h>
-#include <string.h>
-
 #include "common.hip.h"
 #include "colblk_block.hip.h"
 #include "colblk_pipe.hip.h"
@@ -32,23 +29,20 @@ extern "C" int pbl_decode_batch_colblk(const pbl_block_batch* batch, pbl_decode_
   pbl::Args a;
   a.in = *batch;
   a.out = *out;
-  // default: the persistent lagged-look-back kernel (colblk_pipe.hip.h);
-  // PBL_COL_KERNEL=single selects the one-block-per-workgroup kernel (A/B)
-  // or PBL_BATCH_VARLEN (measured on config 5: 412 vs 245 GiB/s, the pipeline's
-  // one-iteration look-back lag convoys behind long blocks)
-  const char* kv = getenv("PBL_COL_KERNEL");
-  const bool single = kv ? strcmp(kv, "single") == 0 : (batch->flags & PBL_BATCH_VARLEN) != 0;
+  // default: the persistent lagged-look-back kernel (colblk_pipe.hip.h).  The
+  // one-block-per-workgroup kernel runs for PBL_KERNEL_SINGLE (A/B) and for
+  // PBL_BATCH_VARLEN batches unless PBL_KERNEL_PIPE forces the pipeline
+  // (config 5: 412 vs 245 GiB/s, the pipeline's one-iteration look-back lag
+  // convoys behind long blocks).
+  const uint32_t f = batch->flags;
+  const bool single = (f & PBL_KERNEL_SINGLE) || ((f & PBL_BATCH_VARLEN) && !(f & PBL_KERNEL_PIPE));
   if (single) {
     hipLaunchKernelGGL(pbl::col::colblk_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
   } else {
-    int dev = 0, cus = 0, per_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pbl::col::cpipe::colblk_pipe_kernel, pbl::kTPB, 0) !=
-            hipSuccess)
-      return PBL_DEVICE_ERROR;
-    uint64_t grid = uint64_t(cus > 0 ? cus : 1) * uint64_t(per_cu > 0 ? per_cu : 1);
-    if (grid > batch->n_blocks) grid = batch->n_blocks;
+    const uint64_t grid = pbl::persistent_grid(st, pbl::kKColPipe,
+                                               reinterpret_cast<const void*>(pbl::col::cpipe::colblk_pipe_kernel),
+                                               batch->n_blocks, nullptr);
+    if (!grid) return PBL_DEVICE_ERROR;
     hipLaunchKernelGGL(pbl::col::cpipe::colblk_pipe_kernel, dim3(uint32_t(grid)), dim3(pbl::kTPB), 0, st, a);
   }
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;

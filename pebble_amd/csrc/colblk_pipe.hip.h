@@ -143,7 +143,7 @@ __device__ __forceinline__ void col_resolve(CLds& L, const Slot& E, const Args& 
     L.st = status;
 #pragma unroll
     for (int c = 0; c < kNumComp; c++) L.bases[c] = excl[c];
-    if (status != PBL_OK && excl[0] + b < O.kv_cap + nb) {
+    if (status != PBL_OK && O.key_off && excl[0] + b < O.kv_cap + nb) {
       to_glb(O.key_off)[excl[0] + b] = 0;
       to_glb(O.val_off)[excl[0] + b] = 0;
     }

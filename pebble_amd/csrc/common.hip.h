@@ -322,10 +322,24 @@ __device__ inline void write_block_meta(const pbl_decode_out& O, uint32_t b, uin
   }
 }
 
+// (a size pass, pbl_size_batch, passes key_off = NULL: every block "overflows",
+// so sizes are computed and nothing is written)
 __device__ inline bool overflows(const pbl_decode_out& O, const uint64_t excl[kNumComp],
                                  const uint64_t agg[kNumComp]) {
-  return excl[0] + agg[0] > O.kv_cap || excl[1] + agg[1] > O.key_cap || excl[2] + agg[2] > O.val_cap ||
+  return !O.key_off || excl[0] + agg[0] > O.kv_cap || excl[1] + agg[1] > O.key_cap || excl[2] + agg[2] > O.val_cap ||
          (O.restarts && excl[3] + agg[3] > O.rst_cap);
 }
+
+// ---- host side: persistent-grid sizing ----------------------------------------
+// The device of a launch is the device of its stream (hipStreamGetDevice), not
+// the calling thread's current device.  The CU count and each persistent
+// kernel's resident workgroups per CU are hardware properties of that device:
+// they are queried once and cached (the library's only process-wide state, and
+// immutable once written; racing first calls store the same values).
+enum PersistentKernel { kKRowPipe = 0, kKRowSingle = 1, kKColPipe = 2, kKMixedPipe = 3, kKNum = 4 };
+
+// Resident grid for `fn` on the stream's device (never more than n_units, at
+// least 1); 0 on a runtime error.
+uint64_t persistent_grid(hipStream_t st, PersistentKernel k, const void* fn, uint64_t n_units, int* cus_out);
 
 }  // namespace pbl

@@ -25,8 +25,7 @@
 // not fit the LDS limits, take the general path (rowblk_general.hip.h): a
 // wave-serial restatement of Iter.First/Next, bit-identical by construction.
 #include <algorithm>
-#include <stdlib.h>
-#include <string.h>
+#include <atomic>
 
 #include "common.hip.h"
 #include "colblk_block.hip.h"
@@ -581,7 +580,7 @@ __device__ __forceinline__ void row_process(Lds& s, const Args& A, const uint32_
     if (wave_id() != 0) return;
     if (status == PBL_OK) {
       slow_walk(src, fits, blen, flags, keybuf, keycap, 1, A.out, b, excl, &ss);
-    } else if (lane_id() == 0 && excl[0] + b < O.kv_cap + nb) {
+    } else if (lane_id() == 0 && O.key_off && excl[0] + b < O.kv_cap + nb) {
       O.key_off[excl[0] + b] = 0;
       O.val_off[excl[0] + b] = 0;
     }
@@ -648,7 +647,7 @@ __device__ __forceinline__ void row_process(Lds& s, const Args& A, const uint32_
       s.status = status;
 #pragma unroll
       for (int c = 0; c < kNumComp; c++) s.bases[c] = excl[c];
-      if (status != PBL_OK && excl[0] + b < O.kv_cap + nb) {
+      if (status != PBL_OK && O.key_off && excl[0] + b < O.kv_cap + nb) {
         O.key_off[excl[0] + b] = 0;
         O.val_off[excl[0] + b] = 0;
       }
@@ -788,6 +787,18 @@ __global__ void __launch_bounds__(kTPB) mixed_decode_kernel(Args A) {
   else col::col_block(s.col, A, b, fmt);
 }
 
+// Size pass epilogue: a block that decoded reports PBL_OK, not the forced
+// overflow of the pass.
+__global__ void size_fixup_kernel(uint32_t* blk_status, pbl_totals* totals, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) __hip_atomic_fetch_and(&totals->status_mask, ~(1u << PBL_OVERFLOW), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+  if (i < n && blk_status[i] == PBL_OVERFLOW) {
+    blk_status[i] = PBL_OK;
+    g_atomic_add(&totals->n_bad_blocks, ~0u);  // (-1)
+  }
+}
+
 __global__ void rebase_kernel(uint64_t* kvb, uint64_t* kb, uint64_t* vb, uint64_t* rb, uint32_t n,
                               uint64_t dkv, uint64_t dk, uint64_t dv, uint64_t dr) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -812,6 +823,43 @@ __global__ void offset_concat_kernel(uint64_t* kvb, uint64_t* kb, uint64_t* vb, 
 }
 
 }  // namespace row
+}  // namespace pbl
+
+namespace pbl {
+
+namespace {
+constexpr int kMaxDevices = 64;
+std::atomic<int> g_cus[kMaxDevices];
+std::atomic<int> g_per_cu[kMaxDevices][kKNum];
+}  // namespace
+
+uint64_t persistent_grid(hipStream_t st, PersistentKernel k, const void* fn, uint64_t n_units, int* cus_out) {
+  int dev = -1;
+  if (st ? hipStreamGetDevice(st, &dev) != hipSuccess : hipGetDevice(&dev) != hipSuccess) return 0;
+  if (dev < 0 || dev >= kMaxDevices) return 0;
+  int cus = g_cus[dev].load(std::memory_order_relaxed);
+  int per_cu = g_per_cu[dev][k].load(std::memory_order_relaxed);
+  if (cus <= 0 || per_cu <= 0) {
+    // the occupancy query answers for the current device: switch to the
+    // stream's device for it and back
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess) return 0;
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) return 0;
+    const bool ok = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kTPB, 0) == hipSuccess;
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (!ok) return 0;
+    cus = cus > 0 ? cus : 1;
+    per_cu = per_cu > 0 ? per_cu : 1;
+    g_cus[dev].store(cus, std::memory_order_relaxed);
+    g_per_cu[dev][k].store(per_cu, std::memory_order_relaxed);
+  }
+  if (cus_out) *cus_out = cus;
+  uint64_t grid = uint64_t(cus) * uint64_t(per_cu);
+  if (grid > n_units) grid = n_units;
+  return grid ? grid : 1;
+}
+
 }  // namespace pbl
 
 extern "C" {
@@ -842,20 +890,16 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
   if (batch->block_format)
     hipLaunchKernelGGL(pbl::row::mixed_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
   else {
-    // persistent grid: as many workgroups as can be resident (never more than blocks)
-    // (PBL_ROW_KERNEL=single selects the one-block-per-workgroup persistent
-    // kernel, kept for A/B measurement; the default is the pipelined kernel)
-    const char* kv = getenv("PBL_ROW_KERNEL");
-    const bool single = kv && strcmp(kv, "single") == 0;
+    // persistent grid: as many workgroups as can be resident (never more than
+    // blocks).  PBL_KERNEL_SINGLE selects the one-block-per-workgroup
+    // persistent kernel (kept for A/B measurement); the default is the pipeline.
+    const bool single = (batch->flags & PBL_KERNEL_SINGLE) != 0;
     const void* fn = single ? reinterpret_cast<const void*>(pbl::row::rowblk_decode_kernel)
                             : reinterpret_cast<const void*>(pbl::row::pipe::rowblk_pipe_kernel);
-    int dev = 0, cus = 0, per_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, pbl::kTPB, 0) != hipSuccess)
-      return PBL_DEVICE_ERROR;
-    uint64_t grid = uint64_t(cus > 0 ? cus : 1) * uint64_t(per_cu > 0 ? per_cu : 1);
-    if (grid > batch->n_blocks) grid = batch->n_blocks;
+    int cus = 0;
+    const uint64_t grid = pbl::persistent_grid(st, single ? pbl::kKRowSingle : pbl::kKRowPipe, fn,
+                                               batch->n_blocks, &cus);
+    if (!grid) return PBL_DEVICE_ERROR;
     if (single)
       hipLaunchKernelGGL(pbl::row::rowblk_decode_kernel, dim3(uint32_t(grid)), dim3(pbl::kTPB), 0, st, a);
     else {
@@ -869,6 +913,82 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
     }
   }
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
+}
+
+int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stream) {
+  if (!batch || !out) return PBL_INVALID_ARG;
+  if (!out->totals || !out->blk_kv_base || !out->blk_key_base || !out->blk_val_base || !out->blk_status)
+    return PBL_INVALID_ARG;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (batch->n_blocks == 0) return pbl_decode_batch(batch, out, stream);
+  if (!batch->blocks || !batch->block_off || !batch->block_len || !out->workspace ||
+      out->workspace_bytes < pbl::ws_alloc_bytes(batch->n_blocks))
+    return PBL_INVALID_ARG;
+  // the decode with every per-KV pointer NULL and zero capacities: each block
+  // takes its overflow branch (sizes computed and published, nothing written);
+  // the fixup then reports the statuses the decode would have had
+  pbl_decode_out o = *out;
+  o.trailer = nullptr;
+  o.kv_flags = nullptr;
+  o.entry_off = nullptr;
+  o.key_off = nullptr;
+  o.val_off = nullptr;
+  o.key_bytes = nullptr;
+  o.val_bytes = nullptr;
+  o.restarts = nullptr;
+  o.kv_cap = o.key_cap = o.val_cap = o.rst_cap = 0;
+  if (hipMemsetAsync(o.totals, 0, sizeof(pbl_totals), st) != hipSuccess) return PBL_DEVICE_ERROR;
+  if (hipMemsetAsync(o.workspace, 0, pbl::ws_bytes(batch->n_blocks), st) != hipSuccess) return PBL_DEVICE_ERROR;
+  pbl::Args a;
+  a.in = *batch;
+  a.out = o;
+  int rc = PBL_OK;
+  if (!batch->block_format && batch->format != PBL_FMT_ROW) {
+    rc = pbl_decode_batch_colblk(batch, &o, stream);
+  } else {
+    // the launch sequence of pbl_decode_batch (whose checks require output
+    // pointers), minus the big-block value pass
+    if (batch->block_format) {
+      hipLaunchKernelGGL(pbl::row::mixed_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
+    } else {
+      int cus = 0;
+      const uint64_t grid = pbl::persistent_grid(
+          st, pbl::kKRowPipe, reinterpret_cast<const void*>(pbl::row::pipe::rowblk_pipe_kernel), batch->n_blocks,
+          &cus);
+      if (!grid) return PBL_DEVICE_ERROR;
+      const uint32_t small = uint32_t(std::min<uint64_t>(batch->n_blocks, uint64_t(cus) * 4));
+      hipLaunchKernelGGL(pbl::row::pipe::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+      hipLaunchKernelGGL(pbl::row::pipe::rowblk_pipe_kernel, dim3(uint32_t(grid)), dim3(pbl::kTPB), 0, st, a);
+    }
+    if (hipGetLastError() != hipSuccess) rc = PBL_DEVICE_ERROR;
+  }
+  if (rc != PBL_OK) return rc;
+  hipLaunchKernelGGL(pbl::row::size_fixup_kernel, dim3((batch->n_blocks + 255) / 256), dim3(256), 0, st,
+                     o.blk_status, o.totals, batch->n_blocks);
+  return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
+}
+
+size_t pbl_struct_layout(uint64_t* out, size_t cap) {
+#define PBL_OFF(T, f) uint64_t(offsetof(T, f))
+  const uint64_t v[] = {
+      sizeof(pbl_block_batch), PBL_OFF(pbl_block_batch, blocks), PBL_OFF(pbl_block_batch, block_off),
+      PBL_OFF(pbl_block_batch, block_len), PBL_OFF(pbl_block_batch, n_blocks), PBL_OFF(pbl_block_batch, format),
+      PBL_OFF(pbl_block_batch, flags), PBL_OFF(pbl_block_batch, reserved), PBL_OFF(pbl_block_batch, block_format),
+      sizeof(pbl_totals), PBL_OFF(pbl_totals, n_kv), PBL_OFF(pbl_totals, key_bytes), PBL_OFF(pbl_totals, val_bytes),
+      PBL_OFF(pbl_totals, n_restarts), PBL_OFF(pbl_totals, status_mask), PBL_OFF(pbl_totals, n_bad_blocks),
+      PBL_OFF(pbl_totals, n_slow_blocks), PBL_OFF(pbl_totals, pad),
+      sizeof(pbl_decode_out), PBL_OFF(pbl_decode_out, trailer), PBL_OFF(pbl_decode_out, kv_flags),
+      PBL_OFF(pbl_decode_out, entry_off), PBL_OFF(pbl_decode_out, key_off), PBL_OFF(pbl_decode_out, val_off),
+      PBL_OFF(pbl_decode_out, key_bytes), PBL_OFF(pbl_decode_out, val_bytes), PBL_OFF(pbl_decode_out, restarts),
+      PBL_OFF(pbl_decode_out, blk_kv_base), PBL_OFF(pbl_decode_out, blk_key_base),
+      PBL_OFF(pbl_decode_out, blk_val_base), PBL_OFF(pbl_decode_out, blk_rst_base),
+      PBL_OFF(pbl_decode_out, blk_status), PBL_OFF(pbl_decode_out, totals), PBL_OFF(pbl_decode_out, kv_cap),
+      PBL_OFF(pbl_decode_out, key_cap), PBL_OFF(pbl_decode_out, val_cap), PBL_OFF(pbl_decode_out, rst_cap),
+      PBL_OFF(pbl_decode_out, workspace), PBL_OFF(pbl_decode_out, workspace_bytes)};
+#undef PBL_OFF
+  const size_t n = sizeof(v) / sizeof(v[0]);
+  for (size_t i = 0; i < n && i < cap && out; i++) out[i] = v[i];
+  return n;
 }
 
 int pbl_rebase_blocks(pbl_decode_out* out, uint32_t n_blocks, uint64_t kv_base, uint64_t key_base,

@@ -446,7 +446,7 @@ __device__ __noinline__ void parse_slow(Meta& M, uint4* X, const Args A) {
       uint32_t st2 = ss.status;
       if (okk && overflows(A.out, excl, agg)) st2 = PBL_OVERFLOW;
       if (st2 == PBL_OK) slow_walk(src, from_lds, blen, flags, keybuf, keycap, kPassAll, A.out, b, excl, &ss);
-      else if (l == 0 && excl[0] + b < A.out.kv_cap + nb) {
+      else if (l == 0 && A.out.key_off && excl[0] + b < A.out.kv_cap + nb) {
         A.out.key_off[excl[0] + b] = 0;
         A.out.val_off[excl[0] + b] = 0;
       }
@@ -461,7 +461,7 @@ __device__ __noinline__ void parse_slow(Meta& M, uint4* X, const Args A) {
     lb_resolve(lb_state, nb, b, agg, excl, &A.out.totals->status_mask);
     uint32_t st2 = ss.status;
     if (okk && overflows(A.out, excl, agg)) st2 = PBL_OVERFLOW;
-    if (st2 != PBL_OK && l == 0 && excl[0] + b < A.out.kv_cap + nb) {
+    if (st2 != PBL_OK && l == 0 && A.out.key_off && excl[0] + b < A.out.kv_cap + nb) {
       A.out.key_off[excl[0] + b] = 0;
       A.out.val_off[excl[0] + b] = 0;
     }
@@ -633,7 +633,7 @@ __device__ __forceinline__ void parse_block(Meta& M, uint4* X, const Args& A) {
   PSTAMP(A, b, 4, l == 0);
   if (okb && overflows(A.out, excl, agg)) status = PBL_OVERFLOW;
   if (l == 0) {
-    if (status != PBL_OK && excl[0] + b < A.out.kv_cap + nb) {
+    if (status != PBL_OK && A.out.key_off && excl[0] + b < A.out.kv_cap + nb) {
       to_glb(A.out.key_off)[excl[0] + b] = 0;
       to_glb(A.out.val_off)[excl[0] + b] = 0;
     }

@@ -10,7 +10,7 @@ offsets are block-relative and never move; decoded bytes stay on their GPU.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Tuple
+from typing import List, Optional, Tuple  # noqa: F401
 
 import numpy as np
 import torch
@@ -43,49 +43,71 @@ def exclusive_bases(all_totals: torch.Tensor, rank: int) -> torch.Tensor:
 
 
 def allgather_totals(local_totals: torch.Tensor, group=None) -> torch.Tensor:
-    """All-gather the 4 local totals (int64) of every rank -> [world, 4]."""
+    """All-gather the 4 local totals (int64) of every rank -> [world, 4], on the
+    device of `local_totals`.  RCCL (backend "nccl") gathers device tensors in
+    place; a gloo group gathers through host memory."""
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    out = torch.empty(world * 4, dtype=torch.int64, device=local_totals.device)
-    if hasattr(dist, "all_gather_into_tensor") and local_totals.device.type == "cuda":
+    dev = local_totals.device
+    if dist.get_backend(group) == "nccl":
+        out = torch.empty(world * 4, dtype=torch.int64, device=dev)
         dist.all_gather_into_tensor(out, local_totals.reshape(4).contiguous(), group=group)
-    else:
-        parts = [torch.empty(4, dtype=torch.int64, device=local_totals.device) for _ in range(world)]
-        dist.all_gather(parts, local_totals.reshape(4).contiguous(), group=group)
-        out = torch.cat(parts)
-    return out.view(world, 4)
+        return out.view(world, 4)
+    loc = local_totals.reshape(4).to("cpu", torch.int64).contiguous()
+    parts = [torch.empty(4, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(parts, loc, group=group)
+    return torch.cat(parts).to(dev).view(world, 4)
+
+
+def shard_host(blocks: np.ndarray, block_off: np.ndarray, block_len: np.ndarray, start: int, end: int,
+               block_format: Optional[np.ndarray] = None):
+    """The host bytes and descriptors of blocks [start, end): (buf, off, lens,
+    block_format) with offsets relative to the shard's first byte (its 16-B
+    phase kept, so the device sees every block at the same alignment)."""
+    if end <= start:
+        return (np.zeros(16, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32),
+                None if block_format is None else np.zeros(0, np.uint8))
+    lo = int(block_off[start]) & ~15
+    hi = int((block_off[start:end].astype(np.int64) + block_len[start:end].astype(np.int64)).max())
+    buf = np.ascontiguousarray(blocks[lo:hi])
+    off = (block_off[start:end].astype(np.uint64) - np.uint64(lo)).astype(np.uint64)
+    lens = np.ascontiguousarray(block_len[start:end], dtype=np.uint32)
+    bf = None if block_format is None else np.ascontiguousarray(block_format[start:end], dtype=np.uint8)
+    return buf, off, lens, bf
 
 
 class ShardedBatchDecoder:
-    """Decode this rank's shard of a host batch on its GPU and concat offsets.
+    """Decode this rank's shard of a host batch on its GPU and concat offsets
+    (SURVEY.md §8(e)).
 
+    Rank r takes the contiguous block range `partition_blocks(block_len,
+    world)[r]` (formats sliced alongside for mixed batches, config 4).
     `decode()` returns the rank-local DecodedBatch whose blk_*_base arrays hold
-    GLOBAL positions (as if the whole batch had been decoded on one device).
+    GLOBAL positions (as if the whole batch had been decoded on one device),
+    and the gathered [world, 4] totals.
     """
 
     def __init__(self, blocks: np.ndarray, block_off: np.ndarray, block_len: np.ndarray, fmt: int = 0,
-                 flags: int = 0, rank: Optional[int] = None, world: Optional[int] = None, device=None):
+                 flags: int = 0, rank: Optional[int] = None, world: Optional[int] = None, device=None,
+                 block_format: Optional[np.ndarray] = None):
         import torch.distributed as dist
         self.rank = dist.get_rank() if rank is None else rank
         self.world = dist.get_world_size() if world is None else world
-        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         s, e = partition_blocks(block_len, self.world)[self.rank]
         self.block_range = (s, e)
         from .batch import BlockBatch
-        if e > s:
-            lo = int(block_off[s])
-            hi = int(block_off[e - 1]) + int(block_len[e - 1])
-            self.batch = BlockBatch.from_host(blocks[lo:hi], block_off[s:e] - lo, block_len[s:e], self.device,
-                                              fmt, flags)
-        else:
-            self.batch = BlockBatch.from_host(np.zeros(16, np.uint8), np.zeros(0, np.uint64),
-                                              np.zeros(0, np.uint32), self.device, fmt, flags)
+        buf, off, lens, bf = shard_host(blocks, block_off, block_len, s, e, block_format)
+        self.batch = BlockBatch.from_host(buf, off, lens, self.device, fmt, flags, block_format=bf)
 
-    def decode(self, group=None):
+    def decode(self, group=None, gather=allgather_totals):
+        """Decode the shard, exchange totals (`gather`: the all-gather, or a
+        stand-in returning the [world, 4] totals for single-process tests) and
+        rebase this rank's per-block bases on device."""
         from .batch import decode, offset_concat
         out = decode(self.batch)
         local = out.totals[:32].view(torch.int64).clone()
-        gathered = allgather_totals(local, group)
+        gathered = gather(local, group)
         offset_concat(out, gathered.reshape(-1).contiguous(), self.rank)
-        torch.cuda.current_stream().synchronize()
+        torch.cuda.current_stream(self.device).synchronize()
         return out, gathered

@@ -45,3 +45,22 @@ def test_python_constants_match_header():
             checked += 1
     assert checked >= 8
     assert N.PBL_BATCH_VARLEN == d["PBL_BATCH_VARLEN"]
+
+
+def test_ctypes_struct_layouts_match_library():
+    """sizeof/offsetof of the ctypes mirrors equal the compiled library's
+    (pbl_struct_layout), field by field."""
+    L = N.lib()
+    cap = 64
+    buf = (ctypes.c_uint64 * cap)()
+    n = L.pbl_struct_layout(ctypes.cast(buf, ctypes.c_void_p), cap)
+    v = list(buf[:n])
+    exp = []
+    for S in (N.BlockBatchC, N.TotalsC, N.DecodeOutC):
+        exp.append(ctypes.sizeof(S))
+        exp += [getattr(S, f).offset for f, _ in S._fields_]
+    assert v == exp
+
+
+def test_every_declared_function_has_a_ctypes_signature():
+    assert set(_declared_functions()) == set(N.SIGNATURES)

@@ -1,0 +1,299 @@
+"""Every BASELINE.json config on the device, bit-exact against the oracle
+(collected before the other GPU files, so that `pytest -x` reaches them first).
+
+  config 1  one 32 KiB row block, restart interval 16, 16 B keys / 100 B values
+  config 2  64 Ki x 32 KiB row blocks                      (full size)
+  config 3  64 Ki x 32 KiB colblk crdb1 blocks             (full size)
+  config 4  one GPU's shard: 128 Ki mixed row + colblk     (full shard)
+  config 5  64 Ki Zipf blocks (keys 8-1024 B, values 0-64 KiB), RI 16 row and
+            colblk DefaultKeySchema; RI 1 / 32 at reduced size
+  sharding  ShardedBatchDecoder at world size 1 with stand-in gathered totals
+  varints   hand-built entries with 3-, 4- and 5-byte varints (canonical and
+            not), the 5th-byte truncation of decodeVarint
+            (sstable/rowblk/rowblk_iter.go:357-360,2020-2038,
+            unsafe_test.go:19-42), 16 KiB+ values and keys
+  size pass pbl_size_batch against the decode's own sizes
+
+Full-size cases compare a SHA-256 digest of every output array.
+"""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+from pebble_amd import _native as N
+from pebble_amd.batch import BlockBatch, decode, gen_zipf_blocks, size_batch
+from pebble_amd.colblk import gen_col_blocks
+from pebble_amd.rowblk import gen_row_blocks, kvs_of_block, make_trailer
+from test_rowblk_gpu import ARRAYS, assert_same, pack
+
+pytestmark = pytest.mark.gpu
+
+
+def gpu(buf, off, lens, fmt=N.PBL_FMT_ROW, block_fmt=None, flags=0):
+    return decode(BlockBatch.from_host(buf, off, lens, "cuda", fmt, flags, block_format=block_fmt)).to_host()
+
+
+def digests_equal(g, o, ctx):
+    for k in ("n_kv", "key_bytes_total", "val_bytes_total", "n_restarts", "status_mask", "n_bad_blocks"):
+        assert g[k] == o[k], (ctx, k, g[k], o[k])
+    for k in ARRAYS:
+        if g[k] is not None:
+            assert hashlib.sha256(g[k].tobytes()).digest() == hashlib.sha256(o[k].tobytes()).digest(), (ctx, k)
+
+
+def test_config1_single_block():
+    buf, off, lens, n = gen_row_blocks(1, 1, 32768, 16, 16, 100)
+    o = oracle.rowblk_decode_batch(buf, off, lens)
+    g = gpu(buf, off, lens)
+    assert_same(g, o, "config 1")
+    assert g["n_kv"] == n and n > 250 and g["n_restarts"] == (n + 15) // 16
+    kvs = kvs_of_block(g, 0)
+    assert all(len(kv.user_key) == 16 and len(kv.value) == 100 for kv in kvs)
+    assert [kv.user_key for kv in kvs] == sorted(kv.user_key for kv in kvs)
+
+
+@pytest.mark.timeout(600)
+def test_config2_full_size():
+    buf, off, lens, n = gen_row_blocks(42, 65536, 32768, 16, 16, 100, n_threads=16)
+    g = gpu(buf, off, lens)
+    assert g["n_kv"] == n and g["status_mask"] == 0 and g["n_slow_blocks"] == 0
+    digests_equal(g, oracle.rowblk_decode_batch(buf, off, lens), "config 2")
+
+
+@pytest.mark.timeout(600)
+def test_config3_full_size():
+    buf, off, lens, n = gen_col_blocks(42, 65536, n_threads=16)
+    g = gpu(buf, off, lens, N.PBL_FMT_COL_CRDB1)
+    assert g["n_kv"] == n and g["status_mask"] == 0
+    digests_equal(g, oracle.decode_batch(buf, off, lens, N.PBL_FMT_COL_CRDB1), "config 3")
+
+
+def mixed_shard(nb, seed=42):
+    """Config 4's per-GPU shard as bench.py builds it: even ids row (config-2
+    shape), odd ids colblk crdb1 (config-3 shape), fixed 32 KiB stride."""
+    h = nb // 2
+    rb, ro, rl, rn = gen_row_blocks(seed, nb - h, 32768, 16, 16, 100, n_threads=16)
+    cb, co, cl, cn = gen_col_blocks(seed, h, n_threads=16)
+    buf = np.zeros(nb * 32768 + 16, np.uint8)
+    v = buf[: nb * 32768].reshape(nb, 32768)
+    v[0::2] = rb[: (nb - h) * 32768].reshape(nb - h, 32768)
+    v[1::2] = cb[: h * 32768].reshape(h, 32768)
+    off = np.arange(nb, dtype=np.uint64) * 32768
+    lens = np.empty(nb, np.uint32)
+    lens[0::2], lens[1::2] = rl, cl
+    fmt = np.empty(nb, np.uint8)
+    fmt[0::2], fmt[1::2] = N.PBL_FMT_ROW, N.PBL_FMT_COL_CRDB1
+    return buf, off, lens, fmt, rn + cn
+
+
+@pytest.mark.timeout(900)
+def test_config4_full_shard():
+    buf, off, lens, fmt, n = mixed_shard(131072)
+    g = gpu(buf, off, lens, N.PBL_FMT_ROW, fmt)
+    assert g["n_kv"] == n and g["status_mask"] == 0
+    digests_equal(g, oracle.decode_batch(buf, off, lens, N.PBL_FMT_ROW, fmt), "config 4")
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("fmt", [N.PBL_FMT_ROW, N.PBL_FMT_COL_DEFAULT])
+def test_config5_64ki(fmt):
+    buf, off, lens, n = gen_zipf_blocks(42, 65536, fmt, 16, 32768, n_threads=16)
+    g = gpu(buf, off, lens, fmt)
+    assert g["n_kv"] == n and g["status_mask"] == 0
+    digests_equal(g, oracle.decode_batch(buf, off, lens, fmt), f"config 5 fmt={fmt}")
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("ri", [1, 32])
+def test_config5_restart_intervals(ri):
+    buf, off, lens, n = gen_zipf_blocks(43 + ri, 8192, N.PBL_FMT_ROW, ri, 32768, n_threads=16)
+    g = gpu(buf, off, lens)
+    assert g["n_kv"] == n and g["status_mask"] == 0
+    digests_equal(g, oracle.rowblk_decode_batch(buf, off, lens), f"config 5 ri={ri}")
+
+
+@pytest.mark.parametrize("kind", ["row", "mixed"])
+def test_sharded_batch_decoder_world1_standin_totals(kind):
+    """ShardedBatchDecoder as rank 1 of 2 in one process: the all-gather is a
+    stand-in returning {shard 0's totals (oracle), this rank's own}; after the
+    device offset concat (pbl_offset_concat) the shard's bases must be the
+    whole-batch bases of its blocks."""
+    import torch
+    from pebble_amd.shard import ShardedBatchDecoder, partition_blocks
+    if kind == "row":
+        buf, off, lens, n = gen_row_blocks(9, 300, 32768, 16, 16, 100)
+        fmt = None
+    else:
+        buf, off, lens, fmt, n = mixed_shard(300, seed=9)
+    whole = oracle.decode_batch(buf, off, lens, N.PBL_FMT_ROW, fmt)
+    (s0, e0), (s1, e1) = partition_blocks(lens, 2)
+    first = oracle.decode_batch(buf, off[s0:e0], lens[s0:e0], N.PBL_FMT_ROW, None if fmt is None else fmt[s0:e0])
+    t0 = [first["n_kv"], first["key_bytes_total"], first["val_bytes_total"], first["n_restarts"]]
+
+    def standin(local, group=None):
+        return torch.stack([torch.tensor(t0, dtype=torch.int64, device=local.device), local.reshape(4)])
+
+    dec = ShardedBatchDecoder(buf, off, lens, N.PBL_FMT_ROW, 0, rank=1, world=2, device="cuda:0", block_format=fmt)
+    assert dec.block_range == (s1, e1)
+    out, gathered = dec.decode(gather=standin)
+    h = out.to_host()
+    for k in ("blk_kv_base", "blk_key_base", "blk_val_base", "blk_rst_base"):
+        assert np.array_equal(h[k], whole[k][s1:e1 + 1]), k
+    kb0, kb1 = int(whole["blk_key_base"][s1]), int(whole["blk_key_base"][e1])
+    assert h["key_bytes"].tobytes() == whole["key_bytes"][kb0:kb1].tobytes()
+    assert int(gathered[:, 0].sum()) == whole["n_kv"]
+
+
+# ---- varint edge cases ------------------------------------------------------------
+
+def varint(v, width=None, junk=0):
+    """LEB128 of v in `width` bytes (non-canonical when wider than needed);
+    `junk` sets bits 4-6 of a 5th byte, which decodeVarint drops (uint32 shift)."""
+    out = []
+    w = width or max(1, (v.bit_length() + 6) // 7)
+    for i in range(w):
+        b = (v >> (7 * i)) & 0x7F
+        if i < w - 1:
+            out.append(b | 0x80)
+        else:
+            out.append(((v >> 28) & 0x0F) | (junk << 4) if w == 5 else (v >> (7 * i)))
+    assert out[-1] < 128
+    return bytes(out)
+
+
+def raw_row_block(entries, ri):
+    """A row block from entries (key, value, (ws, wu, wv), junk): prefix
+    compression against the previous key within each restart run, each varint
+    written `w*` bytes wide (None = canonical); the first entry's shared length
+    is the one byte 0 (rowblk_iter.go:429-434)."""
+    out, restarts, prev = bytearray(), [], b""
+    for i, (key, val, (ws, wu, wv), junk) in enumerate(entries):
+        if i % ri == 0:
+            restarts.append(len(out))
+            sh = 0
+        else:
+            sh = 0
+            while sh < min(len(key), len(prev)) and key[sh] == prev[sh]:
+                sh += 1
+        if i == 0:
+            out += b"\x00"
+        else:
+            out += varint(sh, ws, junk)
+        out += varint(len(key) - sh, wu) + varint(len(val), wv) + key[sh:] + val
+        prev = key
+    for r in restarts:
+        out += r.to_bytes(4, "little")
+    out += len(restarts).to_bytes(4, "little")
+    return bytes(out)
+
+
+def varint_blocks():
+    rng = random.Random(2020)
+    blocks = []
+    widths = [(None, None, None), (4, None, None), (None, 4, None), (None, None, 4), (5, 5, 5), (4, 4, 4),
+              (5, None, None), (None, 5, None), (None, None, 5), (2, 3, 2), (3, 3, 3)]
+    for bi, wset in enumerate(widths):
+        for ri in (1, 4, 16):
+            ents, base = [], bytes(rng.randint(97, 122) for _ in range(10))
+            for i in range(40):
+                key = base + i.to_bytes(2, "big") + make_trailer(i, 1).to_bytes(8, "little")
+                val = bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 1, 9, 130])))
+                w = wset if i % 3 else (None, None, None)
+                ents.append((key, val, w, 0))
+            blocks.append(raw_row_block(ents, ri))
+    # 5th-byte truncation: a 5-byte shared length whose 5th byte carries bits
+    # 4-6 decodes as the low 28 bits (Go's uint32(e)<<28 drops them)
+    for junk in (1, 3, 7):
+        ents = []
+        for i in range(20):
+            key = b"trunc" + i.to_bytes(2, "big") + make_trailer(i, 1).to_bytes(8, "little")
+            ents.append((key, b"v" * i, (5, None, None), junk))
+        blocks.append(raw_row_block(ents, 4))
+    # 3-byte varints on the fast path: values of 16 KiB and more inside a 32 KiB block
+    for vl in (16384, 20000, 30000):
+        ents = [(b"big" + make_trailer(1, 1).to_bytes(8, "little"), bytes([7]) * vl, (None, None, None), 0),
+                (b"big2" + make_trailer(2, 1).to_bytes(8, "little"), b"x" * 100, (None, None, None), 0)]
+        blocks.append(raw_row_block(ents, 16))
+    # keys of 16 KiB and more (unshared lengths past the fast path's 14 bits)
+    for kl in (16384, 24000):
+        k1 = bytes(rng.randint(97, 122) for _ in range(kl)) + make_trailer(5, 1).to_bytes(8, "little")
+        k2 = k1[:kl - 1] + b"~" + make_trailer(6, 1).to_bytes(8, "little")
+        blocks.append(raw_row_block([(k1, b"a", (None, None, None), 0), (k2, b"b", (None, None, None), 0)], 16))
+    return blocks
+
+
+def test_varint_widths_and_truncation():
+    blocks = varint_blocks()
+    for b in blocks:  # the oracle itself decodes every one of them without error
+        st, _kvs, _r = oracle.rowblk_decode_block(b)
+        assert st == 0
+    buf, off, lens = pack(blocks, 8)
+    o = oracle.rowblk_decode_batch(buf, off, lens)
+    g = gpu(buf, off, lens)
+    assert_same(g, o, "varints")
+    assert g["status_mask"] == 0
+    # the truncated 5-byte shared lengths decode as their low 28 bits (0 here):
+    # those entries carry their whole key
+    for b in range(33, 36):
+        kvs = kvs_of_block(g, b)
+        assert [kv.user_key[:5] for kv in kvs] == [b"trunc"] * 20
+
+
+# ---- size pass / kernel A/B ----------------------------------------------------------
+
+@pytest.mark.parametrize("kind", ["row", "col", "mixed", "zipf_row", "zipf_col", "fuzz"])
+def test_size_pass_matches_decode(kind):
+    import torch
+    from test_rowblk_gpu import random_block
+    fmt, bf = N.PBL_FMT_ROW, None
+    if kind == "row":
+        buf, off, lens, _ = gen_row_blocks(3, 200, 32768, 16, 16, 100)
+    elif kind == "col":
+        fmt = N.PBL_FMT_COL_CRDB1
+        buf, off, lens, _ = gen_col_blocks(3, 200)
+    elif kind == "mixed":
+        buf, off, lens, bf, _ = mixed_shard(200, 3)
+    elif kind == "zipf_row":
+        buf, off, lens, _ = gen_zipf_blocks(3, 300, N.PBL_FMT_ROW, 16)
+    elif kind == "zipf_col":
+        fmt = N.PBL_FMT_COL_DEFAULT
+        buf, off, lens, _ = gen_zipf_blocks(3, 300, fmt)
+    else:
+        rng = random.Random(5)
+        blocks = []
+        for _ in range(200):
+            b = bytearray(random_block(rng)[0])
+            if rng.random() < 0.4 and len(b) > 4:
+                b[rng.randrange(len(b))] ^= 0xFF
+            blocks.append(bytes(b))
+        buf, off, lens = pack(blocks)
+    batch = BlockBatch.from_host(buf, off, lens, "cuda", fmt, 0, block_format=bf)
+    sz = size_batch(batch)
+    torch.cuda.synchronize()
+    full = decode(batch).to_host()
+    t = sz.read_totals()
+    assert (t.n_kv, t.key_bytes, t.val_bytes, t.n_restarts) == (
+        full["n_kv"], full["key_bytes_total"], full["val_bytes_total"], full["n_restarts"])
+    assert t.status_mask == full["status_mask"] and t.n_bad_blocks == full["n_bad_blocks"]
+    nb = len(off)
+    for k in ("blk_kv_base", "blk_key_base", "blk_val_base", "blk_rst_base"):
+        assert np.array_equal(getattr(sz, k)[: nb + 1].cpu().numpy().view(np.uint64), full[k]), k
+    assert np.array_equal(sz.blk_status[:nb].cpu().numpy().view(np.uint32), full["blk_status"])
+    # exact-size decode never re-runs and agrees with the estimate path
+    ex = decode(batch, exact=True).to_host()
+    assert_same(ex, full, f"exact {kind}")
+
+
+@pytest.mark.parametrize("fmt", [N.PBL_FMT_ROW, N.PBL_FMT_COL_CRDB1])
+def test_kernel_ab_flags_same_results(fmt):
+    gen = (lambda: gen_row_blocks(8, 300, 32768, 16, 16, 100)) if fmt == N.PBL_FMT_ROW else \
+        (lambda: gen_col_blocks(8, 300))
+    buf, off, lens, n = gen()
+    a = gpu(buf, off, lens, fmt)
+    b = gpu(buf, off, lens, fmt, flags=N.PBL_KERNEL_SINGLE)
+    c = gpu(buf, off, lens, fmt, flags=N.PBL_KERNEL_PIPE)
+    assert_same(b, a, "single")
+    assert_same(c, a, "pipe")

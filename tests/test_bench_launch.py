@@ -1,0 +1,29 @@
+"""bench.py's multi-rank launcher on CPU: `bench.py --gpus N` (no WORLD_SIZE in
+the environment) starts N ranks through torch.distributed.run as a child
+process; each rank reads RANK / LOCAL_RANK / WORLD_SIZE, and rank 0 prints ONE
+JSON line with n_gpus == N (--launch-check: gloo, no GPU touched)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_bench_self_launch_yields_n_ranks(n):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--launch-check"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n and d["launch_check"]
+    assert sorted(x[0] for x in d["ranks"]) == list(range(n))
+    assert sorted(x[1] for x in d["ranks"]) == list(range(n))  # one local rank (GPU) per process
+    assert all(x[2] == n for x in d["ranks"])
+    if n > 1:
+        assert d["parallelism"] == f"shard{n}+rccl_offset_concat"

@@ -190,20 +190,6 @@ def test_rebase_offset_concat():
     assert torch.equal(out.blk_kv_base[:9] - before, torch.full_like(before, 1000))
 
 
-def test_full_size_batch_properties():
-    """Config 2 at full size (64 Ki x 32 KiB): KV count and a checksum of
-    per-block checksums against the oracle on every block."""
-    import hashlib
-    nb = 65536
-    buf, off, lens, n = gen_row_blocks(42, nb, 32768, 16, 16, 100, n_threads=16)
-    g = gpu_decode(buf, off, lens)
-    assert g["n_kv"] == n and g["status_mask"] == 0 and g["n_slow_blocks"] == 0
-    o = oracle.rowblk_decode_batch(buf, off, lens)
-    for k in ARRAYS:
-        if g[k] is not None:
-            assert hashlib.sha256(g[k].tobytes()).digest() == hashlib.sha256(o[k].tobytes()).digest(), k
-
-
 def test_device_offset_concat_matches_exclusive_prefix():
     import torch
     from pebble_amd.batch import BlockBatch, decode, offset_concat

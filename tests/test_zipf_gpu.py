@@ -28,13 +28,12 @@ def test_zipf_row(ri, vp):
 
 @pytest.mark.parametrize("seed", [7, 8, 9])
 @pytest.mark.parametrize("kernel", ["auto", "pipe"])
-def test_zipf_col(seed, kernel, monkeypatch):
+def test_zipf_col(seed, kernel):
     # auto: the batch carries PBL_BATCH_VARLEN -> one-block-per-workgroup kernel;
-    # pipe: the persistent pipeline forced on the same blocks
-    if kernel == "pipe":
-        monkeypatch.setenv("PBL_COL_KERNEL", "pipe")
+    # pipe: the persistent pipeline forced on the same blocks (PBL_KERNEL_PIPE)
     buf, off, lens, n = gen_zipf_blocks(seed, 400, N.PBL_FMT_COL_DEFAULT)
-    g = col_check(buf, off, lens, N.PBL_FMT_COL_DEFAULT, ctx="zipf col")
+    g = col_check(buf, off, lens, N.PBL_FMT_COL_DEFAULT, ctx="zipf col",
+                  flags=N.PBL_KERNEL_PIPE if kernel == "pipe" else 0)
     assert g["n_kv"] == n
 
 
