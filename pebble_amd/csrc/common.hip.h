@@ -19,28 +19,38 @@ constexpr int kLbWin = 8;   // look-back windows (of 64 predecessors) loaded per
 
 // ---- workspace layout ------------------------------------------------------
 // [0,256): ticket counter (u32 [0]), big-block count (u32 [1], row pipeline), pad.  Then
-//   word[n_blocks]        one packed status word per block {state:2 | agg:62}:
-//                         state 1 = aggregate ready (4 counts packed below),
-//                         2 = inclusive prefix ready (in pfx[]), 3 = aggregate
-//                         too wide to pack (in wide[])
-//   pfx[kNumComp][n_blocks]   inclusive prefixes {state:2 | value:62}
-//   wide[kNumComp][n_blocks]  unpackable aggregates {state:2 | value:62}
+//   rec[n_blocks]             one 16-B record per block {w0, w1}, each 8-B half
+//                             self-tagged with a 3-bit state (top bits):
+//                               w0 = Agg | packed aggregate (4 counts), or
+//                               w0 = Wide (aggregate too wide: in wide[]), or
+//                               w0 = Pfx | (n_kv:31 | key:30), w1 = Pfx | (val:37 | rst:24)
+//                                    (packed INCLUSIVE prefix), or
+//                               w0 = PfxWide (inclusive prefix too wide: in pfx[])
+//   pfx[kNumComp][n_blocks]   wide inclusive prefixes {state | value}
+//   wide[kNumComp][n_blocks]  wide aggregates {state | value}
 // All written and read with agent-scope relaxed 8-byte atomics (sc1): each word
-// carries its own state, so a reader that sees a status word before the
-// component words it announces simply polls those (no fences; MI355X_MICROARCH.md
-// "Valid forms", R2 granules).
+// carries its own state, so a reader that sees a record before the words it
+// announces simply polls those (no fences; MI355X_MICROARCH.md "Valid forms",
+// R2 granules).  A resolve normally costs ONE round trip: the windows of
+// predecessor records carry packed inclusive prefixes, so the nearest one ends
+// the walk without a second fetch.
 constexpr uint64_t kWsHeader = 256;
 constexpr int kWsBigCount = 1;  // header u32 [1]: blocks past the LDS stage (row pipeline)
-constexpr uint64_t kStateAgg = 1ull << 62;
-constexpr uint64_t kStatePfx = 2ull << 62;
-constexpr uint64_t kStateWide = 3ull << 62;
-constexpr uint64_t kValMask = (1ull << 62) - 1;
-// packed aggregate fields: n_kv 14 | key bytes 18 | value bytes 18 | restarts 12
-constexpr int kPkBits[kNumComp] = {14, 18, 18, 12};
+constexpr int kStShift = 61;
+constexpr uint64_t kStAgg = 1ull << kStShift;
+constexpr uint64_t kStWide = 2ull << kStShift;
+constexpr uint64_t kStPfx = 3ull << kStShift;
+constexpr uint64_t kStPfxWide = 4ull << kStShift;
+constexpr uint64_t kStMask = 7ull << kStShift;
+constexpr uint64_t kValMask = (1ull << kStShift) - 1;
+// packed aggregate fields (w0 of an Agg record): n_kv 14 | key bytes 18 | value bytes 18 | restarts 11
+constexpr int kPkBits[kNumComp] = {14, 18, 18, 11};
 constexpr int kPkShift[kNumComp] = {0, 14, 32, 50};
+// packed inclusive prefix: w0 = n_kv 31 | key 30, w1 = val 37 | rst 24
+constexpr int kPfBits[kNumComp] = {31, 30, 37, 24};
 
 __host__ __device__ inline uint64_t ws_bytes(uint32_t n_blocks) {
-  return kWsHeader + uint64_t(1 + 2 * kNumComp) * n_blocks * 8ull;
+  return kWsHeader + uint64_t(2 + 2 * kNumComp) * n_blocks * 8ull;
 }
 #ifdef PBL_STAMPS
 constexpr uint64_t kStampWords = 16;  // diagnostic build: per-block phase stamps
@@ -136,136 +146,202 @@ __device__ inline void block_excl_scan2(uint32_t a, uint32_t b, uint32_t* ea, ui
 // workgroup can publish its aggregate as soon as it is known and resolve its
 // exclusive prefix later.  Tickets are handed out in launch order, so every
 // predecessor is resident and publishes its aggregate before it waits: no
-// deadlock for any residency.  Both halves run on wave 0 of the workgroup that
-// owns virtual block `v`; `st` is the workspace after its header.
+// deadlock for any residency.  Both halves run on one wave of the workgroup
+// that owns virtual block `v`; `st` is the workspace after its header.
 __device__ inline bool agg_packable(const uint64_t agg[kNumComp]) {
   return agg[0] < (1ull << kPkBits[0]) && agg[1] < (1ull << kPkBits[1]) && agg[2] < (1ull << kPkBits[2]) &&
          agg[3] < (1ull << kPkBits[3]);
 }
+__device__ inline bool pfx_packable(const uint64_t p[kNumComp]) {
+  return p[0] < (1ull << kPfBits[0]) && p[1] < (1ull << kPfBits[1]) && p[2] < (1ull << kPfBits[2]) &&
+         p[3] < (1ull << kPfBits[3]);
+}
 
-__device__ inline void lb_publish(uint64_t* st, uint32_t n_blocks, uint32_t v, const uint64_t agg[kNumComp]) {
+struct LbPtrs {
+  uint64_t* rec;   // [2 * n_blocks]
+  uint64_t* pfx;   // [kNumComp * n_blocks]
+  uint64_t* wide;  // [kNumComp * n_blocks]
+  __device__ LbPtrs(uint64_t* st, uint32_t n_blocks)
+      : rec(st), pfx(st + 2ull * n_blocks), wide(st + 2ull * n_blocks + uint64_t(kNumComp) * n_blocks) {}
+};
+
+// Store block v's inclusive prefix `p` (lanes 0-3 of the calling wave).
+__device__ inline void lb_store_pfx(const LbPtrs& P, uint32_t n_blocks, uint32_t v, const uint64_t p[kNumComp]) {
   const int l = lane_id();
-  uint64_t* word = st;
-  uint64_t* pfx = st + n_blocks;
-  uint64_t* wide = pfx + uint64_t(kNumComp) * n_blocks;
-  const bool pk = agg_packable(agg);
-  if (v == 0 || !pk) {
-    // block 0: its inclusive prefix IS its aggregate; wide aggregates go to
-    // their own slots (the status word announces them)
-    if (l < kNumComp) {
-      uint64_t a = l == 0 ? agg[0] : l == 1 ? agg[1] : l == 2 ? agg[2] : agg[3];
-      uint64_t* dst = v == 0 ? pfx : wide;
-      st_agent(dst + uint64_t(l) * n_blocks + v, (v == 0 ? kStatePfx : kStateAgg) | (a & kValMask));
+  if (pfx_packable(p)) {
+    if (l == 0) {
+      // w1 first: a reader that sees w0's Pfx before w1's polls w1
+      st_agent(P.rec + 2ull * v + 1, kStPfx | p[2] | (p[3] << kPfBits[2]));
+      st_agent(P.rec + 2ull * v, kStPfx | p[0] | (p[1] << kPfBits[0]));
     }
-  }
-  if (l == 0) {
-    uint64_t packed = 0;
-    if (pk)
-      for (int c = 0; c < kNumComp; c++) packed |= agg[c] << kPkShift[c];
-    st_agent(word + v, (v == 0 ? kStatePfx : pk ? kStateAgg : kStateWide) | packed);
+  } else {
+    if (l < kNumComp) {
+      const uint64_t x = l == 0 ? p[0] : l == 1 ? p[1] : l == 2 ? p[2] : p[3];
+      st_agent(P.pfx + uint64_t(l) * n_blocks + v, kStPfxWide | (x & kValMask));
+    }
+    if (l == 0) st_agent(P.rec + 2ull * v, kStPfxWide);
   }
 }
 
-// Poll one component word until it carries `want` (single lane).
+__device__ inline void lb_publish(uint64_t* st, uint32_t n_blocks, uint32_t v, const uint64_t agg[kNumComp]) {
+  const int l = lane_id();
+  const LbPtrs P(st, n_blocks);
+  if (v == 0) {  // block 0: its inclusive prefix IS its aggregate
+    lb_store_pfx(P, n_blocks, v, agg);
+    return;
+  }
+  if (agg_packable(agg)) {
+    if (l == 0) {
+      uint64_t packed = 0;
+      for (int c = 0; c < kNumComp; c++) packed |= agg[c] << kPkShift[c];
+      st_agent(P.rec + 2ull * v, kStAgg | packed);
+    }
+  } else {
+    // wide aggregates go to their own slots (the record announces them)
+    if (l < kNumComp) {
+      const uint64_t a = l == 0 ? agg[0] : l == 1 ? agg[1] : l == 2 ? agg[2] : agg[3];
+      st_agent(P.wide + uint64_t(l) * n_blocks + v, kStWide | (a & kValMask));
+    }
+    if (l == 0) st_agent(P.rec + 2ull * v, kStWide);
+  }
+}
+
+// Poll one word until its state is `want` (single lane); returns the payload.
 __device__ inline uint64_t lb_poll(uint64_t* p, uint64_t want, uint32_t* spins, bool* timed_out) {
   uint64_t x;
-  while (((x = ld_agent(p)) & ~kValMask) != want) {
+  while (((x = ld_agent(p)) & kStMask) != want) {
     if (++*spins > (1u << 22)) { *timed_out = true; return 0; }
     __builtin_amdgcn_s_sleep(2);
   }
   return x & kValMask;
 }
 
-__device__ inline void lb_resolve(uint64_t* st, uint32_t n_blocks, uint32_t v, const uint64_t agg[kNumComp],
-                                  uint64_t excl[kNumComp], uint32_t* timeout_flag, uint32_t* stats = nullptr) {
+// The 4 component words at src[q * n + idx] in one round trip (loads issued
+// together), each polled on its own only if it is not ready yet.
+__device__ inline void lb_fetch4(uint64_t* src, uint32_t n_blocks, int64_t idx, uint64_t want, uint64_t c[kNumComp],
+                                 uint32_t* spins, bool* timed_out) {
+  uint64_t x[kNumComp];
+#pragma unroll
+  for (int q = 0; q < kNumComp; q++) x[q] = ld_agent(src + uint64_t(q) * n_blocks + idx);
+#pragma unroll
+  for (int q = 0; q < kNumComp; q++)
+    c[q] = (x[q] & kStMask) == want ? (x[q] & kValMask)
+                                    : lb_poll(src + uint64_t(q) * n_blocks + idx, want, spins, timed_out);
+}
+
+// Windows of predecessor records loaded in one round trip: lane l of window k
+// holds rec[top - 64k - l] (w0 and w1).
+template <int W>
+struct LbWindows {
+  uint64_t w0[W], w1[W];
+  int64_t top;
+  __device__ inline void issue(const LbPtrs& P, int64_t top_) {
+    top = top_;
+    const int l = lane_id();
+#pragma unroll
+    for (int k = 0; k < W; k++) {
+      const int64_t idx = top - kWave * k - l;
+      w0[k] = idx >= 0 ? ld_agent(P.rec + 2 * idx) : kStPfx;  // (index -1 acts as a zero prefix)
+      w1[k] = idx >= 0 ? ld_agent(P.rec + 2 * idx + 1) : kStPfx;
+    }
+  }
+};
+
+// Consume loaded windows: accumulate per-lane partial sums into acc.  Returns
+// true when the walk reached an inclusive prefix; otherwise *next_top is where
+// to continue and *wait_idx >= 0 names a predecessor that has not published.
+template <int W>
+__device__ inline bool lb_consume(const LbPtrs& P, uint32_t n_blocks, const LbWindows<W>& G, uint64_t acc[kNumComp],
+                                  int64_t* next_top, int64_t* wait_idx, uint32_t* spins, bool* timed_out) {
   const int l = lane_id();
-  uint64_t* word = st;
-  uint64_t* pfx = st + n_blocks;
-  uint64_t* wide = pfx + uint64_t(kNumComp) * n_blocks;
+  int64_t top = G.top;
+  *wait_idx = -1;
+#pragma unroll
+  for (int k = 0; k < W; k++) {
+    const int64_t idx = G.top - kWave * k - l;
+    const uint64_t state = G.w0[k] & kStMask;
+    const bool is_pfx = state == kStPfx || state == kStPfxWide;
+    const uint64_t pfxm = __ballot(is_pfx);
+    const uint64_t notready = __ballot(state == 0);
+    const int first = pfxm ? __builtin_ctzll(pfxm) : 64;
+    const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
+    if (notready & need) {
+      *wait_idx = G.top - kWave * k - __builtin_ctzll(notready & need);
+      *next_top = top;
+      return false;
+    }
+    uint64_t c[kNumComp] = {0, 0, 0, 0};
+    if (l < first && state == kStAgg) {
+#pragma unroll
+      for (int q = 0; q < kNumComp; q++) c[q] = (G.w0[k] >> kPkShift[q]) & ((1ull << kPkBits[q]) - 1);
+    }
+    if (l < first && state == kStWide) lb_fetch4(P.wide, n_blocks, idx, kStWide, c, spins, timed_out);
+    if (l == first && idx >= 0) {
+      if (state == kStPfx) {
+        uint64_t w1 = G.w1[k];
+        if ((w1 & kStMask) != kStPfx) w1 = kStPfx | lb_poll(P.rec + 2 * idx + 1, kStPfx, spins, timed_out);
+        c[0] = G.w0[k] & ((1ull << kPfBits[0]) - 1);
+        c[1] = (G.w0[k] >> kPfBits[0]) & ((1ull << kPfBits[1]) - 1);
+        c[2] = w1 & ((1ull << kPfBits[2]) - 1);
+        c[3] = (w1 >> kPfBits[2]) & ((1ull << kPfBits[3]) - 1);
+      } else {
+        lb_fetch4(P.pfx, n_blocks, idx, kStPfxWide, c, spins, timed_out);
+      }
+    }
+    // per-lane partial sums; the cross-lane reduction happens once, at the end
+#pragma unroll
+    for (int q = 0; q < kNumComp; q++) acc[q] += c[q];
+    if (first < 64) return true;
+    top -= kWave;
+  }
+  *next_top = top;
+  return false;
+}
+
+// Finish a resolve whose first windows (from v-1 down) are already loaded.
+template <int W>
+__device__ inline void lb_finish(uint64_t* st, uint32_t n_blocks, uint32_t v, const uint64_t agg[kNumComp],
+                                 uint64_t excl[kNumComp], uint32_t* timeout_flag, const LbWindows<W>& first_win) {
+  const int l = lane_id();
+  const LbPtrs P(st, n_blocks);
   uint64_t acc[kNumComp] = {0, 0, 0, 0};
-  int64_t top = int64_t(v) - 1;
-  bool done = v == 0;
   uint32_t spins = 0;
   bool timed_out = false;
-  uint32_t rounds = 0;
+  int64_t top = int64_t(v) - 1, wait_idx = -1;
+  bool done = v == 0 || lb_consume(P, n_blocks, first_win, acc, &top, &wait_idx, &spins, &timed_out);
   while (!done && !timed_out) {
-    rounds++;
-    uint64_t g[kLbWin];
-#pragma unroll
-    for (int k = 0; k < kLbWin; k++) {
-      const int64_t idx = top - kWave * k - l;
-      g[k] = idx >= 0 ? ld_agent(word + idx) : kStatePfx;  // (index -1 acts as a zero prefix)
-    }
-    int64_t wait_idx = -1;
-    const int64_t top0 = top;  // the windows were loaded from here
-#pragma unroll
-    for (int k = 0; k < kLbWin; k++) {
-      if (done || wait_idx >= 0) continue;
-      const int64_t idx = top0 - kWave * k - l;
-      const uint64_t state = g[k] & ~kValMask;
-      const uint64_t pfxm = __ballot(state == kStatePfx);
-      const uint64_t notready = __ballot(state == 0);
-      const int first = pfxm ? __builtin_ctzll(pfxm) : 64;
-      const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
-      if (notready & need) {
-        wait_idx = top0 - kWave * k - __builtin_ctzll(notready & need);
-        continue;
-      }
-      // contributions: packed aggregates, wide aggregates and the prefix at `first`
-      uint64_t c[kNumComp] = {0, 0, 0, 0};
-      if (l < first || (l == first && idx < 0)) {
-        if (state == kStateAgg) {
-#pragma unroll
-          for (int q = 0; q < kNumComp; q++) c[q] = (g[k] >> kPkShift[q]) & ((1ull << kPkBits[q]) - 1);
-        }
-      }
-      const bool fetch = idx >= 0 && ((l < first && state == kStateWide) || (l == first && state == kStatePfx));
-      if (fetch) {
-        const bool p = state == kStatePfx;
-        uint64_t* src = p ? pfx : wide;
-#pragma unroll
-        for (int q = 0; q < kNumComp; q++)
-          c[q] = lb_poll(src + uint64_t(q) * n_blocks + idx, p ? kStatePfx : kStateAgg, &spins, &timed_out);
-      }
-      // per-lane partial sums; the cross-lane reduction happens once, at the end
-#pragma unroll
-      for (int q = 0; q < kNumComp; q++) acc[q] += c[q];
-      if (first < 64) done = true;
-      else top -= kWave;
-    }
-    if (__ballot(timed_out)) { timed_out = true; break; }
-    if (!done && wait_idx >= 0) {
+    if (wait_idx >= 0) {
       // Poll the missing predecessor from ONE lane (a whole-window re-read per
       // poll would flood this CU's memory queue), then re-read the windows.
       if (l == 0) {
-        while ((ld_agent(word + wait_idx) & ~kValMask) == 0) {
+        while ((ld_agent(P.rec + 2 * wait_idx) & kStMask) == 0) {
           if (++spins > (1u << 22)) { timed_out = true; break; }
           __builtin_amdgcn_s_sleep(2);
         }
       }
       if (__shfl(timed_out ? 1 : 0, 0, kWave)) { timed_out = true; break; }
     }
+    LbWindows<kLbWin> G;
+    G.issue(P, top);
+    done = lb_consume(P, n_blocks, G, acc, &top, &wait_idx, &spins, &timed_out);
+    if (__ballot(timed_out)) timed_out = true;
   }
   if (timed_out && l == 0) g_atomic_or(timeout_flag, 1u << PBL_TIMEOUT);
-  if (stats) {
-    stats[0] = rounds;
-    stats[1] = spins;
-  }
 #pragma unroll
   for (int q = 0; q < kNumComp; q++) excl[q] = wave_sum(acc[q]);
   if (v > 0) {
-    if (l < kNumComp) {
-      uint64_t e = l == 0 ? excl[0] : l == 1 ? excl[1] : l == 2 ? excl[2] : excl[3];
-      uint64_t a = l == 0 ? agg[0] : l == 1 ? agg[1] : l == 2 ? agg[2] : agg[3];
-      st_agent(pfx + uint64_t(l) * n_blocks + v, kStatePfx | ((e + a) & kValMask));
-    }
-    if (l == 0) {
-      uint64_t packed = 0;
-      if (agg_packable(agg))
-        for (int q = 0; q < kNumComp; q++) packed |= agg[q] << kPkShift[q];
-      st_agent(word + v, kStatePfx | packed);
-    }
+    uint64_t p[kNumComp];
+#pragma unroll
+    for (int q = 0; q < kNumComp; q++) p[q] = excl[q] + agg[q];
+    lb_store_pfx(P, n_blocks, v, p);
   }
+}
+
+__device__ inline void lb_resolve(uint64_t* st, uint32_t n_blocks, uint32_t v, const uint64_t agg[kNumComp],
+                                  uint64_t excl[kNumComp], uint32_t* timeout_flag) {
+  LbWindows<kLbWin> G;
+  if (v > 0) G.issue(LbPtrs(st, n_blocks), int64_t(v) - 1);
+  lb_finish(st, n_blocks, v, agg, excl, timeout_flag, G);
 }
 
 __device__ inline void lookback(uint64_t* st, uint32_t n_blocks, uint32_t v, const uint64_t agg[kNumComp],

@@ -28,7 +28,7 @@ else:
 for _ in range(3):
     out = decode(b)
 torch.cuda.synchronize()
-ws_state = 256 + 9 * nb * 8
+ws_state = 256 + 10 * nb * 8
 st = out.workspace[ws_state: ws_state + nb * 16 * 8].view(torch.int64).view(nb, 16).cpu().numpy()
 for nm, a, z in [("parse: header", 0, 1), ("parse: rows + publish", 1, 2), ("parse total", 0, 2),
                  ("parse end -> emit start", 2, 3), ("emit: look-back", 3, 4), ("emit: per-row", 4, 5),

@@ -30,7 +30,7 @@ out = decode(b)
 for _ in range(3):
     out = decode(b)
 torch.cuda.synchronize()
-ws_state = 256 + 9 * nb * 8
+ws_state = 256 + 10 * nb * 8
 st = out.workspace[ws_state: ws_state + nb * 16 * 8].view(torch.int64).view(nb, 16).cpu().numpy()
 phases = [("parse: init+count+scan", 0, 1), ("parse: write pass", 1, 2), ("parse: buckets+publish", 2, 3),
           ("parse total", 0, 3), ("parse: look-back resolve", 3, 4), ("resolved -> emit start", 4, 5),
