@@ -416,6 +416,7 @@ enum PersistentKernel { kKRowPipe = 0, kKRowSingle = 1, kKColPipe = 2, kKMixedPi
 
 // Resident grid for `fn` on the stream's device (never more than n_units, at
 // least 1); 0 on a runtime error.
-uint64_t persistent_grid(hipStream_t st, PersistentKernel k, const void* fn, uint64_t n_units, int* cus_out);
+uint64_t persistent_grid(hipStream_t st, PersistentKernel k, const void* fn, uint64_t n_units, int* cus_out,
+                         int block_threads = kTPB);
 
 }  // namespace pbl

@@ -77,12 +77,34 @@ struct Lds {
   uint64_t n2_off, nxt_off;
 };
 
-// 16 bytes at LDS byte address a (any alignment): five dword reads + alignbyte
+// Unaligned LDS access.  gfx950 runs in unaligned access mode (the HSA
+// runtime's default), where one ds_read_b128 / b64 / b32 serves any byte
+// address: a 16-byte gather is one instruction instead of five dword reads
+// and four alignbytes.  Measured on config 2 (same box, A/B): unaligned 16-byte
+// gathers +2.7 % (992 vs 965 GiB/s), unaligned 8-byte header reads in the
+// parse walk -1.5 %; so gathers are unaligned and ld8/le32 stay dword reads
+// (PBL_LDS_UA8 / PBL_LDS_UA16 switch each form for A/B builds).
+typedef u32x4 u32x4_u __attribute__((aligned(1)));
+typedef u32x2 u32x2_u __attribute__((aligned(1)));
+typedef uint32_t u32_u __attribute__((aligned(1)));
+#ifndef PBL_LDS_UA8
+#define PBL_LDS_UA8 0
+#endif
+#ifndef PBL_LDS_UA16
+#define PBL_LDS_UA16 1
+#endif
+
+// 16 bytes at LDS byte address a (any alignment)
 __device__ inline uint4 lds_gather16(lptr<const uint32_t> W, uint32_t a) {
+#if !PBL_LDS_UA16
   uint32_t q = a >> 2, r = a & 3;
   uint32_t x0 = W[q], x1 = W[q + 1], x2 = W[q + 2], x3 = W[q + 3], x4 = W[q + 4];
   return make_uint4(__builtin_amdgcn_alignbyte(x1, x0, r), __builtin_amdgcn_alignbyte(x2, x1, r),
                     __builtin_amdgcn_alignbyte(x3, x2, r), __builtin_amdgcn_alignbyte(x4, x3, r));
+#else
+  const u32x4 v = *(lptr<const u32x4_u>)(reinterpret_cast<lptr<const uint8_t>>(W) + a);
+  return make_uint4(v.x, v.y, v.z, v.w);
+#endif
 }
 
 // Read-only view of the staged block: its base offset lives in a register.
@@ -93,17 +115,26 @@ struct View {
   lptr<const uint32_t> W;  // LDS words (array start)
   uint32_t base;      // byte index of block byte 0 (kPad + shift)
   __device__ inline uint32_t byte(uint32_t i) const { return B[base + i]; }
-  // 8 block bytes [i, i+8) as a little-endian u64 (three aligned LDS dword reads)
+  // 8 block bytes [i, i+8) as a little-endian u64
   __device__ inline uint64_t ld8(uint32_t i) const {
+#if !PBL_LDS_UA8
     uint32_t a = base + i, q = a >> 2, r = a & 3;
     uint32_t x0 = W[q], x1 = W[q + 1], x2 = W[q + 2];
     uint32_t lo = __builtin_amdgcn_alignbyte(x1, x0, r);
     uint32_t hi = __builtin_amdgcn_alignbyte(x2, x1, r);
     return uint64_t(hi) << 32 | lo;
+#else
+    const u32x2 v = *(lptr<const u32x2_u>)(B + base + i);
+    return uint64_t(v.y) << 32 | v.x;
+#endif
   }
   __device__ inline uint32_t le32(uint32_t i) const {
+#if !PBL_LDS_UA8
     uint32_t a = base + i, q = a >> 2, r = a & 3;
     return __builtin_amdgcn_alignbyte(W[q + 1], W[q], r);
+#else
+    return *(lptr<const u32_u>)(B + base + i);
+#endif
   }
   // 16 block bytes starting at block offset i (i may be up to 15 below 0)
   __device__ inline uint4 ld16(int32_t i) const { return lds_gather16(W, uint32_t(int32_t(base) + i)); }
@@ -833,7 +864,8 @@ std::atomic<int> g_cus[kMaxDevices];
 std::atomic<int> g_per_cu[kMaxDevices][kKNum];
 }  // namespace
 
-uint64_t persistent_grid(hipStream_t st, PersistentKernel k, const void* fn, uint64_t n_units, int* cus_out) {
+uint64_t persistent_grid(hipStream_t st, PersistentKernel k, const void* fn, uint64_t n_units, int* cus_out,
+                         int block_threads) {
   int dev = -1;
   if (st ? hipStreamGetDevice(st, &dev) != hipSuccess : hipGetDevice(&dev) != hipSuccess) return 0;
   if (dev < 0 || dev >= kMaxDevices) return 0;
@@ -846,7 +878,7 @@ uint64_t persistent_grid(hipStream_t st, PersistentKernel k, const void* fn, uin
     if (hipGetDevice(&cur) != hipSuccess) return 0;
     if (cur != dev && hipSetDevice(dev) != hipSuccess) return 0;
     const bool ok = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-                    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kTPB, 0) == hipSuccess;
+                    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block_threads, 0) == hipSuccess;
     if (cur != dev) (void)hipSetDevice(cur);
     if (!ok) return 0;
     cus = cus > 0 ? cus : 1;
@@ -898,7 +930,8 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
                             : reinterpret_cast<const void*>(pbl::row::pipe::rowblk_pipe_kernel);
     int cus = 0;
     const uint64_t grid = pbl::persistent_grid(st, single ? pbl::kKRowSingle : pbl::kKRowPipe, fn,
-                                               batch->n_blocks, &cus);
+                                               batch->n_blocks, &cus,
+                                               single ? pbl::kTPB : pbl::row::pipe::kPTPB);
     if (!grid) return PBL_DEVICE_ERROR;
     if (single)
       hipLaunchKernelGGL(pbl::row::rowblk_decode_kernel, dim3(uint32_t(grid)), dim3(pbl::kTPB), 0, st, a);
@@ -906,7 +939,8 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
       // sizes of the blocks past the LDS stage first (one wave each, all at once)
       hipLaunchKernelGGL(pbl::row::pipe::big_block_sizes_kernel, dim3(uint32_t(std::min<uint64_t>(
                              batch->n_blocks, uint64_t(cus > 0 ? cus : 1) * 4))), dim3(pbl::kWave), 0, st, a);
-      hipLaunchKernelGGL(pbl::row::pipe::rowblk_pipe_kernel, dim3(uint32_t(grid)), dim3(pbl::kTPB), 0, st, a);
+      hipLaunchKernelGGL(pbl::row::pipe::rowblk_pipe_kernel, dim3(uint32_t(grid)), dim3(pbl::row::pipe::kPTPB), 0,
+                         st, a);
       // then their value bytes (all big blocks at once, bandwidth-bound)
       hipLaunchKernelGGL(pbl::row::pipe::big_block_values_kernel, dim3(uint32_t(std::min<uint64_t>(
                              batch->n_blocks, uint64_t(cus > 0 ? cus : 1) * 4))), dim3(pbl::kWave), 0, st, a);
@@ -954,11 +988,12 @@ int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stre
       int cus = 0;
       const uint64_t grid = pbl::persistent_grid(
           st, pbl::kKRowPipe, reinterpret_cast<const void*>(pbl::row::pipe::rowblk_pipe_kernel), batch->n_blocks,
-          &cus);
+          &cus, pbl::row::pipe::kPTPB);
       if (!grid) return PBL_DEVICE_ERROR;
       const uint32_t small = uint32_t(std::min<uint64_t>(batch->n_blocks, uint64_t(cus) * 4));
       hipLaunchKernelGGL(pbl::row::pipe::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
-      hipLaunchKernelGGL(pbl::row::pipe::rowblk_pipe_kernel, dim3(uint32_t(grid)), dim3(pbl::kTPB), 0, st, a);
+      hipLaunchKernelGGL(pbl::row::pipe::rowblk_pipe_kernel, dim3(uint32_t(grid)), dim3(pbl::row::pipe::kPTPB), 0,
+                         st, a);
     }
     if (hipGetLastError() != hipSuccess) rc = PBL_DEVICE_ERROR;
   }

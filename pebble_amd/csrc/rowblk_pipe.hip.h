@@ -52,7 +52,11 @@ constexpr uint32_t kKeyCap = 32768;            // user-key bytes per block on th
 constexpr int kBs = 7;                         // output bucket = 128 bytes
 constexpr int kKBkt = kKeyCap >> kBs;          // key buckets
 constexpr int kVBkt = kMaxFastLen >> kBs;      // value buckets (values <= block length)
-constexpr int kEmit = kTPB - kWave;            // emitter threads (waves 1-3)
+#ifndef PBL_PIPE_WAVES
+#define PBL_PIPE_WAVES 4
+#endif
+constexpr int kPTPB = PBL_PIPE_WAVES * kWave;  // threads per pipelined workgroup
+constexpr int kEmit = kPTPB - kWave;           // emitter threads (waves 1..)
 
 enum { kModeNone = 0, kModeFast = 1, kModeErr = 2, kModeDone = 3 };
 
@@ -115,6 +119,13 @@ __device__ __forceinline__ bool hdr3(uint64_t w, uint32_t* sh, uint32_t* un, uin
 }
 
 __device__ __forceinline__ bool hdr2(uint64_t w, uint32_t* sh, uint32_t* un, uint32_t* vl, uint32_t* h) {
+  if (__builtin_expect((uint32_t(w) & 0x808080u) == 0, 1)) {  // three 1-byte varints (values < 128)
+    *sh = uint32_t(w) & 0xffu;
+    *un = uint32_t(w >> 8) & 0xffu;
+    *vl = uint32_t(w >> 16) & 0xffu;
+    *h = 3;
+    return true;
+  }
   uint32_t p = 0, v[3];
   bool ok = true;
 #pragma unroll
@@ -865,19 +876,36 @@ __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const 
 #endif
 }
 
-__device__ __forceinline__ void pf_store_to(const PfRegs& pf, uint4* X, uint64_t off, uint32_t len) {
-  const uint64_t a0 = off & ~uint64_t(15);
-  const uint32_t n16 = uint32_t((((off + len + 15) & ~uint64_t(15)) - a0) >> 4);
-  const uint32_t l = threadIdx.x - kWave;
-  lptr<u32x4> dst = to_lds_ptr(reinterpret_cast<u32x4*>(X)) + 1;
-#define PBL_PF_STORE2(i)                                   \
-  {                                                        \
-    const uint32_t g = l + uint32_t(i) * kPfThreads;       \
-    if (g < n16) dst[g] = pf.r##i;                         \
+// The next block, held in registers by the emit waves between their loads
+// (after the emit stores) and the store to LDS after the iteration's first
+// barrier: kPfE granules per emit lane.
+constexpr int kPfE = (kLdsBlkBytes / 16 + kEmit - 1) / kEmit;
+struct PfEmit {
+  u32x4 r[kPfE];
+  __device__ __forceinline__ void load(const uint8_t* blocks, uint64_t off, uint32_t len) {
+    const uint64_t a0 = off & ~uint64_t(15);
+    const uint32_t n16 = uint32_t((((off + len + 15) & ~uint64_t(15)) - a0) >> 4);
+    if (n16 == 0) return;
+    gptr<const u32x4> src = to_glb(reinterpret_cast<const u32x4*>(blocks + a0));
+    const uint32_t l = threadIdx.x - kWave;
+#pragma unroll
+    for (int i = 0; i < kPfE; i++) {
+      const uint32_t g = l + uint32_t(i) * kEmit;
+      r[i] = src[g < n16 ? g : n16 - 1];
+    }
   }
-  PBL_PF_LIST(PBL_PF_STORE2)
-#undef PBL_PF_STORE2
-}
+  __device__ __forceinline__ void store(uint4* X, uint64_t off, uint32_t len) const {
+    const uint64_t a0 = off & ~uint64_t(15);
+    const uint32_t n16 = uint32_t((((off + len + 15) & ~uint64_t(15)) - a0) >> 4);
+    const uint32_t l = threadIdx.x - kWave;
+    lptr<u32x4> dst = to_lds_ptr(reinterpret_cast<u32x4*>(X)) + 1;
+#pragma unroll
+    for (int i = 0; i < kPfE; i++) {
+      const uint32_t g = l + uint32_t(i) * kEmit;
+      if (g < n16) dst[g] = r[i];
+    }
+  }
+};
 
 // The next block, held in registers by the parse wave (64 lanes x 33 granules
 // >= the 2051 granules of the largest staged block) between its load at the
@@ -930,7 +958,7 @@ struct PfWave {
 // X[(i+1)&1] (free again) and rotates the descriptors; the second barrier
 // publishes them.  Each role executes its own copies of the two barriers, so
 // the prefetch registers stay confined to the parse wave's code.
-__global__ void __launch_bounds__(kTPB, 2) rowblk_pipe_kernel(Args A) {
+__global__ void __launch_bounds__(kPTPB) __attribute__((amdgpu_waves_per_eu(PBL_PIPE_WAVES / 2, PBL_PIPE_WAVES / 2))) rowblk_pipe_kernel(Args A) {
   __shared__ PLds S;
   const int t = threadIdx.x;
   const uint32_t nb = A.in.n_blocks;
@@ -950,12 +978,18 @@ __global__ void __launch_bounds__(kTPB, 2) rowblk_pipe_kernel(Args A) {
     }
   }
   __syncthreads();
-  if (t < kWave && S.m[0].b < nb && S.m[0].blen <= kMaxFastLen) {
-    PfWave pf;
-    pf.load(A.in.blocks, S.m[0].boff, S.m[0].blen);
-    pf.store(S.x[0], S.m[0].boff, S.m[0].blen);
+  if (S.m[0].b < nb && S.m[0].blen <= kMaxFastLen) {
+    // prologue: the first block straight into LDS by every thread
+    const uint64_t off = S.m[0].boff;
+    const uint32_t n16 = PfWave::granules(off, S.m[0].blen);
+    gptr<const u32x4> src = to_glb(reinterpret_cast<const u32x4*>(A.in.blocks + (off & ~uint64_t(15))));
+    lptr<u32x4> dst = to_lds_ptr(reinterpret_cast<u32x4*>(S.x[0])) + 1;
+    for (uint32_t g = t; g < n16; g += kPTPB) dst[g] = src[g];
   }
   __syncthreads();
+  // the parse wave is the pipeline's critical path: it wins VALU arbitration
+  // against the emit wave of the other workgroup on its SIMD
+  if (t < kWave) __builtin_amdgcn_s_setprio(2);
   for (uint32_t i = 0;; i++) {
     Meta& cur = S.m[i & 1];
     Meta& prv = S.m[(i + 1) & 1];
@@ -968,7 +1002,7 @@ __global__ void __launch_bounds__(kTPB, 2) rowblk_pipe_kernel(Args A) {
       nx_len = to_glb(A.in.block_len)[nx];
     }
     const bool pf_on = nx < nb && nx_len <= kMaxFastLen;
-    PfRegs pf;
+    PfEmit pf;
     if (t < kWave) {
       if (cb < nb) parse_block(cur, S.x[i & 1], A);
     } else {
@@ -986,7 +1020,7 @@ __global__ void __launch_bounds__(kTPB, 2) rowblk_pipe_kernel(Args A) {
     __syncthreads();
     PSTAMP(A, cb, 13, t == 0 && cb < nb);
     PSTAMP(A, prv.b, 12, t == kWave && prv.mode != kModeNone);
-    if (t >= kWave && pf_on) pf_store_to(pf, S.x[(i + 1) & 1], nx_off, nx_len);
+    if (t >= kWave && pf_on) pf.store(S.x[(i + 1) & 1], nx_off, nx_len);
     if (t == 0) {
       prv.b = nx < nb ? nx : nb;
       prv.boff = nx_off;
