@@ -504,3 +504,60 @@ uint64_t orc_bench(const uint8_t* blocks, const uint64_t* off, const uint32_t* l
   *seconds = (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
   return s;
 }
+
+/* Single-column decode for the per-codec known-answer tests
+ * (tests/test_oracle_codecs.py), over the column bytes the reference's own
+ * codec tests print (sstable/colblk/testdata/{uints,raw_bytes,bitmap,
+ * prefix_bytes}): `off` is the column's start in `buf` (the tests' `offset=`
+ * argument), `rows` its row count.
+ *   kind 0  UnsafeUints.At (uints.go:41-67)            out[i] = value
+ *   kind 1  RawBytes.At (raw_bytes.go:127-141)         out[2i], out[2i+1] = slice [lo, hi) in buf
+ *   kind 2  Bitmap.At (bitmap.go:29-127)               out[i] = bit
+ *   kind 3  PrefixBytes.At (prefix_bytes.go:286-386)   keys[] = the rows' keys back to back,
+ *                                                      out[i] = end offset of key i in keys[]
+ * Returns the column's end offset (the decoder's), or -1 when the decoder
+ * rejects the bytes. */
+int64_t orc_col_decode(const uint8_t* buf, uint64_t len, uint64_t off, uint32_t rows, int kind, uint64_t* out,
+                       uint8_t* keys, uint64_t keys_cap) {
+  coldec c;
+  memset(&c, 0, sizeof(c));
+  c.d.b = buf;
+  c.d.len = len;
+  c.d.rows = rows;
+  uint64_t end = 0;
+  if (kind == 0) {
+    ucol u;
+    if (!dec_uints(&c.d, off, rows, &u, &end) || end > len) return -1;
+    for (uint32_t i = 0; i < rows; i++) out[i] = u_at(&c.d, &u, i);
+  } else if (kind == 1) {
+    rbcol r;
+    if (!dec_rawbytes(&c.d, off, rows, &r, &end)) return -1;
+    for (uint32_t i = 0; i < rows; i++)
+      if (!rb_slice(&c, &r, i, &out[2 * i], &out[2 * i + 1])) return -1;
+  } else if (kind == 2) {
+    bmcol m;
+    if (!dec_bitmap(&c.d, off, rows, &m, &end)) return -1;
+    for (uint32_t i = 0; i < rows; i++) out[i] = (uint64_t)bm_at(&c.d, &m, i);
+  } else if (kind == 3) {
+    c.schema = FMT_COL_DEFAULT;
+    if (!dec_prefix(&c.d, off, rows, &c.keys, &end)) return -1;
+    c.shared_len = (uint32_t)u_at(&c.d, &c.keys.rb.off, 0);
+    c.data_len = (uint32_t)u_at(&c.d, &c.keys.rb.off, c.keys.rb.n);
+    uint64_t n = 0;
+    for (uint32_t i = 0; i < rows; i++) {
+      uint64_t bl, bh, sl, sh;
+      if (!pb_parts(&c, i, &bl, &bh, &sl, &sh)) return -1;
+      const uint64_t parts[3][2] = {{c.keys.rb.data, c.keys.rb.data + c.shared_len}, {bl, bh}, {sl, sh}};
+      for (int k = 0; k < 3; k++) {
+        const uint64_t m = parts[k][1] - parts[k][0];
+        if (n + m > keys_cap) return -1;
+        memcpy(keys + n, buf + parts[k][0], m);
+        n += m;
+      }
+      out[i] = n;
+    }
+  } else {
+    return -1;
+  }
+  return (int64_t)end;
+}

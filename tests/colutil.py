@@ -113,3 +113,60 @@ def build_block(schema: int, rows, bundle: int = 16):
             fl |= N.PBL_KV_VALBLK_HANDLE if vk == VALUE_BLOCK_HANDLE else N.PBL_KV_BLOB_HANDLE
         exp.append((expected_key(schema, k), tr, val, fl, i))
     return w.finish(), exp
+
+
+# ---- raw DefaultKeySchema data-block assembly (per-codec embedding) ----------------
+# Layout (sstable/colblk/block.go:10-56, data_block.go:600-833): maximum key length
+# LE32 (DataBlockCustomHeaderSize), version 1, 7 columns LE16, rows LE32, then per
+# column {type u8, page offset LE32}, the pages, one 0x00 pad byte.  Columns of
+# colblk.DefaultKeySchema: prefix (PrefixBytes), suffix (RawBytes), trailers (Uint),
+# prefixChanged (Bitmap), values (RawBytes), isValueExternal (Bitmap), isObsolete (Bitmap).
+DEFAULT_COL_TYPES = [4, 3, 2, 1, 3, 1, 1]
+COL_PREFIX, COL_SUFFIX, COL_TRAILERS, COL_PREFIX_CHANGED, COL_VALUES, COL_EXTERNAL, COL_OBSOLETE = range(7)
+
+
+def _suffix_column(rows: int, tail: int) -> bytes:
+    """RawBytes of `rows` slices, all empty but the last (`tail` bytes of 'z')."""
+    if tail == 0:
+        return b"\x00"  # offsets all zero: uint zero encoding, no data
+    assert tail < 256
+    return bytes([1]) + bytes(rows) + bytes([tail]) + b"z" * tail
+
+
+def default_columns(rows: int) -> list:
+    """Minimal valid columns for `rows` rows: empty keys and values, zero
+    trailers, zero bitmaps."""
+    return [bytes([4, 0]),  # PrefixBytes, bundle shift 4, RawBytes offsets all zero
+            b"\x00", b"\x00", b"\x01", b"\x00", b"\x01", b"\x01"]
+
+
+def assemble_block(cols: list, rows: int, max_key_len: int) -> bytes:
+    hdr = 4 + 7 + 5 * len(cols)
+    offs, pos = [], hdr
+    for c in cols:
+        offs.append(pos)
+        pos += len(c)
+    out = bytearray(max_key_len.to_bytes(4, "little") + bytes([1]) + len(cols).to_bytes(2, "little")
+                    + rows.to_bytes(4, "little"))
+    for t, o in zip(DEFAULT_COL_TYPES, offs):
+        out += bytes([t]) + o.to_bytes(4, "little")
+    for c in cols:
+        out += c
+    return bytes(out + b"\x00")
+
+
+def embed_column(col: int, col_bytes: bytes, col_offset: int, rows: int, max_key_len: int = 0) -> bytes:
+    """A DefaultKeySchema block whose column `col` is `col_bytes` (a column the
+    reference's codec tests printed, `col_offset` = its start in those bytes'
+    buffer), placed at a block offset congruent to it mod 8 so that its
+    internal alignment padding stays valid (the suffix column's last slice
+    absorbs the shift; col_bytes must come after it)."""
+    assert col > COL_SUFFIX or col == COL_PREFIX
+    cols = default_columns(rows)
+    cols[col] = col_bytes
+    for tail in range(0, 9):
+        cols[COL_SUFFIX] = _suffix_column(rows, tail)
+        start = 4 + 7 + 5 * len(cols) + sum(len(c) for c in cols[:col])
+        if col == COL_PREFIX or start % 8 == col_offset % 8:
+            return assemble_block(cols, rows, max(max_key_len, tail))
+    raise AssertionError("unreachable")

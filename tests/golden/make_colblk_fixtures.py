@@ -212,22 +212,67 @@ def crdb1_cases():
              "writer_rows": [dict(r, key=r["in_key"]) for r in rows], "finish_rows": len(rows)}]
 
 
+def _args(cmd: str) -> dict:
+    out = {}
+    for tok in cmd.split()[1:]:
+        k, _, v = tok.partition("=")
+        out[k] = v if v else True
+    return out
+
+
 def codec_cases():
-    """Per-codec dumps (uints, raw_bytes, prefix_bytes, bitmap) are recorded
-    verbatim so codec decoders can be pinned individually."""
+    """Per-codec dumps (uints, raw_bytes, prefix_bytes, bitmap) recorded
+    verbatim, each with the values a decoder must return, derived from the
+    reference test's own inputs (never from the dump):
+      uints         the `write i:v` lines since the last `init` (unwritten rows 0)
+                    (uints_test.go TestUints)
+      raw_bytes     the `build` input lines (first `count=` of them)
+                    (raw_bytes_test.go)
+      prefix_bytes  the keys `put` since the last `init` (first `rows=` of them)
+                    (prefix_bytes_test.go; `get`/`unsafe-get` print the same keys)
+      bitmap        the bit string the reference's own DecodeBitmap printed (the
+                    lines before "Binary representation:") (bitmap_test.go:25-70)
+    `offset` is where the column starts in the bytes."""
     out = {}
     for fn in ("uints", "raw_bytes", "prefix_bytes", "bitmap"):
         path = os.path.join(REF, "sstable/colblk/testdata", fn)
         rel = os.path.relpath(path, REF)
         lst = []
+        writes, puts = {}, []
         for c in parse_datadriven(path):
-            if LINE.search(c["expected"]) and not c["expected"].startswith("error"):
-                try:
-                    blk = dump_to_bytes(c["expected"])
-                except AssertionError:
-                    continue
-                lst.append({"source": f"{rel}:{c['line']}", "cmd": c["cmd"], "input": c["input"],
-                            "bytes": blk.hex(), "dump": c["expected"]})
+            a = _args(c["cmd"])
+            verb = c["cmd"].split()[0]
+            if verb == "init":
+                writes, puts = {}, []
+            elif verb == "write":
+                for f in c["input"].split():
+                    i, v = f.split(":")
+                    writes[int(i)] = int(v)
+            elif verb == "put":
+                puts += [k for k in c["input"].strip().split("\n")]
+            if not (LINE.search(c["expected"]) and not c["expected"].startswith("error")):
+                continue
+            try:
+                blk = dump_to_bytes(c["expected"])
+            except AssertionError:
+                continue
+            e = {"source": f"{rel}:{c['line']}", "cmd": c["cmd"], "input": c["input"], "bytes": blk.hex(),
+                 "dump": c["expected"], "offset": int(a.get("offset", 0))}
+            if fn == "uints" and verb == "finish":
+                rows = int(a["rows"])
+                e.update(rows=rows, expect=[writes.get(i, 0) for i in range(rows)])
+            elif fn == "raw_bytes" and verb == "build":
+                sl = c["input"].split("\n")
+                if "count" in a:
+                    sl = sl[: int(a["count"])]
+                e.update(rows=len(sl), expect=[x.encode().hex() for x in sl])
+            elif fn == "prefix_bytes" and verb == "finish":
+                rows = int(a["rows"])
+                e.update(rows=rows, expect=[k.encode().hex() for k in puts[:rows]])
+            elif fn == "bitmap" and verb == "build":
+                bits = "".join(c["expected"].split("Binary representation:")[0].split())
+                e.update(rows=len(bits), expect=[int(ch) for ch in bits])
+            lst.append(e)
         out[fn] = lst
     return out
 

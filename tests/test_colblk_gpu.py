@@ -143,3 +143,17 @@ def test_new_data_block_iter():
     assert b"d@11" not in ks  # the obsolete row is hidden
     with pytest.raises(CorruptionError):
         NewDataBlockIter(bytes.fromhex(c["block"])[:12], SCHEMA_DEFAULT)
+
+
+def test_codec_columns_in_device_blocks():
+    """The per-codec columns of the reference's codec tests (uints, raw_bytes,
+    bitmap, prefix_bytes; tests/test_oracle_codecs.py) embedded in data blocks
+    and decoded on the device: bit-exact with the oracle, and each embedded
+    column yields the values the reference's test wrote."""
+    from test_oracle_codecs import decoded_field, embedded_blocks, expected_field
+    blocks = embedded_blocks()
+    for align in (8, 16):
+        g = check(*pack([b for _, _, b in blocks], align), SCHEMA_DEFAULT, ctx=f"codecs align={align}")
+        for i, (codec, e, _) in enumerate(blocks):
+            kvs = [(kv.user_key, kv.trailer, kv.value, kv.flags, 0) for kv in kvs_of_block(g, i)]
+            assert decoded_field(codec, kvs) == expected_field(codec, e), e["source"]
