@@ -210,6 +210,42 @@ int pbl_rebase_blocks(pbl_decode_out* out, uint32_t n_blocks, uint64_t kv_base,
 int pbl_offset_concat(pbl_decode_out* out, uint32_t n_blocks, const uint64_t* rank_totals,
                       uint32_t rank, void* stream);
 
+/* ---- blockiter.Transforms on the device ------------------ */
+/* Comparer.Split used to find the suffix a SyntheticSuffix replaces. */
+enum {
+  PBL_SPLIT_WHOLE = 0,    /* base.DefaultSplit: no suffix (internal/base/comparer.go:206-208) */
+  PBL_SPLIT_TESTKEYS = 1, /* testkeys.Comparer: before the last '@' (internal/testkeys/testkeys.go:144-150) */
+  PBL_SPLIT_CRDB = 2      /* cockroachkvs.Split: last byte = version length (cockroachkvs/cockroachkvs.go:298-309) */
+};
+typedef struct pbl_transforms {
+  uint64_t synthetic_seq_num;    /* blockiter.SyntheticSeqNum; 0 = unset (transforms.go:90-99) */
+  uint32_t hide_obsolete_points; /* drop PBL_KV_OBSOLETE KVs (transforms.go:24-27)            */
+  uint32_t split;                /* PBL_SPLIT_* (only used with a suffix)                     */
+  const uint8_t* prefix;         /* DEVICE bytes of the SyntheticPrefix (transforms.go:120-162) */
+  const uint8_t* suffix;         /* DEVICE bytes of the SyntheticSuffix (transforms.go:101-118) */
+  uint32_t prefix_len, suffix_len;
+} pbl_transforms;
+
+/* Device scratch pbl_transform_batch needs in out->workspace. */
+uint64_t pbl_transform_workspace_bytes(uint32_t n_blocks);
+
+/*
+ * Apply `t` to a decoded batch (`in`, as pbl_decode_batch left it, n_blocks
+ * blocks) into `out` (same layout contract; caller-allocated; out->workspace of
+ * pbl_transform_workspace_bytes): every visible KV (HideObsoletePoints drops the
+ * obsolete ones) keeps its order, flags, entry offset and value; its trailer
+ * takes the synthetic sequence number (InternalKey.SetSeqNum); its user key
+ * becomes prefix ++ key[:Split(key)] ++ suffix (suffix set) or prefix ++ key;
+ * keys of PBL_KV_INVALID_KEY entries stay empty.  Restart words and statuses
+ * are the input's.  Three stream-ordered launches (count, scan, scatter); on a
+ * capacity overflow every decodable block reports PBL_OVERFLOW and only sizes
+ * are written.  Replaces the iteration-time transforms of rowblk.Iter
+ * (rowblk_iter.go:400,487-517,1168-1187) and colblk.DataBlockIter
+ * (data_block.go:1299-1303,1437-1462,1680-1697) for a whole batch.
+ */
+int pbl_transform_batch(const pbl_decode_out* in, uint32_t n_blocks, const pbl_transforms* t, pbl_decode_out* out,
+                        void* stream);
+
 /* ---- rowblk.Writer (format producer; host memory) ---------------------------- */
 typedef struct pbl_rowblk_writer pbl_rowblk_writer;
 pbl_rowblk_writer* pbl_rowblk_writer_new(int restart_interval);

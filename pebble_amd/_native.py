@@ -103,6 +103,17 @@ class DecodeOutC(ctypes.Structure):
     ]
 
 
+PBL_SPLIT_WHOLE, PBL_SPLIT_TESTKEYS, PBL_SPLIT_CRDB = 0, 1, 2
+
+
+class TransformsC(ctypes.Structure):
+    _fields_ = [
+        ("synthetic_seq_num", ctypes.c_uint64), ("hide_obsolete_points", ctypes.c_uint32),
+        ("split", ctypes.c_uint32), ("prefix", _vp), ("suffix", _vp),
+        ("prefix_len", ctypes.c_uint32), ("suffix_len", ctypes.c_uint32),
+    ]
+
+
 # Every symbol include/pebble_amd.h declares, with its ctypes signature.
 SIGNATURES = {
     "pbl_abi_version": (ctypes.c_int, []),
@@ -110,6 +121,9 @@ SIGNATURES = {
     "pbl_decode_batch": (ctypes.c_int, [ctypes.POINTER(BlockBatchC), ctypes.POINTER(DecodeOutC), _vp]),
     "pbl_size_batch": (ctypes.c_int, [ctypes.POINTER(BlockBatchC), ctypes.POINTER(DecodeOutC), _vp]),
     "pbl_struct_layout": (ctypes.c_size_t, [_vp, ctypes.c_size_t]),
+    "pbl_transform_workspace_bytes": (ctypes.c_uint64, [ctypes.c_uint32]),
+    "pbl_transform_batch": (ctypes.c_int, [ctypes.POINTER(DecodeOutC), ctypes.c_uint32, ctypes.POINTER(TransformsC),
+                                           ctypes.POINTER(DecodeOutC), _vp]),
     "pbl_rebase_blocks": (ctypes.c_int, [ctypes.POINTER(DecodeOutC), ctypes.c_uint32, ctypes.c_uint64,
                                          ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _vp]),
     "pbl_offset_concat": (ctypes.c_int, [ctypes.POINTER(DecodeOutC), ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]),

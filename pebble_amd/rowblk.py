@@ -52,9 +52,14 @@ class InternalKV:
 
 @dataclass
 class Transforms:
-    """blockiter.Transforms subset applied at iteration time (transforms.go:20-56)."""
+    """blockiter.Transforms (sstable/blockiter/transforms.go:20-56).  Iter
+    applies synthetic_seq_num and hide_obsolete_points while iterating; a whole
+    decoded batch takes all four on the device (pebble_amd.transforms)."""
     synthetic_seq_num: int = 0
     hide_obsolete_points: bool = False
+    synthetic_prefix: bytes = b""
+    synthetic_suffix: bytes = b""
+    split: int = 0  # PBL_SPLIT_*: the comparer's Split (finds the suffix a synthetic suffix replaces)
 
 
 class Writer:

@@ -1,0 +1,59 @@
+"""blockiter.Transforms over a decoded batch on the device.
+
+`apply_transforms(decoded, t)` runs `pbl_transform_batch` (pebble_amd/csrc/
+transforms.hip): SyntheticSeqNum, HideObsoletePoints, SyntheticPrefix and
+SyntheticSuffix (sstable/blockiter/transforms.go:20-248) applied to every block
+of a batch `pbl_decode_batch` produced, into a new DecodedBatch with the same
+layout contract.  Pebble applies them per KV inside rowblk.Iter / colblk.
+DataBlockIter (rowblk_iter.go:400,487-517,1168-1187; data_block.go:1299-1303,
+1437-1462,1680-1697); here it is one HBM-bound pass per batch.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from . import _native as N
+from .batch import Capacity, DecodedBatch, DecodeError, _stream_handle
+from .rowblk import Transforms
+
+__all__ = ["Transforms", "apply_transforms"]
+
+
+def _dev_bytes(b: bytes, device) -> Optional[torch.Tensor]:
+    if not b:
+        return None
+    return torch.tensor(list(b), dtype=torch.uint8, device=device)
+
+
+def apply_transforms(d: DecodedBatch, t: Transforms, stream=None, cap: Optional[Capacity] = None) -> DecodedBatch:
+    """Transform decoded batch `d` (its totals must be final: call after the
+    decode's stream synchronised).  Output capacities default to exact upper
+    bounds: every KV kept, every key grown by prefix + suffix."""
+    tot = d.read_totals()
+    n_kv, kb, vb, nr = int(tot.n_kv), int(tot.key_bytes), int(tot.val_bytes), int(tot.n_restarts)
+    grow = len(t.synthetic_prefix) + len(t.synthetic_suffix)
+    cap = cap or Capacity(kv=n_kv, key=kb + grow * n_kv, val=vb, rst=nr)
+    dev = d.trailer.device
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
+    with torch.cuda.stream(st):
+        out = DecodedBatch.allocate(d.n_blocks, cap, dev, entry_off=d.entry_off is not None,
+                                    restarts=d.restarts is not None)
+        ws = int(N.lib().pbl_transform_workspace_bytes(d.n_blocks))
+        if out.workspace.numel() < ws:
+            out.workspace = torch.empty(ws, dtype=torch.uint8, device=dev)
+        pfx = _dev_bytes(t.synthetic_prefix, dev)
+        sfx = _dev_bytes(t.synthetic_suffix, dev)
+    tc = N.TransformsC(t.synthetic_seq_num, 1 if t.hide_obsolete_points else 0, t.split,
+                       pfx.data_ptr() if pfx is not None else None, sfx.data_ptr() if sfx is not None else None,
+                       len(t.synthetic_prefix), len(t.synthetic_suffix))
+    i, o = d.c_struct(), out.c_struct()
+    rc = N.lib().pbl_transform_batch(ctypes.byref(i), d.n_blocks, ctypes.byref(tc), ctypes.byref(o),
+                                     _stream_handle(st))
+    if rc != N.PBL_OK:
+        raise DecodeError(f"pbl_transform_batch failed: {N.STATUS_NAMES.get(rc, rc)}")
+    st.synchronize()  # (the prefix / suffix tensors are released on return)
+    out.read_totals()
+    return out

@@ -85,8 +85,9 @@ def parse_ikey(s: str):
 
 
 def testkeys_split(k: bytes) -> int:
-    """testkeys.Comparer.Split: prefix is everything before the first '@'."""
-    i = k.find(b"@")
+    """testkeys.Comparer.Split: prefix is everything before the last '@'
+    (internal/testkeys/testkeys.go:144-150)."""
+    i = k.rfind(b"@")
     return len(k) if i < 0 else i
 
 
@@ -277,13 +278,63 @@ def codec_cases():
     return out
 
 
+ITER_LINE = re.compile(r"^\s*(first|next):\s*(.*)$")
+
+
+def transform_cases():
+    """sstable/colblk/testdata/data_block/transforms: each `write-block` (rows
+    the DataBlockEncoder saw, data_block_test.go:76-109) with the `iter <args>`
+    cases run over it (args: synthetic-seq-num, hide-obsolete-points,
+    synthetic-prefix, synthetic-suffix; data_block_test.go:140-160).  Kept: the
+    forward scan each case prints from `first` through its consecutive `next`
+    commands, as (user key, seq or None, kind or None, value) rows; None after
+    the last row = the iterator was exhausted ('.')."""
+    path = os.path.join(REF, "sstable/colblk/testdata/data_block/transforms")
+    rel = os.path.relpath(path, REF)
+    out, rows = [], None
+    for c in parse_datadriven(path):
+        cmd = c["cmd"].split()
+        if cmd[0] == "write-block":
+            rows = default_schema_rows([l for l in c["input"].split("\n") if l])
+            out.append({"source": f"{rel}:{c['line']}", "rows": rows, "iters": []})
+        elif cmd[0] == "iter":
+            cmds = [l.strip() for l in c["input"].split("\n") if l.strip()]
+            if not cmds or cmds[0] != "first":
+                continue
+            n = 1
+            while n < len(cmds) and cmds[n] == "next":
+                n += 1
+            seq = []
+            for line in c["expected"].split("\n")[:n]:
+                m = ITER_LINE.match(line)
+                assert m, line
+                body = m.group(2).strip()
+                if body == ".":
+                    seq.append(None)
+                    break
+                k, _, v = body.partition(":")
+                if "#" in k:
+                    uk, tr = parse_ikey(k)
+                    seq.append([uk.hex(), tr >> 8, tr & 0xFF, v.encode().hex()])
+                else:
+                    seq.append([k.encode().hex(), None, None, v.encode().hex()])
+            args = _args(c["cmd"])
+            out[-1]["iters"].append({"line": c["line"], "seq_num": int(args.get("synthetic-seq-num", 0)),
+                                     "hide_obsolete": bool(args.get("hide-obsolete-points", False)),
+                                     "prefix": str(args.get("synthetic-prefix", "")).encode().hex(),
+                                     "suffix": str(args.get("synthetic-suffix", "")).encode().hex(),
+                                     "forward": seq})
+    return out
+
+
 def main():
     cases = data_block_cases() + crdb1_cases()
-    res = {"data_blocks": cases, "codecs": codec_cases()}
+    res = {"data_blocks": cases, "codecs": codec_cases(), "transforms": transform_cases()}
     p = os.path.join(HERE, "colblk_golden.json")
     with open(p, "w") as f:
         json.dump(res, f, indent=1)
-    print("wrote", p, len(cases), "data blocks,", {k: len(v) for k, v in res["codecs"].items()}, "codec dumps")
+    print("wrote", p, len(cases), "data blocks,", {k: len(v) for k, v in res["codecs"].items()}, "codec dumps,",
+          sum(len(t["iters"]) for t in res["transforms"]), "transform scans")
 
 
 if __name__ == "__main__":
