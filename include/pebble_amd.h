@@ -53,7 +53,9 @@ enum {
   PBL_OVERFLOW = 6,              /* an output capacity was too small: nothing written */
   PBL_INVALID_ARG = 7,
   PBL_DEVICE_ERROR = 8,
-  PBL_TIMEOUT = 9                /* in-kernel look-back spin bound hit (never expected) */
+  PBL_TIMEOUT = 9,               /* in-kernel look-back spin bound hit (never expected) */
+  PBL_CORRUPT_CHECKSUM = 10,     /* block.go:177-195 "checksum mismatch"        */
+  PBL_CORRUPT_COMPRESSION = 11   /* snappy.ErrCorrupt -> base.MarkCorruptionError (block.go:550-565) */
 };
 
 /* ---- block formats ---------------------------------------------------------- */
@@ -209,6 +211,49 @@ int pbl_rebase_blocks(pbl_decode_out* out, uint32_t n_blocks, uint64_t kv_base,
  */
 int pbl_offset_concat(pbl_decode_out* out, uint32_t n_blocks, const uint64_t* rank_totals,
                       uint32_t rank, void* stream);
+
+/* ---- physical blocks: checksums and decompression --------- */
+/* Blocks as they sit in an SST: [block bytes][compression indicator u8][checksum
+ * LE32] (sstable/block/block.go:539-571); block_len is the block.Handle length
+ * (the 5-byte trailer follows it). */
+typedef struct pbl_phys_batch {
+  const uint8_t* bytes;      /* DEVICE bytes                                           */
+  const uint64_t* block_off; /* [n_blocks] DEVICE offset of each block in `bytes`        */
+  const uint32_t* block_len; /* [n_blocks] DEVICE block.Handle.Length (trailer excluded) */
+  uint32_t n_blocks;
+  uint32_t reserved;
+} pbl_phys_batch;
+enum { /* block.ChecksumType (block.go:106-114) */
+  PBL_CHECKSUM_NONE = 0, PBL_CHECKSUM_CRC32C = 1, PBL_CHECKSUM_XXHASH = 2, PBL_CHECKSUM_XXHASH64 = 3
+};
+enum { /* block.CompressionIndicator (compression.go:170-193) */
+  PBL_COMPRESSION_NONE = 0, PBL_COMPRESSION_SNAPPY = 1, PBL_COMPRESSION_ZSTD = 7, PBL_COMPRESSION_MINLZ = 8
+};
+
+/*
+ * ValidateChecksum (block.go:164-197) for every block: status[b] = PBL_OK or
+ * PBL_CORRUPT_CHECKSUM; computed[b] (optional) = the checksum computed over the
+ * block bytes and the indicator byte.  CRC32C (internal/crc: Castagnoli, then
+ * Value()'s rotation and delta) or XXH64 truncated to 32 bits; other types return
+ * PBL_UNSUPPORTED.
+ */
+int pbl_verify_checksums(const pbl_phys_batch* batch, uint32_t checksum_type, uint32_t* status, uint32_t* computed,
+                         void* stream);
+/*
+ * Decompressor.DecompressedLen (block.go:549-556) of every block: out_len[b];
+ * status[b] = PBL_OK, PBL_CORRUPT_COMPRESSION or PBL_UNSUPPORTED (zstd, minlz and
+ * the legacy codecs are not decoded on the device).
+ */
+int pbl_decompressed_lengths(const pbl_phys_batch* batch, uint32_t* out_len, uint32_t* status, void* stream);
+/*
+ * DecompressInto (block.go:557-565): block b's decoded bytes at out + out_off[b]
+ * (out_cap[b] bytes available; DEVICE arrays), its length in out_len[b] and
+ * status[b] = PBL_OK / PBL_CORRUPT_COMPRESSION / PBL_OVERFLOW / PBL_UNSUPPORTED.
+ * Uncompressed blocks are copied.  The outputs form a pbl_block_batch {out,
+ * out_off, out_len} for pbl_decode_batch (keep out_off 8-B aligned for colblk).
+ */
+int pbl_decompress_blocks(const pbl_phys_batch* batch, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                          uint32_t* out_len, uint32_t* status, void* stream);
 
 /* ---- blockiter.Transforms on the device ------------------ */
 /* Comparer.Split used to find the suffix a SyntheticSuffix replaces. */

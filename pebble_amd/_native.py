@@ -24,11 +24,15 @@ PBL_OVERFLOW = 6
 PBL_INVALID_ARG = 7
 PBL_DEVICE_ERROR = 8
 PBL_TIMEOUT = 9
+PBL_CORRUPT_CHECKSUM = 10
+PBL_CORRUPT_COMPRESSION = 11
 STATUS_NAMES = {
     0: "OK", 1: "CORRUPT_NO_RESTARTS", 2: "CORRUPT_FIRST_KEY", 3: "CORRUPT_BOUNDS",
     4: "CORRUPT_COLBLK_HEADER", 5: "UNSUPPORTED", 6: "OVERFLOW", 7: "INVALID_ARG",
-    8: "DEVICE_ERROR", 9: "TIMEOUT",
+    8: "DEVICE_ERROR", 9: "TIMEOUT", 10: "CORRUPT_CHECKSUM", 11: "CORRUPT_COMPRESSION",
 }
+PBL_CHECKSUM_NONE, PBL_CHECKSUM_CRC32C, PBL_CHECKSUM_XXHASH, PBL_CHECKSUM_XXHASH64 = 0, 1, 2, 3
+PBL_COMPRESSION_NONE, PBL_COMPRESSION_SNAPPY, PBL_COMPRESSION_ZSTD, PBL_COMPRESSION_MINLZ = 0, 1, 7, 8
 
 ABI_VERSION = 3  # include/pebble_amd.h PBL_ABI_VERSION
 
@@ -106,6 +110,11 @@ class DecodeOutC(ctypes.Structure):
 PBL_SPLIT_WHOLE, PBL_SPLIT_TESTKEYS, PBL_SPLIT_CRDB = 0, 1, 2
 
 
+class PhysBatchC(ctypes.Structure):
+    _fields_ = [("bytes", _vp), ("block_off", _vp), ("block_len", _vp), ("n_blocks", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
 class TransformsC(ctypes.Structure):
     _fields_ = [
         ("synthetic_seq_num", ctypes.c_uint64), ("hide_obsolete_points", ctypes.c_uint32),
@@ -122,6 +131,9 @@ SIGNATURES = {
     "pbl_size_batch": (ctypes.c_int, [ctypes.POINTER(BlockBatchC), ctypes.POINTER(DecodeOutC), _vp]),
     "pbl_struct_layout": (ctypes.c_size_t, [_vp, ctypes.c_size_t]),
     "pbl_transform_workspace_bytes": (ctypes.c_uint64, [ctypes.c_uint32]),
+    "pbl_verify_checksums": (ctypes.c_int, [ctypes.POINTER(PhysBatchC), ctypes.c_uint32, _vp, _vp, _vp]),
+    "pbl_decompressed_lengths": (ctypes.c_int, [ctypes.POINTER(PhysBatchC), _vp, _vp, _vp]),
+    "pbl_decompress_blocks": (ctypes.c_int, [ctypes.POINTER(PhysBatchC), _vp, _vp, _vp, _vp, _vp, _vp]),
     "pbl_transform_batch": (ctypes.c_int, [ctypes.POINTER(DecodeOutC), ctypes.c_uint32, ctypes.POINTER(TransformsC),
                                            ctypes.POINTER(DecodeOutC), _vp]),
     "pbl_rebase_blocks": (ctypes.c_int, [ctypes.POINTER(DecodeOutC), ctypes.c_uint32, ctypes.c_uint64,

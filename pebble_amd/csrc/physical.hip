@@ -1,0 +1,408 @@
+// physical.hip — the physical-block step before data-block decode, on the
+// device: checksum validation and decompression of blocks
+// as they sit in an SST file, [block bytes][compression indicator u8]
+// [checksum LE32] (sstable/block/block.go:539-571).
+//
+//   checksum_crc_kernel   CRC32C (internal/crc/crc.go): one wave per block;
+//                         each lane CRCs a contiguous chunk (slicing-by-4 from an
+//                         LDS table), the wave folds the 64 chunk CRCs with the
+//                         GF(2) shift operator (crc(A||B) = crc(A)*x^(8|B|) +
+//                         crc(B) mod P), then Value()'s rotation + delta
+//   checksum_xxh_kernel   XXH64 truncated to 32 bits (cespare/xxhash/v2, the
+//                         ChecksumTypeXXHash64 of block.go:155-160): one lane
+//                         per block (XXH64's stripes are sequential)
+//   snappy_len_kernel     the decoded length (uvarint header, snappy.DecodedLen)
+//   snappy_kernel         snappy.Decode (golang/snappy block format): one wave
+//                         per block, compressed bytes and output staged in LDS;
+//                         lane 0 walks the elements, the wave copies each one
+//                         (an overlapping copy repeats its period: byte i of a
+//                         copy reads dst[d - off + i % off], all before d)
+// Zstd (indicator 7) and the other codecs report PBL_UNSUPPORTED.
+#include <algorithm>
+
+#include "common.hip.h"
+
+namespace pbl {
+namespace phys {
+
+constexpr uint32_t kPoly = 0x82F63B78u;  // reflected Castagnoli
+
+// GF(2) polynomial product a*b mod P, reflected (zlib's multmodp)
+__device__ inline uint32_t multmodp(uint32_t a, uint32_t b) {
+  uint32_t m = 1u << 31, p = 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = (b & 1) ? (b >> 1) ^ kPoly : b >> 1;
+  }
+  return p;
+}
+
+struct CrcLds {
+  uint32_t tab[4][256];  // slicing-by-4
+  uint32_t x2n[32];      // x^(2^k) mod P
+};
+
+__device__ inline void crc_tables(CrcLds& L) {
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ kPoly : c >> 1;
+    L.tab[0][i] = c;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+    uint32_t c = L.tab[0][i];
+    for (int s = 1; s < 4; s++) {
+      c = L.tab[0][c & 0xff] ^ (c >> 8);
+      L.tab[s][i] = c;
+    }
+  }
+  if (threadIdx.x == 0) {
+    uint32_t p = 1u << 30;  // x^1
+    L.x2n[0] = p;
+    for (int k = 1; k < 32; k++) L.x2n[k] = p = multmodp(p, p);
+  }
+  __syncthreads();
+}
+
+// x^(8n) mod P
+__device__ inline uint32_t x8nmodp(const CrcLds& L, uint64_t n) {
+  uint32_t p = 1u << 31;  // x^0
+  int k = 3;
+  while (n) {
+    if (n & 1) p = multmodp(L.x2n[k & 31], p);
+    n >>= 1;
+    k++;
+  }
+  return p;
+}
+
+// Go's crc32.Update(0, castagnoli, p[0:n]) of one lane's chunk (conditioned)
+__device__ inline uint32_t crc_chunk(const CrcLds& L, gptr<const uint8_t> p, uint64_t n) {
+  uint32_t c = ~0u;
+  uint64_t i = 0;
+  // byte steps up to a 4-B boundary, then 4-B slices, then the tail
+  while (i < n && ((uint64_t(p) + i) & 3)) c = L.tab[0][(c ^ p[i++]) & 0xff] ^ (c >> 8);
+  for (; i + 4 <= n; i += 4) {
+    c ^= *(gptr<const uint32_t>)(p + i);
+    c = L.tab[3][c & 0xff] ^ L.tab[2][(c >> 8) & 0xff] ^ L.tab[1][(c >> 16) & 0xff] ^ L.tab[0][c >> 24];
+  }
+  for (; i < n; i++) c = L.tab[0][(c ^ p[i]) & 0xff] ^ (c >> 8);
+  return ~c;
+}
+
+__global__ void __launch_bounds__(kTPB) checksum_crc_kernel(const pbl_phys_batch B, uint32_t* status,
+                                                            uint32_t* computed) {
+  __shared__ CrcLds L;
+  crc_tables(L);
+  const uint32_t lane = lane_id(), wpb = kTPB / kWave;
+  for (uint32_t b = blockIdx.x * wpb + wave_id(); b < B.n_blocks; b += gridDim.x * wpb) {
+    const uint64_t n = uint64_t(B.block_len[b]) + 1;  // the block and its compression indicator
+    const gptr<const uint8_t> p = to_glb(B.bytes + B.block_off[b]);
+    const uint64_t chunk = ((n + kWave - 1) / kWave + 3) & ~uint64_t(3);
+    const uint64_t lo = min<uint64_t>(n, lane * chunk), hi = min<uint64_t>(n, lo + chunk);
+    uint32_t c = crc_chunk(L, p + lo, hi - lo);
+    uint32_t len = uint32_t(hi - lo);
+    // fold: lane l absorbs lane l+d (the chunk after it) at each level
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint32_t c2 = __shfl_down(c, d, kWave);
+      const uint32_t l2 = __shfl_down(len, d, kWave);
+      if ((lane & (2 * d - 1)) == 0 && lane + d < kWave) {
+        if (l2) c = multmodp(x8nmodp(L, l2), c) ^ c2;
+        len += l2;
+      }
+    }
+    if (lane == 0) {
+      const uint32_t v = ((c >> 15) | (c << 17)) + 0xa282ead8u;  // crc.CRC.Value()
+      const gptr<const uint8_t> t = p + (n - 1) + 1;
+      const uint32_t want = uint32_t(t[0]) | uint32_t(t[1]) << 8 | uint32_t(t[2]) << 16 | uint32_t(t[3]) << 24;
+      status[b] = v == want ? PBL_OK : PBL_CORRUPT_CHECKSUM;
+      if (computed) computed[b] = v;
+    }
+  }
+}
+
+// ---- XXH64 (the XXH64 specification; cespare/xxhash/v2 implements it) ---------
+constexpr uint64_t P1 = 11400714785074694791ull, P2 = 14029467366897019727ull, P3 = 1609587929392839161ull,
+                   P4 = 9650029242287828579ull, P5 = 2870177450012600261ull;
+__device__ inline uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+__device__ inline uint64_t xround(uint64_t acc, uint64_t in) { return rotl(acc + in * P2, 31) * P1; }
+__device__ inline uint64_t xmerge(uint64_t acc, uint64_t v) { return (acc ^ xround(0, v)) * P1 + P4; }
+__device__ inline uint64_t ld64(gptr<const uint8_t> p) {
+  uint64_t v = 0;
+  for (int i = 7; i >= 0; i--) v = v << 8 | p[i];
+  return v;
+}
+
+__device__ inline uint64_t xxh64(gptr<const uint8_t> p, uint64_t n) {
+  uint64_t h, i = 0;
+  if (n >= 32) {
+    uint64_t v1 = P1 + P2, v2 = P2, v3 = 0, v4 = 0ull - P1;
+    for (; i + 32 <= n; i += 32) {
+      v1 = xround(v1, ld64(p + i));
+      v2 = xround(v2, ld64(p + i + 8));
+      v3 = xround(v3, ld64(p + i + 16));
+      v4 = xround(v4, ld64(p + i + 24));
+    }
+    h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+    h = xmerge(h, v1);
+    h = xmerge(h, v2);
+    h = xmerge(h, v3);
+    h = xmerge(h, v4);
+  } else {
+    h = P5;
+  }
+  h += n;
+  for (; i + 8 <= n; i += 8) h = rotl(h ^ xround(0, ld64(p + i)), 27) * P1 + P4;
+  if (i + 4 <= n) {
+    const uint64_t w = uint64_t(p[i]) | uint64_t(p[i + 1]) << 8 | uint64_t(p[i + 2]) << 16 | uint64_t(p[i + 3]) << 24;
+    h = rotl(h ^ (w * P1), 23) * P2 + P3;
+    i += 4;
+  }
+  for (; i < n; i++) h = rotl(h ^ (uint64_t(p[i]) * P5), 11) * P1;
+  h ^= h >> 33;
+  h *= P2;
+  h ^= h >> 29;
+  h *= P3;
+  h ^= h >> 32;
+  return h;
+}
+
+__global__ void __launch_bounds__(kTPB) checksum_xxh_kernel(const pbl_phys_batch B, uint32_t* status,
+                                                            uint32_t* computed) {
+  for (uint32_t b = blockIdx.x * kTPB + threadIdx.x; b < B.n_blocks; b += gridDim.x * kTPB) {
+    const uint64_t n = uint64_t(B.block_len[b]) + 1;
+    const gptr<const uint8_t> p = to_glb(B.bytes + B.block_off[b]);
+    const uint32_t v = uint32_t(xxh64(p, n));
+    const gptr<const uint8_t> t = p + n;
+    const uint32_t want = uint32_t(t[0]) | uint32_t(t[1]) << 8 | uint32_t(t[2]) << 16 | uint32_t(t[3]) << 24;
+    status[b] = v == want ? PBL_OK : PBL_CORRUPT_CHECKSUM;
+    if (computed) computed[b] = v;
+  }
+}
+
+// ---- snappy ---------------------------------------------------------------------
+constexpr uint32_t kSnapCap = 32768;  // staged compressed bytes / decoded bytes per block (LDS)
+
+__device__ inline bool uvarint32(gptr<const uint8_t> p, uint64_t n, uint32_t* v, uint32_t* used) {
+  uint64_t x = 0;
+  for (uint32_t i = 0; i < n && i < 10; i++) {
+    x |= uint64_t(p[i] & 0x7f) << (7 * i);
+    if (p[i] < 0x80) {
+      if (x > 0xffffffffull) return false;
+      *v = uint32_t(x);
+      *used = i + 1;
+      return true;
+    }
+  }
+  return false;
+}
+
+__global__ void __launch_bounds__(kTPB) snappy_len_kernel(const pbl_phys_batch B, uint32_t* out_len, uint32_t* status) {
+  for (uint32_t b = blockIdx.x * kTPB + threadIdx.x; b < B.n_blocks; b += gridDim.x * kTPB) {
+    const uint32_t n = B.block_len[b];
+    const gptr<const uint8_t> p = to_glb(B.bytes + B.block_off[b]);
+    const uint32_t ind = p[n];
+    uint32_t st = PBL_OK, len = 0, used = 0;
+    if (ind == PBL_COMPRESSION_NONE) len = n;
+    else if (ind == PBL_COMPRESSION_SNAPPY) st = uvarint32(p, n, &len, &used) ? PBL_OK : PBL_CORRUPT_COMPRESSION;
+    else st = PBL_UNSUPPORTED;
+    out_len[b] = st == PBL_OK ? len : 0u;
+    status[b] = st;
+  }
+}
+
+struct SnapLds {
+  uint8_t src[kSnapCap + 16];
+  uint8_t dst[kSnapCap + 16];
+};
+
+struct LdsBytes {
+  lptr<uint8_t> p;
+  __device__ uint8_t operator[](uint32_t i) const { return p[i]; }
+};
+struct LdsBytesW {
+  lptr<uint8_t> p;
+  __device__ uint8_t get(uint32_t i) const { return p[i]; }
+  __device__ void set(uint32_t i, uint8_t v) const { p[i] = v; }
+};
+struct GlbBytes {
+  gptr<const uint8_t> p;
+  __device__ uint8_t operator[](uint32_t i) const { return p[i]; }
+};
+struct GlbBytesW {
+  gptr<uint8_t> p;
+  __device__ uint8_t get(uint32_t i) const { return p[i]; }
+  __device__ void set(uint32_t i, uint8_t v) const { p[i] = v; }
+};
+
+// Decode one snappy block.  Lane 0 reads element headers; the wave copies.
+// Returns the decoded length, or ~0u when the input is corrupt.
+// (lane, step): the wave's lanes (lane_id(), 64) or one lane alone (0, 1).
+template <class Src, class Dst>
+__device__ inline uint32_t snappy_wave(Src src, uint32_t n, Dst dst, uint32_t cap, uint32_t lane, uint32_t step) {
+  uint32_t dlen = 0, s = 0;
+  bool ok = true;
+  {  // uvarint decoded length
+    uint64_t x = 0;
+    bool done = false;
+    for (uint32_t i = 0; i < n && i < 10 && !done; i++) {
+      x |= uint64_t(src[i] & 0x7f) << (7 * i);
+      if (src[i] < 0x80) {
+        done = true;
+        s = i + 1;
+      }
+    }
+    ok = done && x <= cap;
+    dlen = uint32_t(x);
+  }
+  uint32_t d = 0;
+  while (ok && s < n) {
+    // element header (every lane reads the same bytes: uniform control flow)
+    const uint32_t t = src[s];
+    uint32_t kind = t & 3, len = 0, off = 0, lit = 0;
+    if (kind == 0) {
+      uint32_t x = t >> 2;
+      if (x < 60) {
+        s += 1;
+      } else {
+        const uint32_t nb = x - 59;
+        if (s + 1 + nb > n) { ok = false; break; }
+        x = 0;
+        for (uint32_t i = 0; i < nb; i++) x |= uint32_t(src[s + 1 + i]) << (8 * i);
+        s += 1 + nb;
+      }
+      len = x + 1;
+      if (len > n - s || len > dlen - d) { ok = false; break; }
+      lit = s;
+      s += len;
+    } else if (kind == 1) {
+      if (s + 2 > n) { ok = false; break; }
+      len = 4 + ((t >> 2) & 7);
+      off = ((t & 0xe0) << 3) | src[s + 1];
+      s += 2;
+    } else if (kind == 2) {
+      if (s + 3 > n) { ok = false; break; }
+      len = 1 + (t >> 2);
+      off = uint32_t(src[s + 1]) | uint32_t(src[s + 2]) << 8;
+      s += 3;
+    } else {
+      if (s + 5 > n) { ok = false; break; }
+      len = 1 + (t >> 2);
+      off = uint32_t(src[s + 1]) | uint32_t(src[s + 2]) << 8 | uint32_t(src[s + 3]) << 16 | uint32_t(src[s + 4]) << 24;
+      s += 5;
+    }
+    if (kind != 0 && (off == 0 || off > d || len > dlen - d)) { ok = false; break; }
+    if (kind == 0) {
+      for (uint32_t i = lane; i < len; i += step) dst.set(d + i, src[lit + i]);
+    } else {
+      for (uint32_t i = lane; i < len; i += step) dst.set(d + i, dst.get(d - off + (i % off)));
+    }
+    wave_sync();
+    d += len;
+  }
+  return ok && d == dlen ? d : ~0u;
+}
+
+__global__ void __launch_bounds__(kWave) snappy_kernel(const pbl_phys_batch B, uint8_t* out, const uint64_t* out_off,
+                                                       const uint32_t* out_cap, uint32_t* out_len, uint32_t* status) {
+  __shared__ SnapLds S;
+  const uint32_t lane = lane_id();
+  for (uint32_t b = blockIdx.x; b < B.n_blocks; b += gridDim.x) {
+    const uint32_t n = B.block_len[b];
+    const gptr<const uint8_t> src = to_glb(B.bytes + B.block_off[b]);
+    const uint32_t ind = src[n];
+    gptr<uint8_t> dst = to_glb(out + out_off[b]);
+    const uint32_t cap = out_cap[b];
+    uint32_t st = PBL_OK, len = 0;
+    if (ind == PBL_COMPRESSION_NONE) {
+      if (n > cap) st = PBL_OVERFLOW;
+      else
+        for (uint32_t i = lane; i < n; i += kWave) dst[i] = src[i];
+      len = n;
+    } else if (ind == PBL_COMPRESSION_SNAPPY) {
+      uint32_t dl = 0, used = 0;
+      if (!uvarint32(src, n, &dl, &used)) st = PBL_CORRUPT_COMPRESSION;
+      else if (dl > cap) st = PBL_OVERFLOW;
+      else if (n <= kSnapCap && dl <= kSnapCap) {
+        // stage the compressed bytes, decode LDS -> LDS, write the output out
+        for (uint32_t i = lane; i < n; i += kWave) S.src[i] = src[i];
+        wave_sync();
+        len = snappy_wave(LdsBytes{to_lds_ptr(S.src)}, n, LdsBytesW{to_lds_ptr(S.dst)}, dl, lane, kWave);
+        wave_sync();
+        if (len == ~0u) st = PBL_CORRUPT_COMPRESSION;
+        else
+          for (uint32_t i = lane; i < len; i += kWave) dst[i] = S.dst[i];
+      } else {
+        // large blocks: global -> global, each element's bytes fenced before the next reads them
+        len = ~0u;
+        if (lane == 0) {
+          // one lane: program order makes every earlier output byte visible to its own loads
+          len = snappy_wave(GlbBytes{src}, n, GlbBytesW{dst}, dl, 0, 1);
+        }
+        len = __shfl(len, 0, kWave);
+        if (len == ~0u) st = PBL_CORRUPT_COMPRESSION;
+      }
+    } else {
+      st = PBL_UNSUPPORTED;
+    }
+    if (lane == 0) {
+      out_len[b] = st == PBL_OK ? len : 0u;
+      status[b] = st;
+    }
+    wave_sync();
+  }
+}
+
+}  // namespace phys
+}  // namespace pbl
+
+extern "C" {
+
+int pbl_verify_checksums(const pbl_phys_batch* batch, uint32_t checksum_type, uint32_t* status, uint32_t* computed,
+                         void* stream) {
+  if (!batch || !status) return PBL_INVALID_ARG;
+  if (batch->n_blocks == 0) return PBL_OK;
+  if (!batch->bytes || !batch->block_off || !batch->block_len) return PBL_INVALID_ARG;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const uint32_t n = batch->n_blocks;
+  if (checksum_type == PBL_CHECKSUM_CRC32C) {
+    const uint32_t wpb = pbl::kTPB / pbl::kWave;
+    const uint32_t grid = uint32_t(std::min<uint64_t>((n + wpb - 1) / wpb, 4096));
+    hipLaunchKernelGGL(pbl::phys::checksum_crc_kernel, dim3(grid), dim3(pbl::kTPB), 0, st, *batch, status, computed);
+  } else if (checksum_type == PBL_CHECKSUM_XXHASH64) {
+    const uint32_t grid = uint32_t(std::min<uint64_t>((n + pbl::kTPB - 1) / pbl::kTPB, 4096));
+    hipLaunchKernelGGL(pbl::phys::checksum_xxh_kernel, dim3(grid), dim3(pbl::kTPB), 0, st, *batch, status, computed);
+  } else {
+    return PBL_UNSUPPORTED;  // ChecksumTypeNone has nothing to validate; ChecksumTypeXXHash is unsupported (block.go:161)
+  }
+  return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
+}
+
+int pbl_decompressed_lengths(const pbl_phys_batch* batch, uint32_t* out_len, uint32_t* status, void* stream) {
+  if (!batch || !out_len || !status) return PBL_INVALID_ARG;
+  if (batch->n_blocks == 0) return PBL_OK;
+  if (!batch->bytes || !batch->block_off || !batch->block_len) return PBL_INVALID_ARG;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const uint32_t grid = uint32_t(std::min<uint64_t>((batch->n_blocks + pbl::kTPB - 1) / pbl::kTPB, 4096));
+  hipLaunchKernelGGL(pbl::phys::snappy_len_kernel, dim3(grid), dim3(pbl::kTPB), 0, st, *batch, out_len, status);
+  return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
+}
+
+int pbl_decompress_blocks(const pbl_phys_batch* batch, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                          uint32_t* out_len, uint32_t* status, void* stream) {
+  if (!batch || !out || !out_off || !out_cap || !out_len || !status) return PBL_INVALID_ARG;
+  if (batch->n_blocks == 0) return PBL_OK;
+  if (!batch->bytes || !batch->block_off || !batch->block_len) return PBL_INVALID_ARG;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const uint32_t grid = std::min<uint32_t>(batch->n_blocks, 2048);
+  hipLaunchKernelGGL(pbl::phys::snappy_kernel, dim3(grid), dim3(pbl::kWave), 0, st, *batch, out, out_off, out_cap,
+                     out_len, status);
+  return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
+}
+
+}  // extern "C"

@@ -55,9 +55,6 @@ def test_every_codec_is_covered():
     assert any("encoding: 2b" in e["dump"] for e in CODECS["prefix_bytes"])
 
 
-EMBED = {"uints": "trailers", "raw_bytes": "values", "bitmap": "obsolete", "prefix_bytes": "keys"}
-
-
 def embedded_blocks():
     """Every non-empty codec column embedded in a DefaultKeySchema data block
     (tests/colutil.py embed_column): uints as the trailers column, raw_bytes

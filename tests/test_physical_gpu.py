@@ -1,0 +1,187 @@
+"""Device checksums and decompression (pebble_amd/csrc/physical.hip) against
+the oracle and the reference's own SSTs: every stored CRC32C of the three test
+files verifies on the device, corrupted blocks are caught, snappy blocks
+decompress on the device and decode to exactly h.txt's KVs, XXH64 and snappy
+agree with the oracle on random inputs (single-wave LDS path and the >32 KiB
+global path), zstd reports PBL_UNSUPPORTED, corrupt snappy is rejected."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+from pebble_amd import _native as N
+from pebble_amd.batch import decode
+from pebble_amd.physical import PhysBatch, decompress, verify_checksums
+from pebble_amd.rowblk import kvs_of_block
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _fixtures():
+    import json
+    with open(os.path.join(GOLDEN, "physical.json")) as f:
+        phys = json.load(f)
+    blob = np.fromfile(os.path.join(GOLDEN, "physical_blocks.bin"), np.uint8)
+    return phys, blob
+
+
+PHYS, BLOB = _fixtures()
+
+
+def file_batch(name, blob=BLOB):
+    bl = PHYS[name]["blocks"]
+    return PhysBatch.from_host(blob, [b["blob_off"] for b in bl], [b["length"] for b in bl])
+
+
+def pack_phys(blocks, checksum, rng=None, indicator=0):
+    """[block][indicator][checksum LE32] at ragged offsets."""
+    rng = rng or random.Random(0)
+    buf, off, lens, pos = bytearray(), [], [], 0
+    for bk in blocks:
+        pos += rng.randrange(0, 8)
+        buf += bytes(pos - len(buf))
+        ind = indicator if isinstance(indicator, int) else indicator(bk)
+        body = bytes(bk) + bytes([ind])
+        off.append(pos)
+        lens.append(len(bk))
+        buf += body + int(checksum(body)).to_bytes(4, "little")
+        pos = len(buf)
+    return np.frombuffer(bytes(buf), np.uint8), off, lens
+
+
+def test_stored_crc32c_checksums_verify():
+    for name in PHYS:
+        st, comp = verify_checksums(file_batch(name), N.PBL_CHECKSUM_CRC32C)
+        assert list(st) == [0] * len(st), name
+        assert list(comp) == [b["checksum"] for b in PHYS[name]["blocks"]], name
+
+
+def test_corrupted_blocks_caught():
+    blob = BLOB.copy()
+    bl = PHYS["hamlet_snappy"]["blocks"] + PHYS["h_zstd"]["blocks"]
+    rng = random.Random(3)
+    bad = set()
+    for i, b in enumerate(bl):
+        if i % 3 == 0:
+            pos = rng.choice([0, b["length"] - 1, b["length"], rng.randrange(b["length"])])  # incl. the indicator
+            blob[b["blob_off"] + pos] ^= 1 << rng.randrange(8)
+            bad.add(i)
+    pb = PhysBatch.from_host(blob, [b["blob_off"] for b in bl], [b["length"] for b in bl])
+    st, _ = verify_checksums(pb, N.PBL_CHECKSUM_CRC32C)
+    assert [i for i, s in enumerate(st) if s == N.PBL_CORRUPT_CHECKSUM] == sorted(bad)
+    assert all(s in (0, N.PBL_CORRUPT_CHECKSUM) for s in st)
+
+
+@pytest.mark.parametrize("kind", ["crc32c", "xxhash64"])
+def test_random_blocks_checksums(kind):
+    rng = random.Random(11)
+    sizes = [0, 1, 2, 3, 4, 5, 7, 31, 32, 33, 63, 64, 255, 256, 257, 4095, 4096, 65536, 200_001]
+    sizes += [rng.randrange(0, 40_000) for _ in range(300)]
+    blocks = [rng.randbytes(n) for n in sizes]
+    fn = (lambda b: oracle.block_checksum(1, b)) if kind == "crc32c" else oracle.xxhash64_checksum
+    ct = N.PBL_CHECKSUM_CRC32C if kind == "crc32c" else N.PBL_CHECKSUM_XXHASH64
+    buf, off, lens = pack_phys(blocks, fn, rng)
+    st, comp = verify_checksums(PhysBatch.from_host(buf, off, lens), ct)
+    assert list(st) == [0] * len(blocks)
+    for i in range(0, len(blocks), 7):  # a corrupted copy of every 7th block
+        b = bytearray(buf[off[i]: off[i] + lens[i] + 5])
+        b[rng.randrange(len(b) - 4)] ^= 0x80
+        pb = PhysBatch.from_host(np.frombuffer(bytes(b), np.uint8), [0], [lens[i]])
+        s, c = verify_checksums(pb, ct)
+        assert s[0] == N.PBL_CORRUPT_CHECKSUM and c[0] == fn(bytes(b[: lens[i] + 1]))
+
+
+def test_unsupported_checksum_types():
+    pb = file_batch("h_no_compression")
+    for ct in (N.PBL_CHECKSUM_NONE, N.PBL_CHECKSUM_XXHASH, 9):
+        with pytest.raises(Exception, match="UNSUPPORTED"):
+            verify_checksums(pb, ct)
+
+
+def hamlet_kvs(batch):
+    r = decode(batch).to_host()
+    assert r["status_mask"] == 0
+    kvs = []
+    for b in range(batch.n_blocks):
+        kvs += kvs_of_block(r, b)
+    return [(kv.user_key.decode(), kv.value.decode()) for kv in kvs]
+
+
+@pytest.mark.parametrize("name", ["hamlet_snappy", "h_no_compression"])
+def test_decompress_then_decode_is_hamlet(name, golden):
+    bb, st = decompress(file_batch(name))
+    assert list(st) == [0] * bb.n_blocks
+    assert list(bb.block_len.cpu().numpy()) == [b["decompressed_len"] for b in PHYS[name]["blocks"]]
+    assert hamlet_kvs(bb) == [tuple(x) for x in golden["hamlet_kvs"]]
+
+
+def test_zstd_unsupported():
+    bb, st = decompress(file_batch("h_zstd"))
+    assert list(st) == [N.PBL_UNSUPPORTED] * len(st)
+    assert list(bb.block_len.cpu().numpy()) == [0] * len(st)
+
+
+def snappy(b: bytes) -> bytes:
+    import pyarrow as pa
+    return pa.Codec("snappy").compress(b, asbytes=True)
+
+
+def compressible(rng, n):
+    words = [rng.randbytes(rng.randrange(1, 12)) for _ in range(64)]
+    out = bytearray()
+    while len(out) < n:
+        out += rng.choice(words) if rng.random() < 0.8 else rng.randbytes(rng.randrange(1, 70))
+    return bytes(out[:n])
+
+
+def test_snappy_random_blocks_lds_and_global_paths():
+    rng = random.Random(5)
+    sizes = [0, 1, 2, 5, 64, 65, 1000, 32767, 32768, 32769, 40_000, 131_072, 300_000]
+    sizes += [rng.randrange(0, 33_000) for _ in range(200)]
+    raw = [compressible(rng, n) if i % 4 else rng.randbytes(n) for i, n in enumerate(sizes)]
+    # runs: long overlapping copies (offset 1..8)
+    raw += [bytes([i % 251]) * 5000 + bytes(range(7)) * 3000 for i in range(4)]
+    comp = [snappy(b) for b in raw]
+    ind = {c: 1 for c in comp}
+    blocks = comp + raw[:20]  # the uncompressed copies (indicator 0)
+    buf, off, lens = pack_phys(blocks, lambda b: 0, rng, indicator=lambda b: 1 if b in ind else 0)
+    bb, st = decompress(PhysBatch.from_host(buf, off, lens))
+    assert list(st) == [0] * len(blocks)
+    out = bb.blocks.cpu().numpy()
+    bo = bb.block_off.cpu().numpy()
+    bl = bb.block_len.cpu().numpy()
+    for i, want in enumerate(raw + raw[:20]):
+        assert bl[i] == len(want), i
+        assert bytes(out[bo[i]: bo[i] + bl[i]]) == want, i
+    for i, c in enumerate(comp[:40]):
+        assert oracle.snappy_decode(c) == raw[i]
+
+
+def test_snappy_corrupt_matches_oracle():
+    rng = random.Random(9)
+    good = [snappy(compressible(rng, rng.randrange(1, 50_000))) for _ in range(40)]
+    blocks = []
+    for g in good:
+        b = bytearray(g)
+        m = rng.randrange(4)
+        if m == 0:
+            b = b[: rng.randrange(1, len(b))]            # truncated
+        elif m == 1:
+            b[rng.randrange(3, len(b))] = rng.randrange(256)  # one byte changed (past the length)
+        elif m == 2:
+            b = bytearray(b"\xff" * 11)                     # unterminated length varint
+        else:
+            b = bytearray(b"\x10\x05\x00")                  # copy before any output
+        blocks.append(bytes(b))
+    buf, off, lens = pack_phys(blocks, lambda b: 0, rng, indicator=1)
+    bb, st = decompress(PhysBatch.from_host(buf, off, lens))
+    out, bo, bl = bb.blocks.cpu().numpy(), bb.block_off.cpu().numpy(), bb.block_len.cpu().numpy()
+    for i, b in enumerate(blocks):
+        want = oracle.snappy_decode(b)
+        if want is None:
+            assert st[i] in (N.PBL_CORRUPT_COMPRESSION,), (i, st[i])
+        else:
+            assert st[i] == 0 and bytes(out[bo[i]: bo[i] + bl[i]]) == want, i
