@@ -233,7 +233,11 @@ __device__ __forceinline__ void col_emit_rows(CLds& L, const Slot& E, const Args
 
   // per-row arrays
   const UCol& vo = d.v_off;
+#ifdef PBL_EXP_COL_NOROW  // traffic attribution only (scripts/col_traffic.sh): per-row arrays skipped
+  for (uint32_t r = t; r <= 0u; r += kTPB) {
+#else
   for (uint32_t r = t; r <= rows; r += kTPB) {
+#endif
     const uint32_t v = vo.w ? uint32_t(S.le(vo.at + r * vo.w, vo.w)) : 0;
     val_off[kvb + b + r] = v - d.v_lo;
     if (r < rows) {
@@ -258,6 +262,9 @@ __device__ __forceinline__ void col_emit_rows(CLds& L, const Slot& E, const Args
   // aligned 16-B granules (keys past the buffer go straight to global memory)
   lds_u8 kb8 = (lds_u8)to_lds(L.key4);
   uint32_t cbase = 0;
+#ifdef PBL_EXP_COL_NOKEY
+  prebuilt = false;
+#endif
   if (prebuilt) {
     // single chunk, built in LDS while wave 0 resolved the look-back
     if (uint32_t(t) < rows) key_off[kvb + b + t] = ex0;
@@ -267,7 +274,11 @@ __device__ __forceinline__ void col_emit_rows(CLds& L, const Slot& E, const Args
       store16(O.key_bytes, ga, lo, hi, lds_bytes16(W, uint32_t(kKeyPad + ga - lo)));
     cbase = tot0;
   }
+#ifdef PBL_EXP_COL_NOKEY  // traffic attribution only: key bytes skipped
+  for (uint32_t c = 0; c < 0u; c++) {
+#else
   for (uint32_t c = 0; c < (prebuilt ? 0u : nch); c++) {
+#endif
     const uint32_t r = c * kChunk + t;
     RowParts p;
     p.klen = 0;
@@ -291,29 +302,50 @@ __device__ __forceinline__ void col_emit_rows(CLds& L, const Slot& E, const Args
   if (t == 0) key_off[kvb + b + rows] = cbase;
   CSTAMP(A, b, 6);
 
-  // value bytes: one contiguous range, global -> global; four output granules
-  // per thread per step so their source loads are in flight together
+  // value bytes: one contiguous range.  Source granules inside the staged head
+  // or tail come from LDS (the values column usually starts inside the 12 KiB
+  // head: reading those bytes from global again cost ~25 % extra fetch); the
+  // rest global -> global, four output granules per thread per step so their
+  // source loads are in flight together
   {
     const uint64_t src_lo = E.boff + d.v_data + d.v_lo;
+    const int64_t rel_lo = int64_t(d.v_data + d.v_lo);  // block-relative
     const uint64_t n = d.v_hi - d.v_lo;
     const uint64_t lo = vbb, hi = vbb + n;
     const gptr<const uint8_t> G = to_glb(A.in.blocks);
     const int64_t s_end = int64_t(src_lo + n);
+    const lds_cu32 HW = (lds_cu32)to_lds(E.head4), TW = (lds_cu32)to_lds(E.tail4);
+    const int64_t nhead = E.nhead, tail_lo = E.tail_lo, blen = E.blen, shift = E.shift;
     constexpr int U = 4;
+#ifdef PBL_EXP_COL_NOVAL  // traffic attribution only: value bytes skipped
+    for (uint64_t g0 = hi; g0 < hi; g0 += 16ull * kTPB * U) {
+#else
     for (uint64_t g0 = (lo & ~uint64_t(15)) + 16ull * t; g0 < hi; g0 += 16ull * kTPB * U) {
+#endif
       u32x4 x[U], y[U];
       uint32_t sh[U];
 #pragma unroll
       for (int u = 0; u < U; u++) {
         const uint64_t ga = g0 + 16ull * kTPB * u;
+        const int64_t j = rel_lo + int64_t(ga) - int64_t(lo);  // block offset of the granule's first byte
         const int64_t sx = int64_t(src_lo) + int64_t(ga) - int64_t(lo);
         const int64_t sa = sx & ~int64_t(15);
         sh[u] = uint32_t(sx - sa);
         const bool live = ga < hi;
         x[u] = u32x4{0, 0, 0, 0};
         y[u] = u32x4{0, 0, 0, 0};
-        if (live && sa + 16 > int64_t(src_lo) && sa < s_end) x[u] = *(gptr<const u32x4>)(G + sa);
-        if (live && sh[u] && sa + 32 > int64_t(src_lo) && sa + 16 < s_end) y[u] = *(gptr<const u32x4>)(G + sa + 16);
+        if (live && j >= 0 && j + 16 <= nhead) {
+          const uint4 w = lds_bytes16(HW, uint32_t(shift + j));
+          x[u] = u32x4{w.x, w.y, w.z, w.w};
+          sh[u] = 0;
+        } else if (live && j >= tail_lo && j + 16 <= blen) {
+          const uint4 w = lds_bytes16(TW, uint32_t(shift + j - tail_lo));
+          x[u] = u32x4{w.x, w.y, w.z, w.w};
+          sh[u] = 0;
+        } else {
+          if (live && sa + 16 > int64_t(src_lo) && sa < s_end) x[u] = *(gptr<const u32x4>)(G + sa);
+          if (live && sh[u] && sa + 32 > int64_t(src_lo) && sa + 16 < s_end) y[u] = *(gptr<const u32x4>)(G + sa + 16);
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; u++) {

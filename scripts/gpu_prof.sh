@@ -1,13 +1,13 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/prof
+D=${PROF_OUT:-gpurun_out/prof}; mkdir -p $D
 R="rocprofv3 --output-format csv"
 P="python3 scripts/prof_decode.py 65536 5 ${PROF_WORKLOAD:-row}"
-timeout -k 10 300 rocprofv3 -L > gpurun_out/prof/counters_list.txt 2>&1; \
-timeout -k 10 300 $R --kernel-trace --stats -d gpurun_out/prof/trace -o trace -- $P > gpurun_out/prof/trace.log 2>&1 && \
-timeout -k 10 300 $R --pmc FETCH_SIZE -d gpurun_out/prof/fetch -o fetch -- $P > gpurun_out/prof/fetch.log 2>&1 && \
-timeout -k 10 300 $R --pmc WRITE_SIZE -d gpurun_out/prof/write -o write -- $P > gpurun_out/prof/write.log 2>&1 && \
-timeout -k 10 300 $R --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY -d gpurun_out/prof/sq1 -o sq1 -- $P > gpurun_out/prof/sq1.log 2>&1 && \
-timeout -k 10 300 $R --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY -d gpurun_out/prof/sq2 -o sq2 -- $P > gpurun_out/prof/sq2.log 2>&1
+timeout -k 10 300 rocprofv3 -L > $D/counters_list.txt 2>&1; \
+timeout -k 10 300 $R --kernel-trace --stats -d $D/trace -o trace -- $P > $D/trace.log 2>&1 && \
+timeout -k 10 300 $R --pmc FETCH_SIZE -d $D/fetch -o fetch -- $P > $D/fetch.log 2>&1 && \
+timeout -k 10 300 $R --pmc WRITE_SIZE -d $D/write -o write -- $P > $D/write.log 2>&1 && \
+timeout -k 10 300 $R --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY -d $D/sq1 -o sq1 -- $P > $D/sq1.log 2>&1 && \
+timeout -k 10 300 $R --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY -d $D/sq2 -o sq2 -- $P > $D/sq2.log 2>&1
 echo rc=$?
-find gpurun_out/prof -name "*.csv" | head -30
+find $D -name "*.csv" | head -30
