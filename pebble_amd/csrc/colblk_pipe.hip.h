@@ -58,7 +58,10 @@ struct CLds {
   uint32_t scratch[16];
   uint32_t bad, nxt, st;
 };
-static_assert(sizeof(CLds) <= 163840 / 4, "four pipelined colblk workgroups per CU");
+#ifndef PBL_COL_PIPE_WG
+#define PBL_COL_PIPE_WG 3  // workgroups per CU: 3 -> 168 VGPRs per lane (4 -> 128 spilled 160 B/lane to scratch: +0.8 GB of traffic per launch)
+#endif
+static_assert(sizeof(CLds) <= 163840 / PBL_COL_PIPE_WG, "pipelined colblk workgroups per CU");
 
 __device__ __forceinline__ Src slot_src(const Slot& P, const Args& A) {
   return Src{(lds_cu8)to_lds(P.head4) + P.shift, (lds_cu8)to_lds(P.tail4) + P.shift,
@@ -391,7 +394,7 @@ __device__ __forceinline__ void col_emit(CLds& L, const Slot& E, const Args& A, 
 }
 
 // ---- the persistent kernel ----------------------------------------------------------
-__global__ void __launch_bounds__(kTPB, 4) colblk_pipe_kernel(Args A) {
+__global__ void __launch_bounds__(kTPB, PBL_COL_PIPE_WG) colblk_pipe_kernel(Args A) {
   __shared__ CLds L;
   const int t = threadIdx.x;
   const uint32_t nb = A.in.n_blocks;

@@ -1,13 +1,13 @@
 # Build libpebble_amd.so from a git revision into exp/<name>.so (for scripts/ab.sh).
-# Usage: bash scripts/build_variant.sh <rev> <name> [extra hipcc flags]
+# Usage: bash scripts/build_variant.sh <rev|.> <name> [extra hipcc flags]   (. = the working tree)
 set -e
 rev=$1; name=$2; shift 2
 root=$(git rev-parse --show-toplevel)
 wt=$(mktemp -d /tmp/pbl_wt.XXXX)
-git -C "$root" worktree add -q --detach "$wt" "$rev"
+if [ "$rev" = "." ]; then cp -r "$root/pebble_amd" "$root/include" "$wt/"; else git -C "$root" worktree add -q --detach "$wt" "$rev"; fi
 mkdir -p "$root/exp"
 (cd "$wt/pebble_amd/csrc" && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -pthread "$@" \
   rowblk_decode.hip colblk_decode.hip $(ls transforms.hip physical.hip 2>/dev/null) rowblk_writer.cpp colblk_writer.cpp zipf_gen.cpp \
   -o "$root/exp/$name.so")
-git -C "$root" worktree remove --force "$wt"
+if [ "$rev" = "." ]; then rm -rf "$wt"; else git -C "$root" worktree remove --force "$wt"; fi
 echo "$root/exp/$name.so"
