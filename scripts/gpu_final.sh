@@ -5,7 +5,7 @@ echo "== gpu tests" && timeout -k 10 600 python -u -m pytest tests -m gpu -x -q 
 [ $rc -eq 0 ] || { tail -40 gpurun_out/final/pytest_gpu.log; exit $rc; }
 echo "== smoke" && timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/final/smoke.log 2>&1 && cat gpurun_out/final/smoke.log | grep smoke
 B="timeout -k 10 300 python bench.py --steps 10 --warmup 2"
-$B --cpu-baseline-seconds 10 --e2e > gpurun_out/final/bench_row.json 2>gpurun_out/final/bench_row.err && echo row ok && \
+$B --cpu-baseline-seconds 10 > gpurun_out/final/bench_row.json 2>gpurun_out/final/bench_row.err && echo row ok && \
 $B --workload col --cpu-baseline-seconds 5 > gpurun_out/final/bench_col.json 2>/dev/null && echo col ok && \
 $B --workload mixed --no-cpu-baseline > gpurun_out/final/bench_mixed.json 2>/dev/null && echo mixed ok && \
 $B --workload zipf --restart-interval 1 --no-cpu-baseline > gpurun_out/final/bench_zipf_ri1.json 2>/dev/null && \
