@@ -47,7 +47,8 @@ struct Slot {
   uint64_t boff;
   uint64_t agg[kNumComp];
   uint32_t b, blen, nhead, tail_lo, shift, status, mode, tot0;
-  uint32_t fast;  // header parsed and the key columns inside the staged head
+  uint32_t fast;    // header parsed and the key columns inside the staged head
+  uint32_t schema;  // the block's format (PBL_FMT_COL_*)
 };
 
 struct CLds {
@@ -114,8 +115,9 @@ struct ColPf {
 // Slot bookkeeping for block b (thread 0 computes; all threads see it after the
 // caller's barrier).  Blocks whose start is not 8-B aligned are staged with the
 // funnel shift instead (8-B column reads from LDS need 8-B alignment).
-__device__ __forceinline__ void slot_setup(Slot& P, uint32_t b, uint64_t boff, uint32_t blen) {
+__device__ __forceinline__ void slot_setup(Slot& P, uint32_t b, uint64_t boff, uint32_t blen, const Args& A) {
   P.b = b;
+  P.schema = A.in.block_format && b < A.in.n_blocks ? uint32_t(to_glb(A.in.block_format)[b]) : A.in.format;
   P.boff = boff;
   P.blen = blen;
   geometry(blen, &P.nhead, &P.tail_lo);
@@ -394,18 +396,15 @@ __device__ __forceinline__ void col_emit(CLds& L, const Slot& E, const Args& A, 
 }
 
 // ---- the persistent kernel ----------------------------------------------------------
-__global__ void __launch_bounds__(kTPB, PBL_COL_PIPE_WG) colblk_pipe_kernel(Args A) {
-  __shared__ CLds L;
+__device__ __forceinline__ void col_pipe_body(CLds& L, const Args& A, const Queue& Q) {
   const int t = threadIdx.x;
   const uint32_t nb = A.in.n_blocks;
-  const uint32_t schema = A.in.format;
-  uint32_t* tick = reinterpret_cast<uint32_t*>(A.out.workspace);
   if (t == 0) {
-    const uint32_t t0 = g_atomic_add(tick, 1u);
+    const uint32_t t0 = Q.take();
     L.s[1].mode = kNone;
     L.s[1].b = nb;
     if (t0 < nb) {
-      slot_setup(L.s[0], t0, to_glb(A.in.block_off)[t0], to_glb(A.in.block_len)[t0]);
+      slot_setup(L.s[0], t0, to_glb(A.in.block_off)[t0], to_glb(A.in.block_len)[t0], A);
     } else {
       L.s[0].b = nb;
       L.s[0].mode = kNone;
@@ -429,9 +428,9 @@ __global__ void __launch_bounds__(kTPB, PBL_COL_PIPE_WG) colblk_pipe_kernel(Args
     if (cb >= nb && E.mode == kNone) break;
     // the next ticket is taken now (its latency overlaps the parse): tickets are
     // held for one iteration only, which keeps the look-back distance short
-    if (t == 0) L.nxt = cb < nb ? g_atomic_add(tick, 1u) : nb;
+    if (t == 0) L.nxt = cb < nb ? Q.take() : nb;
     ColPf pf;
-    col_parse(L, P, E, A, schema);  // (wave 1 first resolves E's prefix)
+    col_parse(L, P, E, A, P.schema);  // (wave 1 first resolves E's prefix)
     __syncthreads();
     const uint32_t nx = L.nxt;
     uint64_t nx_off = 0;
@@ -442,15 +441,22 @@ __global__ void __launch_bounds__(kTPB, PBL_COL_PIPE_WG) colblk_pipe_kernel(Args
     }
     const bool pf_on = nx < nb && (nx_off & 7) == 0;
     if (pf_on) pf.load(A.in.blocks, nx_off, nx_len);  // lands during the emit
-    if (E.mode != kNone) col_emit(L, E, A, schema);
+    if (E.mode != kNone) col_emit(L, E, A, E.schema);
     __syncthreads();
-    if (t == 0) slot_setup(E, nx < nb ? nx : nb, nx_off, nx_len);
+    if (t == 0) slot_setup(E, nx < nb ? nx : nb, nx_off, nx_len, A);
     if (pf_on) pf.store(E, nx_off, nx_len);
     __syncthreads();
     if (nx < nb && !pf_on) slot_stage_funnel(E, A);
     __syncthreads();
   }
 }
+
+#ifndef PBL_COL_PIPE_BODY_ONLY  // (rowblk_decode.hip uses the body in the mixed pipeline)
+__global__ void __launch_bounds__(kTPB, PBL_COL_PIPE_WG) colblk_pipe_kernel(Args A) {
+  __shared__ CLds L;
+  col_pipe_body(L, A, Queue{reinterpret_cast<uint32_t*>(A.out.workspace), nullptr, A.in.n_blocks, A.in.n_blocks});
+}
+#endif
 
 }  // namespace cpipe
 }  // namespace col

@@ -36,6 +36,9 @@ constexpr int kLbWin = 8;   // look-back windows (of 64 predecessors) loaded per
 // the walk without a second fetch.
 constexpr uint64_t kWsHeader = 256;
 constexpr int kWsBigCount = 1;  // header u32 [1]: blocks past the LDS stage (row pipeline)
+constexpr int kWsColTick = 2;   // header u32 [2]: the colblk queue's ticket counter (mixed batches)
+constexpr int kWsRowCount = 3;  // header u32 [3]: row-format blocks in a mixed batch
+constexpr uint32_t kSplitChunk = 4096;  // blocks per chunk of the mixed-batch split
 constexpr int kStShift = 61;
 constexpr uint64_t kStAgg = 1ull << kStShift;
 constexpr uint64_t kStWide = 2ull << kStShift;
@@ -57,9 +60,16 @@ constexpr uint64_t kStampWords = 16;  // diagnostic build: per-block phase stamp
 #else
 constexpr uint64_t kStampWords = 0;
 #endif
-__host__ __device__ inline uint64_t ws_alloc_bytes(uint32_t n_blocks) {
+// Past the look-back state (and the diagnostic stamps): a mixed batch's block
+// ids split by format (row ids ascending, then colblk ids ascending) and the
+// split's per-chunk row counts.  Not cleared per launch.
+__host__ __device__ inline uint64_t ws_ids_offset(uint32_t n_blocks) {
   return ws_bytes(n_blocks) + kStampWords * 8ull * n_blocks;
 }
+__host__ __device__ inline uint64_t ws_alloc_bytes(uint32_t n_blocks) {
+  return ws_ids_offset(n_blocks) + 4ull * n_blocks + 4ull * (n_blocks / kSplitChunk + 1) + 8;
+}
+
 
 // Address-space-typed pointers.  A generic pointer compiles to FLAT
 // instructions, which count against BOTH vmcnt and lgkmcnt: an LDS read issued
@@ -85,6 +95,21 @@ __device__ inline uint32_t g_atomic_add(uint32_t* p, uint32_t v) {
 __device__ inline uint32_t g_atomic_or(uint32_t* p, uint32_t v) {
   return __hip_atomic_fetch_or(to_glb(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+// A persistent kernel's source of blocks: tickets from `tick`, mapped through
+// `ids` (a mixed batch's per-format list) or used as block ids directly.
+// take() returns a block id, or n_blocks when the queue is drained.
+struct Queue {
+  uint32_t* tick;
+  const uint32_t* ids;  // nullptr: ticket == block id
+  uint32_t n;           // tickets in this queue
+  uint32_t n_blocks;    // the sentinel
+  __device__ uint32_t take() const {
+    const uint32_t t = g_atomic_add(tick, 1u);
+    if (t >= n) return n_blocks;
+    return ids ? to_glb(ids)[t] : t;
+  }
+};
 
 __device__ inline uint64_t ld_agent(const uint64_t* p) {
   return __hip_atomic_load(to_glb(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -818,6 +818,121 @@ __global__ void __launch_bounds__(kTPB) mixed_decode_kernel(Args A) {
   else col::col_block(s.col, A, b, fmt);
 }
 
+}  // namespace row
+}  // namespace pbl
+
+#define PBL_COL_PIPE_BODY_ONLY
+#include "colblk_pipe.hip.h"
+
+namespace pbl {
+namespace row {
+
+// ---- mixed row + colblk batches, pipelined (config 4) -------------------------------
+// The batch's block ids are split by format into two ascending lists
+// (mixed_split_*); one persistent launch then runs the row pipeline body
+// (rowblk_pipe.hip.h) in its first workgroups and the colblk pipeline body
+// (colblk_pipe.hip.h) in the rest, each taking tickets from its own list.
+// Both publish into ONE look-back state indexed by the block id, so every
+// block's exclusive prefix is over the batch order, as in the single-format
+// kernels.  Deadlock-free because every workgroup of the launch is resident
+// (persistent grid) and each list is ticketed in ascending id order: the
+// smallest unfinished block has been ticketed and all its predecessors have
+// published.  The workgroup split follows the lists' lengths weighted by the
+// per-block cost of each pipeline (kMixColCost, colblk relative to row, x1000).
+#ifndef PBL_MIX_COL_COST
+#define PBL_MIX_COL_COST 1300
+#endif
+#ifndef PBL_MIX_ROW_PRIO
+#define PBL_MIX_ROW_PRIO 0  // 1: the row parse wave at s_setprio 2 as in rowblk_pipe_kernel (measured 858 vs 870 GiB/s without)
+#endif
+
+__global__ void __launch_bounds__(kTPB) mixed_split_count_kernel(Args A, uint32_t* counts) {
+  const uint32_t nb = A.in.n_blocks;
+  const uint32_t c0 = blockIdx.x * kSplitChunk;
+  uint32_t k = 0;
+  for (uint32_t i = c0 + threadIdx.x; i < nb && i < c0 + kSplitChunk; i += kTPB)
+    k += to_glb(A.in.block_format)[i] == PBL_FMT_ROW;
+  __shared__ uint32_t red[kTPB / kWave];
+  k = wave_sum(k);
+  if (lane_id() == 0) red[wave_id()] = k;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (int w = 0; w < kTPB / kWave; w++) s += red[w];
+    counts[blockIdx.x] = s;
+  }
+}
+
+__global__ void __launch_bounds__(kTPB) mixed_split_scatter_kernel(Args A, const uint32_t* counts, uint32_t n_chunks,
+                                                                   uint32_t* ids) {
+  const uint32_t nb = A.in.n_blocks;
+  const uint32_t c = blockIdx.x;
+  __shared__ uint32_t sc[kTPB];
+  __shared__ uint32_t base_row, base_col;
+  if (threadIdx.x == 0) {
+    uint32_t before = 0, total = 0;
+    for (uint32_t i = 0; i < n_chunks; i++) {
+      const uint32_t x = to_glb(counts)[i];
+      if (i < c) before += x;
+      total += x;
+    }
+    base_row = before;
+    base_col = total + (c * kSplitChunk - before);  // col ids follow all row ids
+    if (c == 0) to_glb(reinterpret_cast<uint32_t*>(A.out.workspace))[kWsRowCount] = total;
+  }
+  __syncthreads();
+  // in-order compaction of the chunk, kTPB ids at a time
+  for (uint32_t i0 = c * kSplitChunk; i0 < nb && i0 < (c + 1) * kSplitChunk; i0 += kTPB) {
+    const uint32_t i = i0 + threadIdx.x;
+    const bool live = i < nb && i < (c + 1) * kSplitChunk;
+    const uint32_t isrow = live && to_glb(A.in.block_format)[i] == PBL_FMT_ROW;
+    sc[threadIdx.x] = isrow;
+    __syncthreads();
+    // inclusive scan (Hillis-Steele over kTPB entries)
+    for (uint32_t d = 1; d < kTPB; d <<= 1) {
+      const uint32_t v = threadIdx.x >= d ? sc[threadIdx.x - d] : 0u;
+      __syncthreads();
+      sc[threadIdx.x] += v;
+      __syncthreads();
+    }
+    const uint32_t incl = sc[threadIdx.x], nrow = sc[kTPB - 1];
+    const uint32_t nlive = (nb - i0 < kTPB ? nb - i0 : kTPB);
+    if (live) {
+      if (isrow) to_glb(ids)[base_row + incl - 1] = i;
+      else to_glb(ids)[base_col + (threadIdx.x - (incl - isrow))] = i;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      base_row += nrow;
+      base_col += nlive - nrow;
+    }
+    __syncthreads();
+  }
+}
+
+union MixedPipeLds {
+  pipe::PLds row;
+  col::cpipe::CLds col;
+};
+
+__global__ void __launch_bounds__(pipe::kPTPB) __attribute__((amdgpu_waves_per_eu(PBL_PIPE_WAVES / 2, PBL_PIPE_WAVES / 2)))
+mixed_pipe_kernel(Args A, const uint32_t* ids) {
+  __shared__ MixedPipeLds L;
+  const uint32_t nb = A.in.n_blocks;
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(A.out.workspace);
+  const uint32_t n_row = __hip_atomic_load(to_glb(hdr) + kWsRowCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t n_col = nb - n_row;
+  const uint64_t G = gridDim.x;
+  uint64_t g_row = n_col == 0 ? G : n_row == 0 ? 0
+                 : (G * 1000ull * n_row + (1000ull * n_row + uint64_t(PBL_MIX_COL_COST) * n_col) / 2) /
+                       (1000ull * n_row + uint64_t(PBL_MIX_COL_COST) * n_col);
+  if (n_row && n_col) g_row = g_row < 1 ? 1 : g_row > G - 1 ? G - 1 : g_row;
+  if (blockIdx.x < g_row)
+    pipe::row_pipe_body(L.row, A, Queue{hdr, ids, n_row, nb}, PBL_MIX_ROW_PRIO);
+  else
+    col::cpipe::col_pipe_body(L.col, A, Queue{hdr + kWsColTick, ids + n_row, n_col, nb});
+}
+
 // Size pass epilogue: a block that decoded reports PBL_OK, not the forced
 // overflow of the pass.
 __global__ void size_fixup_kernel(uint32_t* blk_status, pbl_totals* totals, uint32_t n) {
@@ -894,6 +1009,38 @@ uint64_t persistent_grid(hipStream_t st, PersistentKernel k, const void* fn, uin
 
 }  // namespace pbl
 
+namespace {
+// Mixed batches: PBL_KERNEL_SINGLE keeps the one-block-per-workgroup kernel
+// (A/B); the default splits the ids by format and runs the mixed pipeline,
+// with the big row blocks' size / value passes around it.
+int launch_mixed(const pbl_block_batch* batch, const pbl::Args& a, hipStream_t st, bool single, bool values) {
+  if (single) {
+    hipLaunchKernelGGL(pbl::row::mixed_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
+    return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
+  }
+  const uint32_t nb = batch->n_blocks;
+  uint8_t* ws = reinterpret_cast<uint8_t*>(a.out.workspace);
+  uint32_t* ids = reinterpret_cast<uint32_t*>(ws + pbl::ws_ids_offset(nb));
+  uint32_t* counts = ids + nb;
+  const uint32_t nch = (nb + pbl::kSplitChunk - 1) / pbl::kSplitChunk;
+  hipLaunchKernelGGL(pbl::row::mixed_split_count_kernel, dim3(nch), dim3(pbl::kTPB), 0, st, a, counts);
+  hipLaunchKernelGGL(pbl::row::mixed_split_scatter_kernel, dim3(nch), dim3(pbl::kTPB), 0, st, a,
+                     static_cast<const uint32_t*>(counts), nch, ids);
+  int cus = 0;
+  const uint64_t grid = pbl::persistent_grid(st, pbl::kKMixedPipe,
+                                             reinterpret_cast<const void*>(pbl::row::mixed_pipe_kernel), nb, &cus,
+                                             pbl::row::pipe::kPTPB);
+  if (!grid) return PBL_DEVICE_ERROR;
+  const uint32_t small = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4));
+  hipLaunchKernelGGL(pbl::row::pipe::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+  hipLaunchKernelGGL(pbl::row::mixed_pipe_kernel, dim3(uint32_t(grid)), dim3(pbl::row::pipe::kPTPB), 0, st, a,
+                     static_cast<const uint32_t*>(ids));
+  if (values)
+    hipLaunchKernelGGL(pbl::row::pipe::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+  return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
+}
+}  // namespace
+
 extern "C" {
 
 int pbl_abi_version(void) { return PBL_ABI_VERSION; }
@@ -919,9 +1066,10 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
   pbl::Args a;
   a.in = *batch;
   a.out = *out;
-  if (batch->block_format)
-    hipLaunchKernelGGL(pbl::row::mixed_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
-  else {
+  if (batch->block_format) {
+    const int rc = launch_mixed(batch, a, st, batch->flags & PBL_KERNEL_SINGLE, true);
+    if (rc != PBL_OK) return rc;
+  } else {
     // persistent grid: as many workgroups as can be resident (never more than
     // blocks).  PBL_KERNEL_SINGLE selects the one-block-per-workgroup
     // persistent kernel (kept for A/B measurement); the default is the pipeline.
@@ -983,7 +1131,8 @@ int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stre
     // the launch sequence of pbl_decode_batch (whose checks require output
     // pointers), minus the big-block value pass
     if (batch->block_format) {
-      hipLaunchKernelGGL(pbl::row::mixed_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
+      rc = launch_mixed(batch, a, st, batch->flags & PBL_KERNEL_SINGLE, false);
+      if (rc != PBL_OK) return rc;
     } else {
       int cus = 0;
       const uint64_t grid = pbl::persistent_grid(

@@ -497,7 +497,9 @@ __global__ void __launch_bounds__(kWave) big_block_sizes_kernel(Args A) {
   // 64 lengths per wave per round; the big blocks among them one after another
   for (uint64_t base = uint64_t(blockIdx.x) * kWave; base < nb; base += uint64_t(gridDim.x) * kWave) {
    const uint64_t bl = base + lane_id();
-   uint64_t big = __ballot(bl < nb && to_glb(A.in.block_len)[bl] > kMaxFastLen);
+   // (row blocks only: a mixed batch's colblk blocks are the colblk pipeline's)
+   uint64_t big = __ballot(bl < nb && to_glb(A.in.block_len)[bl] > kMaxFastLen &&
+                           (!A.in.block_format || to_glb(A.in.block_format)[bl] == PBL_FMT_ROW));
    while (big) {
     const uint32_t b = uint32_t(base) + uint32_t(__builtin_ctzll(big));
     big &= big - 1;
@@ -539,6 +541,7 @@ __global__ void __launch_bounds__(kWave) big_block_values_kernel(Args A) {
   for (uint64_t base = uint64_t(blockIdx.x) * kWave; base < nb; base += uint64_t(gridDim.x) * kWave) {
     const uint64_t bl = base + lane_id();
     uint64_t big = __ballot(bl < nb && to_glb(A.in.block_len)[bl] > kMaxFastLen &&
+                            (!A.in.block_format || to_glb(A.in.block_format)[bl] == PBL_FMT_ROW) &&
                             to_glb(A.out.blk_status)[bl] == PBL_OK);
     while (big) {
       const uint32_t b = uint32_t(base) + uint32_t(__builtin_ctzll(big));
@@ -958,13 +961,11 @@ struct PfWave {
 // X[(i+1)&1] (free again) and rotates the descriptors; the second barrier
 // publishes them.  Each role executes its own copies of the two barriers, so
 // the prefetch registers stay confined to the parse wave's code.
-__global__ void __launch_bounds__(kPTPB) __attribute__((amdgpu_waves_per_eu(PBL_PIPE_WAVES / 2, PBL_PIPE_WAVES / 2))) rowblk_pipe_kernel(Args A) {
-  __shared__ PLds S;
+__device__ __forceinline__ void row_pipe_body(PLds& S, const Args& A, const Queue& Q, bool prio = true) {
   const int t = threadIdx.x;
   const uint32_t nb = A.in.n_blocks;
-  uint32_t* tick = A.out.workspace ? reinterpret_cast<uint32_t*>(A.out.workspace) : nullptr;
   if (t == 0) {
-    const uint32_t t0 = g_atomic_add(tick, 1u);
+    const uint32_t t0 = Q.take();
     S.m[0].b = t0;
     S.m[0].mode = kModeNone;
     S.m[1].mode = kModeNone;
@@ -972,7 +973,7 @@ __global__ void __launch_bounds__(kPTPB) __attribute__((amdgpu_waves_per_eu(PBL_
     if (t0 < nb) {
       S.m[0].boff = to_glb(A.in.block_off)[t0];
       S.m[0].blen = to_glb(A.in.block_len)[t0];
-      S.nxt = g_atomic_add(tick, 1u);
+      S.nxt = Q.take();
     } else {
       S.nxt = nb;
     }
@@ -989,7 +990,7 @@ __global__ void __launch_bounds__(kPTPB) __attribute__((amdgpu_waves_per_eu(PBL_
   __syncthreads();
   // the parse wave is the pipeline's critical path: it wins VALU arbitration
   // against the emit wave of the other workgroup on its SIMD
-  if (t < kWave) __builtin_amdgcn_s_setprio(2);
+  if (t < kWave && prio) __builtin_amdgcn_s_setprio(2);
   for (uint32_t i = 0;; i++) {
     Meta& cur = S.m[i & 1];
     Meta& prv = S.m[(i + 1) & 1];
@@ -1026,10 +1027,15 @@ __global__ void __launch_bounds__(kPTPB) __attribute__((amdgpu_waves_per_eu(PBL_
       prv.boff = nx_off;
       prv.blen = nx_len;
       prv.mode = kModeNone;
-      S.nxt = nx < nb ? g_atomic_add(tick, 1u) : nb;
+      S.nxt = nx < nb ? Q.take() : nb;
     }
     __syncthreads();
   }
+}
+
+__global__ void __launch_bounds__(kPTPB) __attribute__((amdgpu_waves_per_eu(PBL_PIPE_WAVES / 2, PBL_PIPE_WAVES / 2))) rowblk_pipe_kernel(Args A) {
+  __shared__ PLds S;
+  row_pipe_body(S, A, Queue{reinterpret_cast<uint32_t*>(A.out.workspace), nullptr, A.in.n_blocks, A.in.n_blocks});
 }
 
 }  // namespace pipe

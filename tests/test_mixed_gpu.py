@@ -1,0 +1,103 @@
+"""Mixed row + colblk batches (config 4, block_format[]): the pipelined mixed
+kernel (format split into two ascending id lists, row and colblk pipeline
+bodies in one persistent launch, one look-back over the batch order) and the
+one-block-per-workgroup kernel (PBL_KERNEL_SINGLE) against the oracle,
+bit-exact on every output array."""
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+from colutil import build_block, random_rows
+from pebble_amd import _native as N
+from pebble_amd.colblk import SCHEMA_DEFAULT, gen_col_blocks
+from pebble_amd.rowblk import gen_row_blocks
+from test_rowblk_gpu import assert_same, pack
+
+pytestmark = pytest.mark.gpu
+KERNELS = {"pipe": 0, "single": N.PBL_KERNEL_SINGLE}
+
+
+def gpu(buf, off, lens, bf, flags=0, cap=None, exact=False):
+    from pebble_amd.batch import BlockBatch, decode
+    b = BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, flags, block_format=bf)
+    return decode(b, cap=cap, exact=exact).to_host()
+
+
+def check(blocks, fmts, kernel, align=8, ctx="", **kw):
+    buf, off, lens = pack(blocks, align)
+    bf = np.array(fmts, np.uint8)
+    o = oracle.decode_batch(buf, off, lens, N.PBL_FMT_ROW, bf)
+    g = gpu(buf, off, lens, bf, KERNELS[kernel], **kw)
+    assert_same(g, o, f"{ctx} kernel={kernel}")
+    return g
+
+
+def pool(seed, n_row, n_col, size=8192):
+    rb, ro, rl, _ = gen_row_blocks(seed, n_row, size, 16, 16, 100)
+    cb, co, cl, _ = gen_col_blocks(seed, n_col, size)
+    rows = [bytes(rb[ro[i]:ro[i] + rl[i]]) for i in range(n_row)]
+    cols = [bytes(cb[co[i]:co[i] + cl[i]]) for i in range(n_col)]
+    return rows, cols
+
+
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_mixed_shapes(kernel):
+    rows, cols = pool(1, 40, 40)
+    rng = random.Random(2)
+    dflt = build_block(SCHEMA_DEFAULT, random_rows(rng, SCHEMA_DEFAULT, 150))[0]
+    R, C, D = N.PBL_FMT_ROW, N.PBL_FMT_COL_CRDB1, N.PBL_FMT_COL_DEFAULT
+    cases = {
+        "interleaved": ([x for p in zip(rows, cols) for x in p], [R, C] * 40),
+        "all_row": (rows, [R] * 40),
+        "all_col": (cols, [C] * 40),
+        "one_row": (cols[:20] + rows[:1] + cols[20:], [C] * 20 + [R] + [C] * 20),
+        "one_col": (rows[:30] + cols[:1], [R] * 30 + [C]),
+        "runs": (rows[:10] + cols[:25] + [dflt] + rows[10:], [R] * 10 + [C] * 25 + [D] + [R] * 30),
+    }
+    for name, (blocks, fmts) in cases.items():
+        for align in (8, 1):
+            check(blocks, fmts, kernel, align, name)
+
+
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_mixed_random_across_split_chunks(kernel):
+    """> 4096 blocks: the format split spans several chunks."""
+    rows, cols = pool(3, 64, 64, 4096)
+    rng = random.Random(4)
+    blocks, fmts = [], []
+    for _ in range(9000):
+        if rng.random() < 0.45:
+            blocks.append(rng.choice(rows)); fmts.append(N.PBL_FMT_ROW)
+        else:
+            blocks.append(rng.choice(cols)); fmts.append(N.PBL_FMT_COL_CRDB1)
+    g = check(blocks, fmts, kernel, 8, "random9000")
+    assert g["status_mask"] == 0
+
+
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_mixed_big_and_corrupt_blocks(kernel):
+    """Row blocks past the LDS stage (the big-block passes must skip colblk
+    blocks), colblk blocks past the head stage, corrupt blocks of both kinds."""
+    rows, cols = pool(5, 8, 8)
+    big_row = bytes(gen_row_blocks(6, 1, 131072, 16, 16, 100)[0][:131072])
+    rng = random.Random(7)
+    big_col = build_block(SCHEMA_DEFAULT, random_rows(rng, SCHEMA_DEFAULT, 30, key_len=(1000, 1500), shared=900,
+                                                      val_len=(0, 8)))[0]
+    bad_row = rows[0][:100]
+    bad_col = bytearray(cols[0]); bad_col[5] ^= 0xff
+    blocks = rows[:4] + [big_row] + cols[:4] + [big_col, bad_row, bytes(bad_col)] + rows[4:] + cols[4:] + [big_row]
+    R, C, D = N.PBL_FMT_ROW, N.PBL_FMT_COL_CRDB1, N.PBL_FMT_COL_DEFAULT
+    fmts = [R] * 4 + [R] + [C] * 4 + [D, R, C] + [R] * 4 + [C] * 4 + [R]
+    g = check(blocks, fmts, kernel, 8, "big+corrupt")
+    assert g["n_bad_blocks"] >= 1
+
+
+def test_mixed_overflow_retry_and_size_pass():
+    from pebble_amd.batch import Capacity
+    rows, cols = pool(8, 20, 20)
+    blocks = [x for p in zip(rows, cols) for x in p]
+    fmts = [N.PBL_FMT_ROW, N.PBL_FMT_COL_CRDB1] * 20
+    check(blocks, fmts, "pipe", 8, "overflow", cap=Capacity(kv=10, key=10, val=10, rst=10))
+    check(blocks, fmts, "pipe", 8, "exact", exact=True)
