@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define PBL_ABI_VERSION 3
+#define PBL_ABI_VERSION 4
 
 /* ---- status codes (per block, and OR-ed as bit masks into totals) ---------- */
 enum {
@@ -55,7 +55,9 @@ enum {
   PBL_DEVICE_ERROR = 8,
   PBL_TIMEOUT = 9,               /* in-kernel look-back spin bound hit (never expected) */
   PBL_CORRUPT_CHECKSUM = 10,     /* block.go:177-195 "checksum mismatch"        */
-  PBL_CORRUPT_COMPRESSION = 11   /* snappy.ErrCorrupt -> base.MarkCorruptionError (block.go:550-565) */
+  PBL_CORRUPT_COMPRESSION = 11,  /* snappy.ErrCorrupt -> base.MarkCorruptionError (block.go:550-565) */
+  PBL_CORRUPT_FOOTER = 12,       /* parseFooter's CorruptionErrorf sites (sstable/table.go:328-404) */
+  PBL_CORRUPT_INDEX = 13         /* DecodeHandleWithProperties "invalid block.Handle" (block/block.go:94-104) */
 };
 
 /* ---- block formats ---------------------------------------------------------- */
@@ -254,6 +256,62 @@ int pbl_decompressed_lengths(const pbl_phys_batch* batch, uint32_t* out_len, uin
  */
 int pbl_decompress_blocks(const pbl_phys_batch* batch, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                           uint32_t* out_len, uint32_t* status, void* stream);
+
+/* ---- table footer and index blocks ------------------------ */
+enum { /* TableFormat (sstable/format.go:20-60); the footer's (magic, version) */
+  PBL_TABLE_LEVELDB = 1, PBL_TABLE_ROCKSDBV2 = 2,
+  PBL_TABLE_PEBBLEV1 = 3, PBL_TABLE_PEBBLEV2 = 4, PBL_TABLE_PEBBLEV3 = 5, PBL_TABLE_PEBBLEV4 = 6,
+  PBL_TABLE_PEBBLEV5 = 7, PBL_TABLE_PEBBLEV6 = 8, PBL_TABLE_PEBBLEV7 = 9, PBL_TABLE_PEBBLEV8 = 10
+};
+typedef struct pbl_footer {
+  uint32_t table_format;   /* PBL_TABLE_*                                               */
+  uint32_t checksum_type;  /* PBL_CHECKSUM_* of every block of the table                */
+  uint64_t metaindex_off, metaindex_len;
+  uint64_t index_off, index_len;  /* the (top-level) index block's handle             */
+  uint64_t footer_off, footer_len;
+  uint32_t attributes;     /* Pebblev7+ attribute bitset, else 0                        */
+  uint32_t reserved;
+} pbl_footer;
+/*
+ * parseFooter (sstable/table.go:328-404) on HOST memory: `buf` holds the last
+ * buf_len bytes of a file of file_size bytes (readFooter reads the last
+ * maxFooterLen = 61 bytes).  LevelDB, RocksDBv2 and Pebblev1-v8 footers; the
+ * Pebblev6+ footer checksum (CRC32C Value) is verified.  Returns PBL_OK or
+ * PBL_CORRUPT_FOOTER (bad magic, unsupported version or checksum type, short
+ * footer, checksum mismatch, handles past the end of the file).
+ */
+int pbl_parse_footer(const uint8_t* buf, uint64_t buf_len, uint64_t file_size, pbl_footer* out);
+
+typedef struct pbl_index_out {
+  uint64_t* handle_off;  /* [cap] block.Handle.Offset of each entry, in block order              */
+  uint64_t* handle_len;  /* [cap] block.Handle.Length                                             */
+  uint64_t* props_off;   /* [cap] (nullable) where the entry's block-property bytes start: in the
+                            decoded val_bytes (row) or in the batch's block bytes (colblk)         */
+  uint32_t* props_len;   /* [cap] (nullable)                                                      */
+  uint64_t* blk_base;    /* [n_blocks + 1] first entry of each index block; [n_blocks] = total    */
+  uint32_t* blk_status;  /* [n_blocks] PBL_OK / PBL_CORRUPT_INDEX / PBL_CORRUPT_COLBLK_HEADER /
+                            PBL_OVERFLOW (or the row decode's status)                             */
+  uint64_t cap;          /* entries the handle arrays hold                                         */
+} pbl_index_out;
+/*
+ * rowblk.IndexIter.BlockHandleWithProperties (rowblk/rowblk_index_iter.go:82-84)
+ * for every entry of a batch of row-format index blocks that pbl_decode_batch
+ * (flags 0) has decoded into `decoded`: entry k's value at
+ * val_bytes[blk_val_base[b] + val_off[..]] through block.DecodeHandleWithProperties
+ * (block/block.go:80-104: uvarint offset, uvarint length, the rest = properties).
+ * Entry k of the handle arrays is KV k of `decoded` (blk_base = blk_kv_base).  A
+ * value that is not a handle makes its block PBL_CORRUPT_INDEX.
+ */
+int pbl_index_handles_row(const pbl_decode_out* decoded, uint32_t n_blocks, pbl_index_out* out, void* stream);
+/*
+ * colblk.IndexIter over a batch of columnar index blocks (colblk/index_block.go:
+ * IndexBlockDecoder.Init :150-156, BlockHandleWithProperties :310-321):
+ * separators RawBytes, offsets and lengths Uint, block properties RawBytes;
+ * column layout checks as for data blocks (PBL_CORRUPT_COLBLK_HEADER).  Blocks
+ * are sized first (blk_base), then written; a total past cap reports
+ * PBL_OVERFLOW for the blocks that do not fit and writes none of their entries.
+ */
+int pbl_index_handles_col(const pbl_block_batch* batch, pbl_index_out* out, void* stream);
 
 /* ---- blockiter.Transforms on the device ------------------ */
 /* Comparer.Split used to find the suffix a SyntheticSuffix replaces. */

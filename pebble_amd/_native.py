@@ -26,15 +26,21 @@ PBL_DEVICE_ERROR = 8
 PBL_TIMEOUT = 9
 PBL_CORRUPT_CHECKSUM = 10
 PBL_CORRUPT_COMPRESSION = 11
+PBL_CORRUPT_FOOTER = 12
+PBL_CORRUPT_INDEX = 13
 STATUS_NAMES = {
     0: "OK", 1: "CORRUPT_NO_RESTARTS", 2: "CORRUPT_FIRST_KEY", 3: "CORRUPT_BOUNDS",
     4: "CORRUPT_COLBLK_HEADER", 5: "UNSUPPORTED", 6: "OVERFLOW", 7: "INVALID_ARG",
     8: "DEVICE_ERROR", 9: "TIMEOUT", 10: "CORRUPT_CHECKSUM", 11: "CORRUPT_COMPRESSION",
+    12: "CORRUPT_FOOTER", 13: "CORRUPT_INDEX",
 }
+# TableFormat (footer magic, version)
+PBL_TABLE_LEVELDB, PBL_TABLE_ROCKSDBV2 = 1, 2
+PBL_TABLE_PEBBLEV1 = 3  # .. PBL_TABLE_PEBBLEV8 = 10
 PBL_CHECKSUM_NONE, PBL_CHECKSUM_CRC32C, PBL_CHECKSUM_XXHASH, PBL_CHECKSUM_XXHASH64 = 0, 1, 2, 3
 PBL_COMPRESSION_NONE, PBL_COMPRESSION_SNAPPY, PBL_COMPRESSION_ZSTD, PBL_COMPRESSION_MINLZ = 0, 1, 7, 8
 
-ABI_VERSION = 3  # include/pebble_amd.h PBL_ABI_VERSION
+ABI_VERSION = 4  # include/pebble_amd.h PBL_ABI_VERSION
 
 PBL_FMT_ROW = 0
 PBL_FMT_COL_DEFAULT = 1
@@ -115,6 +121,21 @@ class PhysBatchC(ctypes.Structure):
                 ("reserved", ctypes.c_uint32)]
 
 
+class FooterC(ctypes.Structure):
+    _fields_ = [
+        ("table_format", ctypes.c_uint32), ("checksum_type", ctypes.c_uint32),
+        ("metaindex_off", ctypes.c_uint64), ("metaindex_len", ctypes.c_uint64),
+        ("index_off", ctypes.c_uint64), ("index_len", ctypes.c_uint64),
+        ("footer_off", ctypes.c_uint64), ("footer_len", ctypes.c_uint64),
+        ("attributes", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+    ]
+
+
+class IndexOutC(ctypes.Structure):
+    _fields_ = [("handle_off", _vp), ("handle_len", _vp), ("props_off", _vp), ("props_len", _vp),
+                ("blk_base", _vp), ("blk_status", _vp), ("cap", ctypes.c_uint64)]
+
+
 class TransformsC(ctypes.Structure):
     _fields_ = [
         ("synthetic_seq_num", ctypes.c_uint64), ("hide_obsolete_points", ctypes.c_uint32),
@@ -134,6 +155,10 @@ SIGNATURES = {
     "pbl_verify_checksums": (ctypes.c_int, [ctypes.POINTER(PhysBatchC), ctypes.c_uint32, _vp, _vp, _vp]),
     "pbl_decompressed_lengths": (ctypes.c_int, [ctypes.POINTER(PhysBatchC), _vp, _vp, _vp]),
     "pbl_decompress_blocks": (ctypes.c_int, [ctypes.POINTER(PhysBatchC), _vp, _vp, _vp, _vp, _vp, _vp]),
+    "pbl_parse_footer": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(FooterC)]),
+    "pbl_index_handles_row": (ctypes.c_int, [ctypes.POINTER(DecodeOutC), ctypes.c_uint32, ctypes.POINTER(IndexOutC),
+                                             _vp]),
+    "pbl_index_handles_col": (ctypes.c_int, [ctypes.POINTER(BlockBatchC), ctypes.POINTER(IndexOutC), _vp]),
     "pbl_transform_batch": (ctypes.c_int, [ctypes.POINTER(DecodeOutC), ctypes.c_uint32, ctypes.POINTER(TransformsC),
                                            ctypes.POINTER(DecodeOutC), _vp]),
     "pbl_rebase_blocks": (ctypes.c_int, [ctypes.POINTER(DecodeOutC), ctypes.c_uint32, ctypes.c_uint64,

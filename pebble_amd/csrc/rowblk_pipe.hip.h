@@ -267,6 +267,9 @@ __device__ __forceinline__ void run_write(Meta& M, const View& V, uint32_t r, ui
 // scratch), and the per-KV metadata is written from registers once the block
 // scan has placed the run.
 constexpr int kRunBuf = 16;
+#ifndef PBL_PAR_REGS
+#define PBL_PAR_REGS 0
+#endif
 
 struct RunBuf {
   uint32_t ea[kRunBuf];  // pos | shared << 16
@@ -349,6 +352,20 @@ __device__ __forceinline__ void run_emit_meta(Meta& M, const View& V, const RunB
         else fl |= PBL_KV_BLOB_HANDLE;
       }
       uint32_t par = j, parsh = 0;
+#if PBL_PAR_REGS
+      // prefix parent from the parked registers: the nearest earlier entry of
+      // the run with a shorter shared prefix (runs start at shared 0)
+      if (sh != 0) {
+#pragma unroll
+        for (int i = 0; i < k; i++) {
+          const uint32_t shi = B.ea[i] >> 16;
+          if (shi < sh) {
+            par = j - uint32_t(k - i);
+            parsh = shi;
+          }
+        }
+      }
+#else
       if (sh != 0) {
         uint32_t c = j - 1, csh = prev_sh;
         if (csh >= sh) { c = pp; csh = ppsh; }
@@ -359,6 +376,7 @@ __device__ __forceinline__ void run_emit_meta(Meta& M, const View& V, const RunB
         par = c;
         parsh = csh;
       }
+#endif
       M.eoff[j] = uint16_t(pos);
       M.ksrc[j] = uint16_t(pos + h);
       M.sh[j] = uint16_t(sh);

@@ -1,0 +1,137 @@
+"""Whole tables through the device (pebble_amd/sstable.py): footer -> index
+blocks (physical step + decode + pbl_index_handles_row, one or two levels) ->
+data-block handles as device arrays -> checksums, decompression, decode; the
+handles equal the fixture's independent walk and the KVs equal h.txt.  Columnar
+index blocks (pbl_index_handles_col) against the reference's index_block dumps
+and the oracle, with corrupt blocks and a capacity overflow."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from pebble_amd import _native as N
+from pebble_amd.batch import BlockBatch, decode
+from pebble_amd.rowblk import Writer, kvs_of_block
+from pebble_amd.sstable import Table, index_handles_col, index_handles_row
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+with open(os.path.join(GOLDEN, "sstable.json")) as f:
+    FIX = json.load(f)
+
+
+def table(name):
+    return Table(open(os.path.join(GOLDEN, "sst", FIX["tables"][name]["file"]), "rb").read())
+
+
+@pytest.mark.parametrize("name", ["hamlet_snappy", "h_no_compression", "h_two_level"])
+def test_tables_decode_to_hamlet(name, golden):
+    t = table(name)
+    assert t.footer.index == tuple(FIX["tables"][name]["index"])
+    h = t.data_block_handles()
+    n = int(h.blk_base[-1].item())
+    got = list(zip(h.handle_off[:n].cpu().tolist(), h.handle_len[:n].cpu().tolist()))
+    assert got == [tuple(x) for x in FIX["tables"][name]["data_handles"]]
+    r = t.decode().to_host()
+    assert r["status_mask"] == 0
+    kvs = []
+    for b in range(len(got)):
+        kvs += kvs_of_block(r, b)
+    assert [(kv.user_key.decode(), kv.value.decode()) for kv in kvs] == [tuple(x) for x in golden["hamlet_kvs"]]
+
+
+def test_zstd_table_reports_unsupported():
+    t = table("h_zstd")
+    with pytest.raises(Exception, match="UNSUPPORTED"):
+        t.data_block_handles()
+
+
+def test_corrupt_table_block_is_caught():
+    data = bytearray(open(os.path.join(GOLDEN, "sst", "h_no_compression.sst"), "rb").read())
+    o, ln = FIX["tables"]["h_no_compression"]["data_handles"][3]
+    data[o + ln // 2] ^= 0x20
+    with pytest.raises(Exception, match="checksum"):
+        Table(bytes(data)).data_blocks()
+
+
+def pack(blocks, align=8):
+    offs, lens, pos = [], [], 0
+    for bk in blocks:
+        pos = (pos + align - 1) // align * align
+        offs.append(pos)
+        lens.append(len(bk))
+        pos += len(bk)
+    buf = np.zeros(pos + 16, np.uint8)
+    for o, bk in zip(offs, blocks):
+        buf[o:o + len(bk)] = np.frombuffer(bk, np.uint8)
+    return buf, np.array(offs, np.uint64), np.array(lens, np.uint32)
+
+
+def test_colblk_index_blocks():
+    blocks = [bytes.fromhex(c["block_hex"]) for c in FIX["index_blocks"]]
+    bad = bytearray(blocks[0])
+    bad[12] = 3
+    blocks_all = blocks + [bytes(bad), blocks[2][:5]]
+    for align in (8, 1):
+        buf, off, lens = pack(blocks_all, align)
+        bb = BlockBatch.from_host(buf, off, lens, "cuda")
+        h = index_handles_col(bb)
+        st = h.status()
+        base = h.blk_base.cpu().numpy()
+        ho, hl = h.handle_off.cpu().numpy(), h.handle_len.cpu().numpy()
+        po, pl = h.props_off.cpu().numpy(), h.props_len.cpu().numpy()
+        for i, blk in enumerate(blocks_all):
+            ost, rows = oracle.index_block_col(blk)
+            assert st[i] == ost, i
+            if ost:
+                assert base[i + 1] == base[i]
+                continue
+            assert base[i + 1] - base[i] == len(rows)
+            for r, (_sep, o, ln, props) in enumerate(rows):
+                k = base[i] + r
+                assert (ho[k], hl[k]) == (o, ln)
+                assert bytes(buf[po[k]:po[k] + pl[k]]) == props
+        for i, c in enumerate(FIX["index_blocks"]):
+            assert [(int(ho[base[i] + r]), int(hl[base[i] + r])) for r in range(len(c["rows"]))] == \
+                [(r[1], r[2]) for r in c["rows"]]
+    # capacity overflow: the blocks that do not fit report PBL_OVERFLOW
+    buf, off, lens = pack(blocks)
+    h = index_handles_col(BlockBatch.from_host(buf, off, lens, "cuda"), cap=7)
+    assert h.total(len(blocks)) > 7  # (the re-run with the exact size succeeded)
+    from pebble_amd.sstable import IndexHandles
+    import ctypes
+    out = IndexHandles.allocate(len(blocks), 7, "cuda")
+    c = out.c_struct()
+    bb = BlockBatch.from_host(buf, off, lens, "cuda")
+    assert N.lib().pbl_index_handles_col(ctypes.byref(bb.c_struct()), ctypes.byref(c), None) == 0
+    st = out.status()
+    assert st[0] == 0 and (st == N.PBL_OVERFLOW).any()
+
+
+def test_row_index_corrupt_values():
+    """A row index block whose value is not a block handle (an unterminated
+    varint, an empty value) is PBL_CORRUPT_INDEX, as DecodeHandleWithProperties
+    errors; good blocks in the same batch are unaffected."""
+    def index_block(vals):
+        w = Writer(1)
+        for i, v in enumerate(vals):
+            w.add_raw(b"key%03d" % i + bytes(8), v)
+        return w.finish()
+    good = index_block([bytes([5, 7]), bytes([0x80, 0x01, 0x90, 0x01]) + b"props"])
+    bad1 = index_block([bytes([5, 7]), b"\xff" * 11])
+    bad2 = index_block([b""])
+    buf, off, lens = pack([good, bad1, bad2, good])
+    bb = BlockBatch.from_host(buf, off, lens, "cuda")
+    d = decode(bb)
+    h = index_handles_row(d, 4)
+    st = h.status()
+    assert list(st) == [0, N.PBL_CORRUPT_INDEX, N.PBL_CORRUPT_INDEX, 0]
+    base = h.blk_base.cpu().numpy()
+    ho, hl = h.handle_off.cpu().numpy(), h.handle_len.cpu().numpy()
+    for b in (0, 3):
+        assert [(int(ho[base[b] + i]), int(hl[base[b] + i])) for i in range(2)] == [(5, 7), (128, 144)]
+    for blk, s in ((good, 0), (bad1, 13), (bad2, 13)):
+        assert oracle.index_block_row(blk)[0] == s
