@@ -211,11 +211,14 @@ def lib() -> ctypes.CDLL:
     except Exception:  # pragma: no cover - torch is always present in this image
         pass
     L = ctypes.CDLL(LIB_PATH)
+    ab_build = bool(os.environ.get("PBL_LIB"))
     for name, (res, args) in SIGNATURES.items():
+        if ab_build and not hasattr(L, name):
+            continue  # an older A/B build (scripts/ab.sh): entry points it predates stay unbound
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    if L.pbl_abi_version() != ABI_VERSION:
+    if L.pbl_abi_version() != ABI_VERSION and not ab_build:
         raise RuntimeError("libpebble_amd.so ABI mismatch")
     _lib = L
     return L

@@ -396,11 +396,12 @@ __device__ __forceinline__ void col_emit(CLds& L, const Slot& E, const Args& A, 
 }
 
 // ---- the persistent kernel ----------------------------------------------------------
-__device__ __forceinline__ void col_pipe_body(CLds& L, const Args& A, const Queue& Q) {
+template <class Q>
+__device__ __forceinline__ void col_pipe_body(CLds& L, const Args& A, const Q& q) {
   const int t = threadIdx.x;
   const uint32_t nb = A.in.n_blocks;
   if (t == 0) {
-    const uint32_t t0 = Q.take();
+    const uint32_t t0 = q.take();
     L.s[1].mode = kNone;
     L.s[1].b = nb;
     if (t0 < nb) {
@@ -428,7 +429,7 @@ __device__ __forceinline__ void col_pipe_body(CLds& L, const Args& A, const Queu
     if (cb >= nb && E.mode == kNone) break;
     // the next ticket is taken now (its latency overlaps the parse): tickets are
     // held for one iteration only, which keeps the look-back distance short
-    if (t == 0) L.nxt = cb < nb ? Q.take() : nb;
+    if (t == 0) L.nxt = cb < nb ? q.take() : nb;
     ColPf pf;
     col_parse(L, P, E, A, P.schema);  // (wave 1 first resolves E's prefix)
     __syncthreads();
@@ -454,7 +455,7 @@ __device__ __forceinline__ void col_pipe_body(CLds& L, const Args& A, const Queu
 #ifndef PBL_COL_PIPE_BODY_ONLY  // (rowblk_decode.hip uses the body in the mixed pipeline)
 __global__ void __launch_bounds__(kTPB, PBL_COL_PIPE_WG) colblk_pipe_kernel(Args A) {
   __shared__ CLds L;
-  col_pipe_body(L, A, Queue{reinterpret_cast<uint32_t*>(A.out.workspace), nullptr, A.in.n_blocks, A.in.n_blocks});
+  col_pipe_body(L, A, TicketQueue{reinterpret_cast<uint32_t*>(A.out.workspace), A.in.n_blocks});
 }
 #endif
 

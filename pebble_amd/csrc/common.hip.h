@@ -96,18 +96,27 @@ __device__ inline uint32_t g_atomic_or(uint32_t* p, uint32_t v) {
   return __hip_atomic_fetch_or(to_glb(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// A persistent kernel's source of blocks: tickets from `tick`, mapped through
-// `ids` (a mixed batch's per-format list) or used as block ids directly.
-// take() returns a block id, or n_blocks when the queue is drained.
-struct Queue {
+// A persistent kernel's source of blocks.  take() returns a block id, or
+// n_blocks when the queue is drained.  TicketQueue: tickets are block ids (the
+// single-format kernels); ListQueue: tickets index an id list (a mixed batch's
+// per-format list).  Separate types keep the list indirection out of the
+// single-format kernels' code.
+struct TicketQueue {
   uint32_t* tick;
-  const uint32_t* ids;  // nullptr: ticket == block id
-  uint32_t n;           // tickets in this queue
-  uint32_t n_blocks;    // the sentinel
+  uint32_t n_blocks;
   __device__ uint32_t take() const {
     const uint32_t t = g_atomic_add(tick, 1u);
-    if (t >= n) return n_blocks;
-    return ids ? to_glb(ids)[t] : t;
+    return t < n_blocks ? t : n_blocks;
+  }
+};
+struct ListQueue {
+  uint32_t* tick;
+  const uint32_t* ids;
+  uint32_t n;         // tickets in this queue
+  uint32_t n_blocks;  // the sentinel
+  __device__ uint32_t take() const {
+    const uint32_t t = g_atomic_add(tick, 1u);
+    return t < n ? to_glb(ids)[t] : n_blocks;
   }
 };
 

@@ -928,9 +928,9 @@ mixed_pipe_kernel(Args A, const uint32_t* ids) {
                        (1000ull * n_row + uint64_t(PBL_MIX_COL_COST) * n_col);
   if (n_row && n_col) g_row = g_row < 1 ? 1 : g_row > G - 1 ? G - 1 : g_row;
   if (blockIdx.x < g_row)
-    pipe::row_pipe_body(L.row, A, Queue{hdr, ids, n_row, nb}, PBL_MIX_ROW_PRIO);
+    pipe::row_pipe_body<PBL_MIX_ROW_PRIO != 0>(L.row, A, ListQueue{hdr, ids, n_row, nb});
   else
-    col::cpipe::col_pipe_body(L.col, A, Queue{hdr + kWsColTick, ids + n_row, n_col, nb});
+    col::cpipe::col_pipe_body(L.col, A, ListQueue{hdr + kWsColTick, ids + n_row, n_col, nb});
 }
 
 // Size pass epilogue: a block that decoded reports PBL_OK, not the forced

@@ -748,6 +748,26 @@ __device__ __forceinline__ bool emit_resolve(const Meta& M, const Args& A, uint6
   return true;
 }
 
+#ifndef PBL_VAL_GLOBAL
+#define PBL_VAL_GLOBAL 0  // 1: value granules gathered from the block in global memory, not LDS
+#endif
+// 16 bytes at block offset x (may start before the block: those bytes are
+// masked by the caller) from global memory: two aligned loads and a funnel
+// shift, each load only inside the block's 16-B aligned extent.
+struct GlbBlk {
+  gptr<const uint8_t> g;
+  int64_t base, lo_al, hi_al;
+  __device__ __forceinline__ uint4 ld16(int32_t x) const {
+    const int64_t s_ = base + x, a = s_ & ~int64_t(15);
+    const uint32_t sh = uint32_t(s_ - a);
+    u32x4 p = u32x4{0, 0, 0, 0}, q = u32x4{0, 0, 0, 0};
+    if (a >= lo_al && a < hi_al) p = *(gptr<const u32x4>)(g + a);
+    if (sh && a + 16 < hi_al) q = *(gptr<const u32x4>)(g + a + 16);
+    const uint4 x4 = make_uint4(p.x, p.y, p.z, p.w), y4 = make_uint4(q.x, q.y, q.z, q.w);
+    return sh ? col::funnel16(x4, y4, sh) : x4;
+  }
+};
+
 // Emit stage, part 2 (waves 1-3): per-KV arrays, restart words, key and value
 // bytes of block M.b at the resolved bases.
 __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const Args& A, const uint64_t* excl) {
@@ -810,6 +830,12 @@ __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const 
   if (tvb) {
     const uint64_t d0 = vbb, d1 = vbb + tvb;
     const gptr<uint8_t> vbytes = to_glb(O.val_bytes);
+#if PBL_VAL_GLOBAL
+    const GlbBlk VG{to_glb(static_cast<const uint8_t*>(A.in.blocks)), int64_t(M.boff), int64_t(M.boff & ~uint64_t(15)),
+                    int64_t((M.boff + M.blen + 15) & ~uint64_t(15))};
+#else
+    const View& VG = V;
+#endif
     uint64_t a = (d0 & ~uint64_t(15)) + 16 * uint64_t(tb);
     for (; a < d1; a += 32 * kEmit) {
       uint4 w[2];
@@ -851,11 +877,11 @@ __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const 
         sb[u] = v1;
         eb[u] = oe[u] < v2 ? oe[u] : v2;
         const uint32_t gqa = uint32_t(d0 + sa[u] - (a + uint64_t(u) * 16 * kEmit));
-        ga[u] = V.ld16(int32_t(A0 >> 16) + int32_t(sa[u] - v0) - int32_t(gqa));
+        ga[u] = VG.ld16(int32_t(A0 >> 16) + int32_t(sa[u] - v0) - int32_t(gqa));
         const uint32_t gqb = gqa + (sb[u] - sa[u]);
         // (only read when the granule straddles into the next value: keep the
         // address inside the block otherwise)
-        gb[u] = V.ld16(oe[u] > v1 && !gen[u] ? int32_t(A1 >> 16) - int32_t(gqb) : 0);
+        gb[u] = VG.ld16(oe[u] > v1 && !gen[u] ? int32_t(A1 >> 16) - int32_t(gqb) : 0);
       }
 #pragma unroll
       for (int u = 0; u < 2; u++) {
@@ -881,7 +907,7 @@ __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const 
             const uint32_t v0 = vout_of(M, j), v1 = vout_of(M, j + 1);
             const uint32_t s_ = o[u] > v0 ? o[u] : v0, e_ = oe[u] < v1 ? oe[u] : v1;
             const uint32_t gq = uint32_t(d0 + s_ - g);
-            merge16(w[u], V.ld16(int32_t(vsrc_of(M, j)) + int32_t(s_ - v0) - int32_t(gq)), gq, gq + (e_ - s_));
+            merge16(w[u], VG.ld16(int32_t(vsrc_of(M, j)) + int32_t(s_ - v0) - int32_t(gq)), gq, gq + (e_ - s_));
             if (v1 >= oe[u]) break;
             j++;
           }
@@ -979,11 +1005,13 @@ struct PfWave {
 // X[(i+1)&1] (free again) and rotates the descriptors; the second barrier
 // publishes them.  Each role executes its own copies of the two barriers, so
 // the prefetch registers stay confined to the parse wave's code.
-__device__ __forceinline__ void row_pipe_body(PLds& S, const Args& A, const Queue& Q, bool prio = true) {
+template <bool kPrio, class Q>
+__device__ __forceinline__ void row_pipe_body(PLds& S, const Args& A, const Q& Q_) {
+  const Q& q = Q_;
   const int t = threadIdx.x;
   const uint32_t nb = A.in.n_blocks;
   if (t == 0) {
-    const uint32_t t0 = Q.take();
+    const uint32_t t0 = q.take();
     S.m[0].b = t0;
     S.m[0].mode = kModeNone;
     S.m[1].mode = kModeNone;
@@ -991,7 +1019,7 @@ __device__ __forceinline__ void row_pipe_body(PLds& S, const Args& A, const Queu
     if (t0 < nb) {
       S.m[0].boff = to_glb(A.in.block_off)[t0];
       S.m[0].blen = to_glb(A.in.block_len)[t0];
-      S.nxt = Q.take();
+      S.nxt = q.take();
     } else {
       S.nxt = nb;
     }
@@ -1008,7 +1036,7 @@ __device__ __forceinline__ void row_pipe_body(PLds& S, const Args& A, const Queu
   __syncthreads();
   // the parse wave is the pipeline's critical path: it wins VALU arbitration
   // against the emit wave of the other workgroup on its SIMD
-  if (t < kWave && prio) __builtin_amdgcn_s_setprio(2);
+  if (kPrio && t < kWave) __builtin_amdgcn_s_setprio(2);
   for (uint32_t i = 0;; i++) {
     Meta& cur = S.m[i & 1];
     Meta& prv = S.m[(i + 1) & 1];
@@ -1045,7 +1073,7 @@ __device__ __forceinline__ void row_pipe_body(PLds& S, const Args& A, const Queu
       prv.boff = nx_off;
       prv.blen = nx_len;
       prv.mode = kModeNone;
-      S.nxt = nx < nb ? Q.take() : nb;
+      S.nxt = nx < nb ? q.take() : nb;
     }
     __syncthreads();
   }
@@ -1053,7 +1081,7 @@ __device__ __forceinline__ void row_pipe_body(PLds& S, const Args& A, const Queu
 
 __global__ void __launch_bounds__(kPTPB) __attribute__((amdgpu_waves_per_eu(PBL_PIPE_WAVES / 2, PBL_PIPE_WAVES / 2))) rowblk_pipe_kernel(Args A) {
   __shared__ PLds S;
-  row_pipe_body(S, A, Queue{reinterpret_cast<uint32_t*>(A.out.workspace), nullptr, A.in.n_blocks, A.in.n_blocks});
+  row_pipe_body<true>(S, A, TicketQueue{reinterpret_cast<uint32_t*>(A.out.workspace), A.in.n_blocks});
 }
 
 }  // namespace pipe
