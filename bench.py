@@ -271,7 +271,10 @@ def main():
     ab = alg_bytes(hres, nb, input_bytes)
     achieved = ab / (kern_ms * 1e-3) / 1e9
     traffic = None
-    tp = os.path.join(ROOT, "profiles", "pmc_traffic.json" if a.workload == "row" else f"pmc_traffic_{a.workload}.json")
+    tname = ("pmc_traffic.json" if a.workload == "row" else
+             f"pmc_traffic_zipf_ri{a.restart_interval}.json" if a.workload == "zipf" and a.zipf_format == "row" else
+             f"pmc_traffic_{a.workload}.json")
+    tp = os.path.join(ROOT, "profiles", tname)
     if os.path.exists(tp):
         try:
             with open(tp) as f:

@@ -4,10 +4,11 @@
 // [checksum LE32] (sstable/block/block.go:539-571).
 //
 //   checksum_crc_kernel   CRC32C (internal/crc/crc.go): one wave per block;
-//                         each lane CRCs a contiguous chunk (slicing-by-4 from an
-//                         LDS table), the wave folds the 64 chunk CRCs with the
-//                         GF(2) shift operator (crc(A||B) = crc(A)*x^(8|B|) +
-//                         crc(B) mod P), then Value()'s rotation + delta
+//                         lane l CRCs the 16-B granules l, l+64, ... (coalesced
+//                         1 KiB wave loads, slicing-by-16 tables in LDS), carrying
+//                         its state across the 1008-B gaps by a constant GF(2)
+//                         multiply; the lane states combine by shift and XOR
+//                         (the CRC is linear), then Value()'s rotation + delta
 //   checksum_xxh_kernel   XXH64 truncated to 32 bits (cespare/xxhash/v2, the
 //                         ChecksumTypeXXHash64 of block.go:155-160): one lane
 //                         per block (XXH64's stripes are sequential)
@@ -21,6 +22,7 @@
 #include <algorithm>
 
 #include "common.hip.h"
+#include "colblk_block.hip.h"
 
 namespace pbl {
 namespace phys {
@@ -41,29 +43,33 @@ __device__ inline uint32_t multmodp(uint32_t a, uint32_t b) {
   return p;
 }
 
+// Tables: slicing-by-16 (T[k][b] = CRC of byte b followed by k zero bytes) and
+// multiplication by the constant K = x^(8*1008) mod P split by byte.
+constexpr uint32_t kGap = 63 * 16;  // bytes between a lane's consecutive granules
 struct CrcLds {
-  uint32_t tab[4][256];  // slicing-by-4
-  uint32_t x2n[32];      // x^(2^k) mod P
+  uint32_t t[16][256];
+  uint32_t m[4][256];
+  uint32_t x2n[32];  // x^(2^k) mod P
 };
 
 __device__ inline void crc_tables(CrcLds& L) {
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
     uint32_t c = i;
     for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ kPoly : c >> 1;
-    L.tab[0][i] = c;
-  }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
-    uint32_t c = L.tab[0][i];
-    for (int s = 1; s < 4; s++) {
-      c = L.tab[0][c & 0xff] ^ (c >> 8);
-      L.tab[s][i] = c;
-    }
+    L.t[0][i] = c;
   }
   if (threadIdx.x == 0) {
     uint32_t p = 1u << 30;  // x^1
     L.x2n[0] = p;
     for (int k = 1; k < 32; k++) L.x2n[k] = p = multmodp(p, p);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+    uint32_t c = L.t[0][i];
+    for (int k = 1; k < 16; k++) {
+      c = L.t[0][c & 0xff] ^ (c >> 8);
+      L.t[k][i] = c;
+    }
   }
   __syncthreads();
 }
@@ -80,46 +86,87 @@ __device__ inline uint32_t x8nmodp(const CrcLds& L, uint64_t n) {
   return p;
 }
 
-// Go's crc32.Update(0, castagnoli, p[0:n]) of one lane's chunk (conditioned)
-__device__ inline uint32_t crc_chunk(const CrcLds& L, gptr<const uint8_t> p, uint64_t n) {
-  uint32_t c = ~0u;
-  uint64_t i = 0;
-  // byte steps up to a 4-B boundary, then 4-B slices, then the tail
-  while (i < n && ((uint64_t(p) + i) & 3)) c = L.tab[0][(c ^ p[i++]) & 0xff] ^ (c >> 8);
-  for (; i + 4 <= n; i += 4) {
-    c ^= *(gptr<const uint32_t>)(p + i);
-    c = L.tab[3][c & 0xff] ^ L.tab[2][(c >> 8) & 0xff] ^ L.tab[1][(c >> 16) & 0xff] ^ L.tab[0][c >> 24];
-  }
-  for (; i < n; i++) c = L.tab[0][(c ^ p[i]) & 0xff] ^ (c >> 8);
-  return ~c;
+__device__ inline void crc_mul_tables(CrcLds& L) {
+  __shared__ uint32_t K;
+  if (threadIdx.x == 0) K = x8nmodp(L, kGap);
+  __syncthreads();
+  for (uint32_t e = threadIdx.x; e < 1024; e += blockDim.x) L.m[e >> 8][e & 255] = multmodp(K, (e & 255u) << (8 * (e >> 8)));
+  __syncthreads();
 }
 
+// raw (unconditioned) CRC update of state s by 16 bytes w (slicing-by-16)
+__device__ __forceinline__ uint32_t crc16(const CrcLds& L, uint32_t s, const uint4& w) {
+  const uint32_t a = w.x ^ s;
+  return L.t[15][a & 0xff] ^ L.t[14][(a >> 8) & 0xff] ^ L.t[13][(a >> 16) & 0xff] ^ L.t[12][a >> 24] ^
+         L.t[11][w.y & 0xff] ^ L.t[10][(w.y >> 8) & 0xff] ^ L.t[9][(w.y >> 16) & 0xff] ^ L.t[8][w.y >> 24] ^
+         L.t[7][w.z & 0xff] ^ L.t[6][(w.z >> 8) & 0xff] ^ L.t[5][(w.z >> 16) & 0xff] ^ L.t[4][w.z >> 24] ^
+         L.t[3][w.w & 0xff] ^ L.t[2][(w.w >> 8) & 0xff] ^ L.t[1][(w.w >> 16) & 0xff] ^ L.t[0][w.w >> 24];
+}
+// s * x^(8*kGap) mod P
+__device__ __forceinline__ uint32_t crc_gap(const CrcLds& L, uint32_t s) {
+  return L.m[0][s & 0xff] ^ L.m[1][(s >> 8) & 0xff] ^ L.m[2][(s >> 16) & 0xff] ^ L.m[3][s >> 24];
+}
+
+// Data granule j (bytes [16j, 16j+16) of the block) from global memory: one
+// aligned load, or two and a funnel shift when the block is not 16-B aligned
+// (the batch is readable to the next 16-B boundary past every block's trailer).
+__device__ __forceinline__ uint4 granule(gptr<const uint8_t> base, uint32_t sh, uint32_t j) {
+  const gptr<const u32x4> a = (gptr<const u32x4>)(base - sh + 16ull * j);
+  const u32x4 x = a[0];
+  const uint4 x4 = make_uint4(x.x, x.y, x.z, x.w);
+  if (!sh) return x4;
+  const u32x4 y = a[1];
+  return col::funnel16(x4, make_uint4(y.x, y.y, y.z, y.w), sh);
+}
+
+// One wave per block.  Lane l takes the 16-B granules l, l+64, l+128, ... (each
+// wave load is 1 KiB contiguous); its raw CRC is carried across the 1008-byte
+// gaps by the constant multiply, the 64 lane states are shifted to the end of
+// the data and XORed, the < 16-byte tail is added by lane 0, and the init ~0
+// enters as x^(8n) * ~0 (linearity of the CRC).  Then Go's final complement and
+// crc.CRC.Value()'s rotation and delta.
 __global__ void __launch_bounds__(kTPB) checksum_crc_kernel(const pbl_phys_batch B, uint32_t* status,
                                                             uint32_t* computed) {
   __shared__ CrcLds L;
   crc_tables(L);
+  crc_mul_tables(L);
   const uint32_t lane = lane_id(), wpb = kTPB / kWave;
   for (uint32_t b = blockIdx.x * wpb + wave_id(); b < B.n_blocks; b += gridDim.x * wpb) {
     const uint64_t n = uint64_t(B.block_len[b]) + 1;  // the block and its compression indicator
-    const gptr<const uint8_t> p = to_glb(B.bytes + B.block_off[b]);
-    const uint64_t chunk = ((n + kWave - 1) / kWave + 3) & ~uint64_t(3);
-    const uint64_t lo = min<uint64_t>(n, lane * chunk), hi = min<uint64_t>(n, lo + chunk);
-    uint32_t c = crc_chunk(L, p + lo, hi - lo);
-    uint32_t len = uint32_t(hi - lo);
-    // fold: lane l absorbs lane l+d (the chunk after it) at each level
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-      const uint32_t c2 = __shfl_down(c, d, kWave);
-      const uint32_t l2 = __shfl_down(len, d, kWave);
-      if ((lane & (2 * d - 1)) == 0 && lane + d < kWave) {
-        if (l2) c = multmodp(x8nmodp(L, l2), c) ^ c2;
-        len += l2;
-      }
+    const uint64_t off = B.block_off[b];
+    const gptr<const uint8_t> p = to_glb(B.bytes + off);
+    const uint32_t sh = uint32_t(off & 15);
+    const uint64_t G = n >> 4;  // full granules
+    uint32_t s = 0;
+    uint64_t j = lane;
+    // four granules in flight per lane
+    for (; j + 3 * kWave < G; j += 4 * kWave) {
+      const uint4 g0 = granule(p, sh, uint32_t(j)), g1 = granule(p, sh, uint32_t(j + kWave)),
+                  g2 = granule(p, sh, uint32_t(j + 2 * kWave)), g3 = granule(p, sh, uint32_t(j + 3 * kWave));
+      s = crc16(L, j == lane ? s : crc_gap(L, s), g0);
+      s = crc16(L, crc_gap(L, s), g1);
+      s = crc16(L, crc_gap(L, s), g2);
+      s = crc16(L, crc_gap(L, s), g3);
     }
+    for (; j < G; j += kWave) {
+      const uint4 g = granule(p, sh, uint32_t(j));
+      s = crc16(L, j == lane ? s : crc_gap(L, s), g);
+    }
+    // shift to the end of the full granules (16*G): the lane's last ends at 16*(jl+1)
+    if (uint64_t(lane) < G) {
+      const uint64_t jl = lane + ((G - 1 - lane) / kWave) * kWave;
+      const uint64_t after = 16 * (G - jl - 1);
+      if (after) s = multmodp(x8nmodp(L, after), s);
+    }
+#pragma unroll
+    for (int d = kWave / 2; d >= 1; d >>= 1) s ^= __shfl_xor(s, d, kWave);
     if (lane == 0) {
+      uint32_t t = s;
+      for (uint64_t i = 16 * G; i < n; i++) t = L.t[0][(t ^ p[i]) & 0xff] ^ (t >> 8);  // the tail, raw
+      const uint32_t c = ~(t ^ multmodp(x8nmodp(L, n), ~0u));
       const uint32_t v = ((c >> 15) | (c << 17)) + 0xa282ead8u;  // crc.CRC.Value()
-      const gptr<const uint8_t> t = p + (n - 1) + 1;
-      const uint32_t want = uint32_t(t[0]) | uint32_t(t[1]) << 8 | uint32_t(t[2]) << 16 | uint32_t(t[3]) << 24;
+      const gptr<const uint8_t> tr = p + n;
+      const uint32_t want = uint32_t(tr[0]) | uint32_t(tr[1]) << 8 | uint32_t(tr[2]) << 16 | uint32_t(tr[3]) << 24;
       status[b] = v == want ? PBL_OK : PBL_CORRUPT_CHECKSUM;
       if (computed) computed[b] = v;
     }

@@ -2,7 +2,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 D=${PROF_OUT:-gpurun_out/prof}; mkdir -p $D
 R="rocprofv3 --output-format csv"
-P="python3 scripts/prof_decode.py 65536 5 ${PROF_WORKLOAD:-row}"
+P="python3 scripts/prof_decode.py ${PROF_BLOCKS:-65536} 5 ${PROF_WORKLOAD:-row}"
 timeout -k 10 300 rocprofv3 -L > $D/counters_list.txt 2>&1; \
 timeout -k 10 300 $R --kernel-trace --stats -d $D/trace -o trace -- $P > $D/trace.log 2>&1 && \
 timeout -k 10 300 $R --pmc FETCH_SIZE -d $D/fetch -o fetch -- $P > $D/fetch.log 2>&1 && \

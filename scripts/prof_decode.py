@@ -18,12 +18,35 @@ if workload == "col":
     from pebble_amd.colblk import gen_col_blocks
     buf, off, lens, n = gen_col_blocks(42, nb, 32768, n_threads=16)
     b = BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_COL_CRDB1, 0)
-elif workload == "zipf":
-    # config 5, row format, restart interval 16 (bench.py --workload zipf)
+elif workload.startswith("zipf"):
+    # config 5 (bench.py --workload zipf): "zipf" / "zipf:RI" row format at
+    # restart interval RI (default 16), "zipf:col" colblk DefaultKeySchema
     from pebble_amd import _native as N
     from pebble_amd.batch import gen_zipf_blocks
-    buf, off, lens, n = gen_zipf_blocks(42, nb, N.PBL_FMT_ROW, 16, 32768, n_threads=16)
-    b = BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, 0)
+    arg = workload.split(":")[1] if ":" in workload else "16"
+    fmt = N.PBL_FMT_COL_DEFAULT if arg == "col" else N.PBL_FMT_ROW
+    ri = 16 if arg == "col" else int(arg)
+    buf, off, lens, n = gen_zipf_blocks(42, nb, fmt, ri, 32768, n_threads=16)
+    b = BlockBatch.from_host(buf, off, lens, "cuda", fmt, 0)
+elif workload == "mixed":
+    # config 4 shard: even ids row (config-2 shape), odd ids colblk crdb1 (config-3 shape)
+    import numpy as np
+    from pebble_amd import _native as N
+    from pebble_amd.colblk import gen_col_blocks
+    h = nb // 2
+    rb, ro, rl, rn = gen_row_blocks(42, nb - h, 32768, 16, 16, 100, n_threads=16)
+    cb, co, cl, cn = gen_col_blocks(42, h, 32768, n_threads=16)
+    buf = np.zeros(nb * 32768 + 16, np.uint8)
+    v = buf[: nb * 32768].reshape(nb, 32768)
+    v[0::2] = rb[: (nb - h) * 32768].reshape(nb - h, 32768)
+    v[1::2] = cb[: h * 32768].reshape(h, 32768)
+    off = np.arange(nb, dtype=np.uint64) * 32768
+    lens = np.empty(nb, np.uint32)
+    lens[0::2], lens[1::2] = rl, cl
+    bf = np.empty(nb, np.uint8)
+    bf[0::2], bf[1::2] = N.PBL_FMT_ROW, N.PBL_FMT_COL_CRDB1
+    n = rn + cn
+    b = BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, 0, block_format=bf)
 else:
     buf, off, lens, n = gen_row_blocks(42, nb, 32768, 16, 16, 100, n_threads=16)
     b = BlockBatch.from_host(buf, off, lens, "cuda")

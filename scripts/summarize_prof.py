@@ -43,10 +43,12 @@ if "FETCH_SIZE" in means and "WRITE_SIZE" in means:
     out["hbm_bytes_per_launch"] = fetch + write
     json.dump({"kernel": KERNEL, "workload": WORKLOAD, "workload_blocks": NB, "block_size": 32768,
                "fetch_bytes_corrected": fetch, "write_bytes": write,
-               **({"restart_interval": 16, "zipf_format": "row"} if WORKLOAD == "zipf" else {}),
+               **({"restart_interval": int(WORKLOAD.split(":")[1]) if ":" in WORKLOAD else 16, "zipf_format": "row"}
+                  if WORKLOAD.startswith("zipf") else {}),
                "hbm_bytes_per_launch": fetch + write,
                "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes; FETCH_SIZE(KiB)x2x1024 "
                          "(gfx950 16-B/lane streaming-read correction), WRITE_SIZE(KiB)x1024",
-               "source": f"profiles/{tag}_pmc.json"}, open(os.path.join(dst, "pmc_traffic.json" if WORKLOAD == "row" else f"pmc_traffic_{WORKLOAD}.json"), "w"), indent=1)
+               "source": f"profiles/{tag}_pmc.json"}, open(os.path.join(dst, "pmc_traffic.json" if WORKLOAD == "row" else
+                      f"pmc_traffic_{WORKLOAD.replace(':', '_ri')}.json"), "w"), indent=1)
 json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
