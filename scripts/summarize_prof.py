@@ -41,7 +41,7 @@ if "FETCH_SIZE" in means and "WRITE_SIZE" in means:
     fetch = means["FETCH_SIZE"] * 2 * 1024
     write = means["WRITE_SIZE"] * 1024
     out["hbm_bytes_per_launch"] = fetch + write
-    json.dump({"kernel": KERNEL, "workload": WORKLOAD, "workload_blocks": NB, "block_size": 32768,
+    json.dump({"kernel": KERNEL, "workload": WORKLOAD.split(":")[0], "workload_blocks": NB, "block_size": 32768,
                "fetch_bytes_corrected": fetch, "write_bytes": write,
                **({"restart_interval": int(WORKLOAD.split(":")[1]) if ":" in WORKLOAD else 16, "zipf_format": "row"}
                   if WORKLOAD.startswith("zipf") else {}),
