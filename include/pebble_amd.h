@@ -217,7 +217,9 @@ int pbl_offset_concat(pbl_decode_out* out, uint32_t n_blocks, const uint64_t* ra
 /* ---- physical blocks: checksums and decompression --------- */
 /* Blocks as they sit in an SST: [block bytes][compression indicator u8][checksum
  * LE32] (sstable/block/block.go:539-571); block_len is the block.Handle length
- * (the 5-byte trailer follows it). */
+ * (the 5-byte trailer follows it).  The kernels read in aligned 16-B granules:
+ * `bytes` must stay readable for 16 bytes past every block's trailer (an SST
+ * file's own following bytes, or 16 bytes of padding after the buffer). */
 typedef struct pbl_phys_batch {
   const uint8_t* bytes;      /* DEVICE bytes                                           */
   const uint64_t* block_off; /* [n_blocks] DEVICE offset of each block in `bytes`        */

@@ -1036,7 +1036,10 @@ __device__ __forceinline__ void row_pipe_body(PLds& S, const Args& A, const Q& Q
   __syncthreads();
   // the parse wave is the pipeline's critical path: it wins VALU arbitration
   // against the emit wave of the other workgroup on its SIMD
-  if (kPrio && t < kWave) __builtin_amdgcn_s_setprio(2);
+#ifndef PBL_PARSE_PRIO
+#define PBL_PARSE_PRIO 2
+#endif
+  if (kPrio && t < kWave) __builtin_amdgcn_s_setprio(PBL_PARSE_PRIO);
   for (uint32_t i = 0;; i++) {
     Meta& cur = S.m[i & 1];
     Meta& prv = S.m[(i + 1) & 1];
