@@ -106,7 +106,10 @@ typedef struct pbl_block_batch {
                                 physical trailer).  Must be readable up to the next
                                 16-byte boundary after every block.                 */
   const uint64_t* block_off; /* [n_blocks] byte offset of each block in `blocks`    */
-  const uint32_t* block_len; /* [n_blocks] byte length of each block                */
+  const uint32_t* block_len; /* [n_blocks] byte length of each block (< 4 GiB: the
+                                rowblk 64-bit offsets of rowblk_64bit_test.go:28-183
+                                are out of scope; blocks are <= 32 KiB in practice
+                                and the general path handles any u32 length)      */
   uint32_t n_blocks;
   uint32_t format;           /* PBL_FMT_* for every block of the batch              */
   uint32_t flags;            /* PBL_ROW_* flags                                     */

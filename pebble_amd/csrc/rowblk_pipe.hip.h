@@ -267,9 +267,6 @@ __device__ __forceinline__ void run_write(Meta& M, const View& V, uint32_t r, ui
 // scratch), and the per-KV metadata is written from registers once the block
 // scan has placed the run.
 constexpr int kRunBuf = 16;
-#ifndef PBL_PAR_REGS
-#define PBL_PAR_REGS 0
-#endif
 
 struct RunBuf {
   uint32_t ea[kRunBuf];  // pos | shared << 16
@@ -352,20 +349,6 @@ __device__ __forceinline__ void run_emit_meta(Meta& M, const View& V, const RunB
         else fl |= PBL_KV_BLOB_HANDLE;
       }
       uint32_t par = j, parsh = 0;
-#if PBL_PAR_REGS
-      // prefix parent from the parked registers: the nearest earlier entry of
-      // the run with a shorter shared prefix (runs start at shared 0)
-      if (sh != 0) {
-#pragma unroll
-        for (int i = 0; i < k; i++) {
-          const uint32_t shi = B.ea[i] >> 16;
-          if (shi < sh) {
-            par = j - uint32_t(k - i);
-            parsh = shi;
-          }
-        }
-      }
-#else
       if (sh != 0) {
         uint32_t c = j - 1, csh = prev_sh;
         if (csh >= sh) { c = pp; csh = ppsh; }
@@ -376,7 +359,6 @@ __device__ __forceinline__ void run_emit_meta(Meta& M, const View& V, const RunB
         par = c;
         parsh = csh;
       }
-#endif
       M.eoff[j] = uint16_t(pos);
       M.ksrc[j] = uint16_t(pos + h);
       M.sh[j] = uint16_t(sh);
@@ -748,26 +730,6 @@ __device__ __forceinline__ bool emit_resolve(const Meta& M, const Args& A, uint6
   return true;
 }
 
-#ifndef PBL_VAL_GLOBAL
-#define PBL_VAL_GLOBAL 0  // 1: value granules gathered from the block in global memory, not LDS
-#endif
-// 16 bytes at block offset x (may start before the block: those bytes are
-// masked by the caller) from global memory: two aligned loads and a funnel
-// shift, each load only inside the block's 16-B aligned extent.
-struct GlbBlk {
-  gptr<const uint8_t> g;
-  int64_t base, lo_al, hi_al;
-  __device__ __forceinline__ uint4 ld16(int32_t x) const {
-    const int64_t s_ = base + x, a = s_ & ~int64_t(15);
-    const uint32_t sh = uint32_t(s_ - a);
-    u32x4 p = u32x4{0, 0, 0, 0}, q = u32x4{0, 0, 0, 0};
-    if (a >= lo_al && a < hi_al) p = *(gptr<const u32x4>)(g + a);
-    if (sh && a + 16 < hi_al) q = *(gptr<const u32x4>)(g + a + 16);
-    const uint4 x4 = make_uint4(p.x, p.y, p.z, p.w), y4 = make_uint4(q.x, q.y, q.z, q.w);
-    return sh ? col::funnel16(x4, y4, sh) : x4;
-  }
-};
-
 // Emit stage, part 2 (waves 1-3): per-KV arrays, restart words, key and value
 // bytes of block M.b at the resolved bases.
 __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const Args& A, const uint64_t* excl) {
@@ -830,12 +792,6 @@ __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const 
   if (tvb) {
     const uint64_t d0 = vbb, d1 = vbb + tvb;
     const gptr<uint8_t> vbytes = to_glb(O.val_bytes);
-#if PBL_VAL_GLOBAL
-    const GlbBlk VG{to_glb(static_cast<const uint8_t*>(A.in.blocks)), int64_t(M.boff), int64_t(M.boff & ~uint64_t(15)),
-                    int64_t((M.boff + M.blen + 15) & ~uint64_t(15))};
-#else
-    const View& VG = V;
-#endif
     uint64_t a = (d0 & ~uint64_t(15)) + 16 * uint64_t(tb);
     for (; a < d1; a += 32 * kEmit) {
       uint4 w[2];
@@ -877,11 +833,11 @@ __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const 
         sb[u] = v1;
         eb[u] = oe[u] < v2 ? oe[u] : v2;
         const uint32_t gqa = uint32_t(d0 + sa[u] - (a + uint64_t(u) * 16 * kEmit));
-        ga[u] = VG.ld16(int32_t(A0 >> 16) + int32_t(sa[u] - v0) - int32_t(gqa));
+        ga[u] = V.ld16(int32_t(A0 >> 16) + int32_t(sa[u] - v0) - int32_t(gqa));
         const uint32_t gqb = gqa + (sb[u] - sa[u]);
         // (only read when the granule straddles into the next value: keep the
         // address inside the block otherwise)
-        gb[u] = VG.ld16(oe[u] > v1 && !gen[u] ? int32_t(A1 >> 16) - int32_t(gqb) : 0);
+        gb[u] = V.ld16(oe[u] > v1 && !gen[u] ? int32_t(A1 >> 16) - int32_t(gqb) : 0);
       }
 #pragma unroll
       for (int u = 0; u < 2; u++) {
@@ -907,7 +863,7 @@ __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const 
             const uint32_t v0 = vout_of(M, j), v1 = vout_of(M, j + 1);
             const uint32_t s_ = o[u] > v0 ? o[u] : v0, e_ = oe[u] < v1 ? oe[u] : v1;
             const uint32_t gq = uint32_t(d0 + s_ - g);
-            merge16(w[u], VG.ld16(int32_t(vsrc_of(M, j)) + int32_t(s_ - v0) - int32_t(gq)), gq, gq + (e_ - s_));
+            merge16(w[u], V.ld16(int32_t(vsrc_of(M, j)) + int32_t(s_ - v0) - int32_t(gq)), gq, gq + (e_ - s_));
             if (v1 >= oe[u]) break;
             j++;
           }
