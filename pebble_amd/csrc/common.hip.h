@@ -15,7 +15,15 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));  // native 8-B vecto
 constexpr int kTPB = 256;   // threads per workgroup (4 waves); one workgroup per block
 constexpr int kWave = 64;
 constexpr int kNumComp = 4; // look-back components: n_kv, key bytes, value bytes, restarts
-constexpr int kLbWin = 8;   // look-back windows (of 64 predecessors) loaded per round trip
+#ifndef PBL_LB_WIN
+#define PBL_LB_WIN 2
+#endif
+// Look-back windows (of 64 predecessors) loaded per round trip.  Fewer windows
+// mean more round trips on a long walk but a smaller, lower-pressure resolve
+// (it is inlined into every persistent kernel): measured on the MI355X (config
+// 2 / 3 / 4 GiB/s) 8 windows 972 / 1199 / 857, 4: 999 / - / -, 2: 1036 / 1270
+// / 893, 1: 1035 / 1228 / -.
+constexpr int kLbWin = PBL_LB_WIN;
 
 // ---- workspace layout ------------------------------------------------------
 // [0,256): ticket counter (u32 [0]), big-block count (u32 [1], row pipeline), pad.  Then

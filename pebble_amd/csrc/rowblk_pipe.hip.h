@@ -43,8 +43,18 @@ namespace pipe {
                                   ws_bytes((A_).in.n_blocks))[uint64_t(b_) * 16 + (i_)] =       \
           __builtin_amdgcn_s_memtime();                                                         \
   } while (0)
+// slot i_ = the wave's HW_ID (SIMD / CU / SE) and XCC_ID: where the roles run
+#define PHWID(A_, b_, i_, lane0_)                                                              \
+  do {                                                                                          \
+    if (lane0_)                                                                                 \
+      reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>((A_).out.workspace) +             \
+                                  ws_bytes((A_).in.n_blocks))[uint64_t(b_) * 16 + (i_)] =       \
+          uint64_t(__builtin_amdgcn_s_getreg(4 | (31 << 11))) |                                 \
+          uint64_t(__builtin_amdgcn_s_getreg(20 | (15 << 11))) << 32;                           \
+  } while (0)
 #else
 #define PSTAMP(A_, b_, i_, lane0_) do {} while (0)
+#define PHWID(A_, b_, i_, lane0_) do {} while (0)
 #endif
 
 constexpr int kKv = 400;                       // KVs (and runs) per block on the pipelined path
@@ -52,6 +62,9 @@ constexpr uint32_t kKeyCap = 32768;            // user-key bytes per block on th
 constexpr int kBs = 7;                         // output bucket = 128 bytes
 constexpr int kKBkt = kKeyCap >> kBs;          // key buckets
 constexpr int kVBkt = kMaxFastLen >> kBs;      // value buckets (values <= block length)
+#ifndef PBL_EMIT_PF_EARLY
+#define PBL_EMIT_PF_EARLY 2
+#endif
 #ifndef PBL_PIPE_WAVES
 #define PBL_PIPE_WAVES 4
 #endif
@@ -570,6 +583,7 @@ __device__ __forceinline__ void parse_block(Meta& M, uint4* X, const Args& A) {
   uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
   const View V = lds_view(X, uint32_t(kPad + (boff & 15)));
   PSTAMP(A, b, 0, l == 0);
+  PHWID(A, b, 14, l == 0);
 
   uint32_t roff, nres;
   uint32_t status = fits ? init_checks(LdsRd{V}, blen, flags, &roff, &nres)
@@ -732,7 +746,9 @@ __device__ __forceinline__ bool emit_resolve(const Meta& M, const Args& A, uint6
 
 // Emit stage, part 2 (waves 1-3): per-KV arrays, restart words, key and value
 // bytes of block M.b at the resolved bases.
-__device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const Args& A, const uint64_t* excl) {
+template <class F>
+__device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const Args& A, const uint64_t* excl,
+                                           const F& mid) {
   const int tb = int(threadIdx.x) - kWave;
   const uint32_t b = M.b, flags = A.in.flags;
   const pbl_decode_out& O = A.out;
@@ -740,12 +756,14 @@ __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const 
   const View V = lds_view(X, uint32_t(kPad + (M.boff & 15)));
   const uint64_t kvb = excl[0], kbb = excl[1], vbb = excl[2], rbb = excl[3];
   PSTAMP(A, b, 5, tb == 0);
+  PHWID(A, b, 15, tb == 0);
 
   const gptr<uint32_t> key_off = to_glb(O.key_off), val_off = to_glb(O.val_off);
   const gptr<uint64_t> trailer = to_glb(O.trailer);
   const gptr<uint8_t> kv_flags = to_glb(O.kv_flags);
   const gptr<uint32_t> entry_off = to_glb(O.entry_off), restarts = to_glb(O.restarts);
 
+  auto per_kv = [&]() {
   // per-KV arrays (coalesced, thread per KV)
   for (uint32_t j = tb; j <= nkv; j += kEmit) {
     const uint64_t o = kvb + b + j;
@@ -762,6 +780,8 @@ __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const 
     for (uint32_t r = tb; r < nres; r += kEmit) restarts[rbb + r] = V.le32(roff + 4 * r);
   PSTAMP(A, b, 6, tb == 0);
 
+  };
+  auto key_bytes = [&]() {
   // key bytes: one 16-B aligned output granule per thread; each the merge of
   // the segments of the 1-2 keys it overlaps (each key its prefix chain)
   if (tkb) {
@@ -783,6 +803,8 @@ __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const 
     }
   }
   PSTAMP(A, b, 7, tb == 0);
+  };
+  auto value_bytes = [&]() {
   // value bytes: one 16-B aligned output granule per thread, two granules per
   // step with their LDS round trips interleaved: (1) bucket -> first KV,
   // (2) a 5-word window of packed (vout | vsrc) words -> the KV holding the
@@ -872,6 +894,25 @@ __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const 
       }
     }
   }
+  };
+#if PBL_EMIT_PF_EARLY == 2
+  mid();
+  value_bytes();
+  per_kv();
+  key_bytes();
+#elif PBL_EMIT_PF_EARLY
+  // values first: the next block's loads (mid) then land during the key and
+  // per-KV phases instead of between the iteration's barriers
+  value_bytes();
+  mid();
+  per_kv();
+  key_bytes();
+#else
+  per_kv();
+  key_bytes();
+  value_bytes();
+  mid();
+#endif
   PSTAMP(A, b, 8, tb == 0);
 #ifdef PBL_STAMPS
   // the last emitter wave to finish: per-wave end stamps
@@ -1015,13 +1056,15 @@ __device__ __forceinline__ void row_pipe_body(PLds& S, const Args& A, const Q& Q
       uint64_t excl[kNumComp];
 #ifdef PBL_EXP_NO_EMIT
       emit_resolve(prv, A, excl);  // diagnostic build: parse timing without the emit stage
-#else
-      if (emit_resolve(prv, A, excl)) emit_write(prv, S.x[(i + 1) & 1], A, excl);
-#endif
-      // the next block's loads go out once this wave's stores are issued: they
-      // land while the parse wave finishes (no prefetch registers live during
-      // the emit loops)
       if (pf_on) pf.load(A.in.blocks, nx_off, nx_len);
+#else
+      // the next block's loads go out once this wave's value stores are issued
+      auto pf_issue = [&]() {
+        if (pf_on) pf.load(A.in.blocks, nx_off, nx_len);
+      };
+      if (emit_resolve(prv, A, excl)) emit_write(prv, S.x[(i + 1) & 1], A, excl, pf_issue);
+      else pf_issue();
+#endif
     }
     __syncthreads();
     PSTAMP(A, cb, 13, t == 0 && cb < nb);

@@ -50,3 +50,19 @@ t0 = st[:, 0][st[:, 0] > 0]
 t1 = st[:, 8][st[:, 8] > 0]
 print(f"kernel span (first parse .. last emit) {t1.max() - t0.min():.0f} cycles; "
       f"{(t1.max() - t0.min()) / nb * 512:.0f} cycles per block per workgroup-slot")
+# Role placement (slots 14/15: HW_ID | XCC_ID << 32 of the parse wave and emit wave 1):
+# per CU, the SIMDs its parse waves ran on.
+hw = st[:, 14].astype(np.uint64)
+hw1 = st[:, 15].astype(np.uint64)
+ok = hw != 0
+simd = (hw >> np.uint64(4)) & np.uint64(3)
+cu = ((hw >> np.uint64(32)) & np.uint64(15)) << np.uint64(12) | ((hw >> np.uint64(8)) & np.uint64(0x1f)) | \
+     (((hw >> np.uint64(12)) & np.uint64(0xf)) << np.uint64(5))
+sets = {}
+for c, s in zip(cu[ok].tolist(), simd[ok].tolist()):
+    sets.setdefault(c, set()).add(s)
+sizes = np.bincount([len(v) for v in sets.values()], minlength=5)
+print(f"CUs seen {len(sets)}; parse-wave SIMD sets per CU by size (0..4): {sizes.tolist()}")
+print("parse-wave SIMD histogram:", np.bincount(simd[ok].astype(np.int64), minlength=4).tolist(),
+      " emit-wave-1 SIMD histogram:", np.bincount(((hw1[hw1 != 0] >> np.uint64(4)) & np.uint64(3)).astype(np.int64),
+                                                  minlength=4).tolist())
