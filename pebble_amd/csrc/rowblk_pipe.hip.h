@@ -65,6 +65,10 @@ constexpr int kVBkt = kMaxFastLen >> kBs;      // value buckets (values <= block
 #ifndef PBL_EMIT_PF_EARLY
 #define PBL_EMIT_PF_EARLY 2
 #endif
+#ifndef PBL_VU
+#define PBL_VU 2
+#endif
+constexpr int kVU = PBL_VU;  // value granules per emit-loop step (their LDS round trips interleaved)
 #ifndef PBL_PIPE_WAVES
 #define PBL_PIPE_WAVES 4
 #endif
@@ -815,12 +819,12 @@ __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const 
     const uint64_t d0 = vbb, d1 = vbb + tvb;
     const gptr<uint8_t> vbytes = to_glb(O.val_bytes);
     uint64_t a = (d0 & ~uint64_t(15)) + 16 * uint64_t(tb);
-    for (; a < d1; a += 32 * kEmit) {
-      uint4 w[2];
-      uint32_t lo[2], hi[2], o[2], oe[2], j0[2];
-      bool live[2];
+    for (; a < d1; a += 16 * kVU * kEmit) {
+      uint4 w[kVU];
+      uint32_t lo[kVU], hi[kVU], o[kVU], oe[kVU], j0[kVU];
+      bool live[kVU];
 #pragma unroll
-      for (int u = 0; u < 2; u++) {
+      for (int u = 0; u < kVU; u++) {
         const uint64_t g = a + uint64_t(u) * 16 * kEmit;
         live[u] = g < d1;
         lo[u] = g < d0 ? uint32_t(d0 - g) : 0u;
@@ -829,16 +833,16 @@ __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const 
         oe[u] = live[u] ? uint32_t(g + hi[u] - d0) : 0u;
         j0[u] = M.vbkt[o[u] >> kBs];
       }
-      uint32_t vw[2][5];
+      uint32_t vw[kVU][5];
 #pragma unroll
-      for (int u = 0; u < 2; u++)
+      for (int u = 0; u < kVU; u++)
 #pragma unroll
         for (int k = 0; k < 5; k++) vw[u][k] = M.vp[j0[u] + k];
-      uint4 ga[2], gb[2];
-      uint32_t sa[2], ea[2], sb[2], eb[2];
-      bool gen[2];
+      uint4 ga[kVU], gb[kVU];
+      uint32_t sa[kVU], ea[kVU], sb[kVU], eb[kVU];
+      bool gen[kVU];
 #pragma unroll
-      for (int u = 0; u < 2; u++) {
+      for (int u = 0; u < kVU; u++) {
         const uint32_t q = o[u];
         const bool s1 = (vw[u][1] & 0xffff) <= q;
         const bool s2 = s1 && (vw[u][2] & 0xffff) <= q;
@@ -862,7 +866,7 @@ __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const 
         gb[u] = V.ld16(oe[u] > v1 && !gen[u] ? int32_t(A1 >> 16) - int32_t(gqb) : 0);
       }
 #pragma unroll
-      for (int u = 0; u < 2; u++) {
+      for (int u = 0; u < kVU; u++) {
         if (!live[u]) continue;
         const uint64_t g = a + uint64_t(u) * 16 * kEmit;
         if (!gen[u]) {
