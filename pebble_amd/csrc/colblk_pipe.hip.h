@@ -200,10 +200,11 @@ __device__ __forceinline__ void col_parse_rows(CLds& L, Slot& P, const Args& A, 
   }
 }
 
+template <bool kSizeOnly = false>
 __device__ __forceinline__ void col_parse(CLds& L, Slot& P, const Slot& E, const Args& A, uint32_t schema) {
   const Src S = slot_src(P, A);
   CSTAMP(A, P.b, 0);
-  if (wave_id() == 1 && E.mode != kNone) col_resolve(L, E, A);
+  if (!kSizeOnly && wave_id() == 1 && E.mode != kNone) col_resolve(L, E, A);
   if (wave_id() == 0 && P.b < A.in.n_blocks) {
     const uint32_t st = parse_block_wave(S, schema, &P.d);
     if (lane_id() == 0) {
@@ -396,7 +397,9 @@ __device__ __forceinline__ void col_emit(CLds& L, const Slot& E, const Args& A, 
 }
 
 // ---- the persistent kernel ----------------------------------------------------------
-template <class Q>
+// kSizeOnly: parse and publish every block's aggregate, no resolve and no
+// outputs (the first pass of a sequential mixed batch, rowblk_decode.hip).
+template <class Q, bool kSizeOnly = false>
 __device__ __forceinline__ void col_pipe_body(CLds& L, const Args& A, const Q& q) {
   const int t = threadIdx.x;
   const uint32_t nb = A.in.n_blocks;
@@ -431,7 +434,7 @@ __device__ __forceinline__ void col_pipe_body(CLds& L, const Args& A, const Q& q
     // held for one iteration only, which keeps the look-back distance short
     if (t == 0) L.nxt = cb < nb ? q.take() : nb;
     ColPf pf;
-    col_parse(L, P, E, A, P.schema);  // (wave 1 first resolves E's prefix)
+    col_parse<kSizeOnly>(L, P, E, A, P.schema);  // (wave 1 first resolves E's prefix)
     __syncthreads();
     const uint32_t nx = L.nxt;
     uint64_t nx_off = 0;
@@ -442,7 +445,7 @@ __device__ __forceinline__ void col_pipe_body(CLds& L, const Args& A, const Q& q
     }
     const bool pf_on = nx < nb && (nx_off & 7) == 0;
     if (pf_on) pf.load(A.in.blocks, nx_off, nx_len);  // lands during the emit
-    if (E.mode != kNone) col_emit(L, E, A, E.schema);
+    if (!kSizeOnly && E.mode != kNone) col_emit(L, E, A, E.schema);
     __syncthreads();
     if (t == 0) slot_setup(E, nx < nb ? nx : nb, nx_off, nx_len, A);
     if (pf_on) pf.store(E, nx_off, nx_len);

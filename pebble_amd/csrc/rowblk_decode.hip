@@ -842,6 +842,9 @@ namespace row {
 #ifndef PBL_MIX_COL_COST
 #define PBL_MIX_COL_COST 1300
 #endif
+#ifndef PBL_MIXED_SEQ
+#define PBL_MIXED_SEQ 1  // 0: one mixed_pipe_kernel launch (A/B)
+#endif
 #ifndef PBL_MIX_ROW_PRIO
 #define PBL_MIX_ROW_PRIO 0  // 1: the row parse wave at s_setprio 2 as in rowblk_pipe_kernel (measured 858 vs 870 GiB/s without)
 #endif
@@ -931,6 +934,77 @@ mixed_pipe_kernel(Args A, const uint32_t* ids) {
     pipe::row_pipe_body<PBL_MIX_ROW_PRIO != 0>(L.row, A, ListQueue{hdr, ids, n_row, nb});
   else
     col::cpipe::col_pipe_body(L.col, A, ListQueue{hdr + kWsColTick, ids + n_row, n_col, nb});
+}
+
+// Sequential mixed batches (the default): three persistent launches over the
+// split id lists instead of one.  (1) mixed_col_size_kernel parses every
+// colblk block and publishes its aggregate; (2) mixed_row_kernel runs the row
+// pipeline over the row list, its look-back walking through the colblk
+// aggregates; (3) mixed_col_kernel runs the colblk pipeline over the colblk
+// list (its predecessors' prefixes are all published: its look-back ends at
+// the row block before it).  Each launch gets its own occupancy (row 2, colblk
+// 3 workgroups per CU) and its own code: the single mixed launch holds both
+// bodies under the union LDS layout (2 workgroups per CU for both roles) and
+// its roles advance at the pace of the slower one.  Deadlock-free: (2) waits
+// only on aggregates published by (1) or by its own resident workgroups in
+// ticket order, (3) on aggregates published by (1) and its own workgroups.
+constexpr int kWsColTick2 = 4;  // header u32 [4]: the colblk queue of launch (3)
+
+// (1): one wave per colblk block, straight from global memory (no staging: a
+// size needs the header, the key columns' offsets and the value bounds only),
+// many waves per CU to hide the latency (measured: a 256-thread workgroup per
+// block 0.73 ms, a wave per block 0.47 ms on config 4's 64 Ki colblk blocks).
+// Same parse_block_wave / row_parts / value_ok as the pipeline, so the
+// aggregate is the one the pipeline publishes again in (3).
+__global__ void __launch_bounds__(kWave) mixed_col_size_kernel(Args A, const uint32_t* ids) {
+  __shared__ col::Desc d;
+  const uint32_t nb = A.in.n_blocks;
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(A.out.workspace);
+  uint64_t* lb_state = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(A.out.workspace) + kWsHeader);
+  const uint32_t n_row = __hip_atomic_load(to_glb(hdr) + kWsRowCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t n_col = nb - n_row;
+  for (uint32_t i = blockIdx.x; i < n_col; i += gridDim.x) {
+    const uint32_t b = to_glb(ids)[n_row + i];
+    const uint32_t blen = to_glb(A.in.block_len)[b];
+    const uint32_t schema = to_glb(A.in.block_format)[b];
+    const col::Src S{nullptr, nullptr, (col::glb_cu8)(A.in.blocks + to_glb(A.in.block_off)[b]), 0u, 0xffffffffu, blen};
+    uint32_t st = col::parse_block_wave(S, schema, &d);
+    const uint32_t rows = st == PBL_OK ? d.rows : 0;
+    uint64_t kb = 0;
+    bool bad = false;
+    // (not unrolled: 4 rows per lane in flight measured 0.89 against 0.47 ms)
+    for (uint32_t r = lane_id(); r < rows; r += kWave) {
+      const col::RowParts p = col::row_parts<false>(S, d, schema, r);
+      bad |= !p.ok || !col::value_ok(S, d, r);
+      kb += p.klen;
+    }
+    kb = wave_sum(kb);
+    if (st == PBL_OK) {
+      if (__ballot(bad)) st = PBL_CORRUPT_BOUNDS;
+      else if (kb > 0xffffffffull || uint64_t(d.v_hi - d.v_lo) > 0xffffffffull) st = PBL_UNSUPPORTED;
+    }
+    const bool ok = st == PBL_OK;
+    const uint64_t agg[kNumComp] = {ok ? rows : 0u, ok ? kb : 0ull, ok ? uint64_t(d.v_hi - d.v_lo) : 0ull, 0ull};
+    lb_publish(lb_state, nb, b, agg);
+    wave_sync();  // (d is rewritten by the next block's parse)
+  }
+}
+
+__global__ void __launch_bounds__(pipe::kPTPB) __attribute__((amdgpu_waves_per_eu(PBL_PIPE_WAVES / 2, PBL_PIPE_WAVES / 2)))
+mixed_row_kernel(Args A, const uint32_t* ids) {
+  __shared__ pipe::PLds S;
+  const uint32_t nb = A.in.n_blocks;
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(A.out.workspace);
+  const uint32_t n_row = __hip_atomic_load(to_glb(hdr) + kWsRowCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  pipe::row_pipe_body<true>(S, A, ListQueue{hdr, ids, n_row, nb});
+}
+
+__global__ void __launch_bounds__(kTPB, PBL_COL_PIPE_WG) mixed_col_kernel(Args A, const uint32_t* ids) {
+  __shared__ col::cpipe::CLds L;
+  const uint32_t nb = A.in.n_blocks;
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(A.out.workspace);
+  const uint32_t n_row = __hip_atomic_load(to_glb(hdr) + kWsRowCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  col::cpipe::col_pipe_body(L, A, ListQueue{hdr + kWsColTick2, ids + n_row, nb - n_row, nb});
 }
 
 // Size pass epilogue: a block that decoded reports PBL_OK, not the forced
@@ -1027,6 +1101,23 @@ int launch_mixed(const pbl_block_batch* batch, const pbl::Args& a, hipStream_t s
   hipLaunchKernelGGL(pbl::row::mixed_split_scatter_kernel, dim3(nch), dim3(pbl::kTPB), 0, st, a,
                      static_cast<const uint32_t*>(counts), nch, ids);
   int cus = 0;
+#if PBL_MIXED_SEQ
+  const uint64_t g_r = pbl::persistent_grid(st, pbl::kKMixedRow, reinterpret_cast<const void*>(pbl::row::mixed_row_kernel),
+                                            nb, &cus, pbl::row::pipe::kPTPB);
+  const uint64_t g_c = pbl::persistent_grid(st, pbl::kKMixedCol, reinterpret_cast<const void*>(pbl::row::mixed_col_kernel),
+                                            nb, &cus);
+  if (!g_r || !g_c) return PBL_DEVICE_ERROR;
+  const uint32_t g_cs = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 32));
+  const uint32_t small = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4));
+  const uint32_t* cids = static_cast<const uint32_t*>(ids);
+  hipLaunchKernelGGL(pbl::row::pipe::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+  hipLaunchKernelGGL(pbl::row::mixed_col_size_kernel, dim3(g_cs), dim3(pbl::kWave), 0, st, a, cids);
+  hipLaunchKernelGGL(pbl::row::mixed_row_kernel, dim3(uint32_t(g_r)), dim3(pbl::row::pipe::kPTPB), 0, st, a, cids);
+  hipLaunchKernelGGL(pbl::row::mixed_col_kernel, dim3(uint32_t(g_c)), dim3(pbl::kTPB), 0, st, a, cids);
+  if (values)
+    hipLaunchKernelGGL(pbl::row::pipe::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+  return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
+#else
   const uint64_t grid = pbl::persistent_grid(st, pbl::kKMixedPipe,
                                              reinterpret_cast<const void*>(pbl::row::mixed_pipe_kernel), nb, &cus,
                                              pbl::row::pipe::kPTPB);
@@ -1038,6 +1129,7 @@ int launch_mixed(const pbl_block_batch* batch, const pbl::Args& a, hipStream_t s
   if (values)
     hipLaunchKernelGGL(pbl::row::pipe::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
+#endif
 }
 }  // namespace
 
