@@ -363,7 +363,7 @@ __device__ inline void lb_finish(uint64_t* st, uint32_t n_blocks, uint32_t v, co
       }
       if (__shfl(timed_out ? 1 : 0, 0, kWave)) { timed_out = true; break; }
     }
-    LbWindows<kLbWin> G;
+    LbWindows<W> G;
     G.issue(P, top);
     done = lb_consume(P, n_blocks, G, acc, &top, &wait_idx, &spins, &timed_out);
     if (__ballot(timed_out)) timed_out = true;
@@ -379,9 +379,10 @@ __device__ inline void lb_finish(uint64_t* st, uint32_t n_blocks, uint32_t v, co
   }
 }
 
+template <int W = kLbWin>
 __device__ inline void lb_resolve(uint64_t* st, uint32_t n_blocks, uint32_t v, const uint64_t agg[kNumComp],
                                   uint64_t excl[kNumComp], uint32_t* timeout_flag) {
-  LbWindows<kLbWin> G;
+  LbWindows<W> G;
   if (v > 0) G.issue(LbPtrs(st, n_blocks), int64_t(v) - 1);
   lb_finish(st, n_blocks, v, agg, excl, timeout_flag, G);
 }

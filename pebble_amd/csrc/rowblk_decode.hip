@@ -842,6 +842,9 @@ namespace row {
 #ifndef PBL_MIX_COL_COST
 #define PBL_MIX_COL_COST 1300
 #endif
+#ifndef PBL_MIX_ROW_LB_WIN
+#define PBL_MIX_ROW_LB_WIN 2  // measured 1 / 2 / 4 / 8 windows: - / 965 / 954 / 946 GiB/s on config 4
+#endif
 #ifndef PBL_MIXED_SEQ
 #define PBL_MIXED_SEQ 1  // 0: one mixed_pipe_kernel launch (A/B)
 #endif
@@ -996,7 +999,8 @@ mixed_row_kernel(Args A, const uint32_t* ids) {
   const uint32_t nb = A.in.n_blocks;
   uint32_t* hdr = reinterpret_cast<uint32_t*>(A.out.workspace);
   const uint32_t n_row = __hip_atomic_load(to_glb(hdr) + kWsRowCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  pipe::row_pipe_body<true>(S, A, ListQueue{hdr, ids, n_row, nb});
+  // (its look-back walks over the interleaved colblk aggregates as well)
+  pipe::row_pipe_body<true, ListQueue, PBL_MIX_ROW_LB_WIN>(S, A, ListQueue{hdr, ids, n_row, nb});
 }
 
 __global__ void __launch_bounds__(kTPB, PBL_COL_PIPE_WG) mixed_col_kernel(Args A, const uint32_t* ids) {

@@ -575,6 +575,7 @@ __global__ void __launch_bounds__(kWave) big_block_values_kernel(Args A) {
 }
 
 // Parse stage: wave 0, block M.b staged in X (if it fits).
+template <int W = kLbWin>
 __device__ __forceinline__ void parse_block(Meta& M, uint4* X, const Args& A) {
   const int l = lane_id();
   const uint32_t b = M.b, blen = M.blen;
@@ -661,7 +662,7 @@ __device__ __forceinline__ void parse_block(Meta& M, uint4* X, const Args& A) {
   // resolve this block's exclusive prefix now: the parse wave has slack, the
   // emit waves then start on their stores at once next iteration
   uint64_t excl[kNumComp];
-  lb_resolve(lb_state, nb, b, agg, excl, &A.out.totals->status_mask);
+  lb_resolve<W>(lb_state, nb, b, agg, excl, &A.out.totals->status_mask);
   PSTAMP(A, b, 4, l == 0);
   if (okb && overflows(A.out, excl, agg)) status = PBL_OVERFLOW;
   if (l == 0) {
@@ -1006,7 +1007,7 @@ struct PfWave {
 // X[(i+1)&1] (free again) and rotates the descriptors; the second barrier
 // publishes them.  Each role executes its own copies of the two barriers, so
 // the prefetch registers stay confined to the parse wave's code.
-template <bool kPrio, class Q>
+template <bool kPrio, class Q, int W = kLbWin>  // W: the parse wave's look-back windows per round trip
 __device__ __forceinline__ void row_pipe_body(PLds& S, const Args& A, const Q& Q_) {
   const Q& q = Q_;
   const int t = threadIdx.x;
@@ -1055,7 +1056,7 @@ __device__ __forceinline__ void row_pipe_body(PLds& S, const Args& A, const Q& Q
     const bool pf_on = nx < nb && nx_len <= kMaxFastLen;
     PfEmit pf;
     if (t < kWave) {
-      if (cb < nb) parse_block(cur, S.x[i & 1], A);
+      if (cb < nb) parse_block<W>(cur, S.x[i & 1], A);
     } else {
       uint64_t excl[kNumComp];
 #ifdef PBL_EXP_NO_EMIT

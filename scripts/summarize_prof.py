@@ -26,16 +26,28 @@ WORKLOAD = sys.argv[4] if len(sys.argv) > 4 else "row"
 
 shutil.copy(os.path.join(src, "trace", "trace_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
 pmc = collections.defaultdict(list)
+# KERNEL may name several kernels joined by "+" (a decode made of several
+# launches, e.g. the mixed path): per-dispatch means and trace averages are
+# summed over them
+KERNELS = KERNEL.split("+")
 for f in glob.glob(os.path.join(src, "*", "*_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        if KERNEL in r["Kernel_Name"]:
-            pmc[r["Counter_Name"]].append(float(r["Counter_Value"]))
-means = {k: sum(v) / len(v) for k, v in pmc.items()}
+        for k in KERNELS:
+            if k + "(" in r["Kernel_Name"]:
+                pmc[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
+means = collections.defaultdict(float)
+for (k, c), v in pmc.items():
+    means[c] += sum(v) / len(v)
+means = dict(means)
 stats = {}
 for r in csv.DictReader(open(os.path.join(src, "trace", "trace_kernel_stats.csv"))):
-    if KERNEL in r["Name"]:
-        stats = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
-                 "max_ns": float(r["MaxNs"])}
+    for k in KERNELS:
+        if k + "(" in r["Name"]:
+            if not stats:
+                stats = {"calls": int(r["Calls"]), "avg_ns": 0.0, "min_ns": 0.0, "max_ns": 0.0}
+            stats["avg_ns"] += float(r["AverageNs"])
+            stats["min_ns"] += float(r["MinNs"])
+            stats["max_ns"] += float(r["MaxNs"])
 out = {"kernel": KERNEL, "workload_blocks": NB, "trace": stats, "pmc_per_dispatch_mean": means}
 if "FETCH_SIZE" in means and "WRITE_SIZE" in means:
     fetch = means["FETCH_SIZE"] * 2 * 1024
