@@ -843,7 +843,7 @@ namespace row {
 #define PBL_MIX_COL_COST 1300
 #endif
 #ifndef PBL_MIX_ROW_LB_WIN
-#define PBL_MIX_ROW_LB_WIN 2  // measured 1 / 2 / 4 / 8 windows: - / 965 / 954 / 946 GiB/s on config 4
+#define PBL_MIX_ROW_LB_WIN 2  // measured 2 / 4 / 8 windows: 965 / 954 / 946 GiB/s on config 4
 #endif
 #ifndef PBL_MIXED_SEQ
 #define PBL_MIXED_SEQ 1  // 0: one mixed_pipe_kernel launch (A/B)
@@ -959,7 +959,11 @@ constexpr int kWsColTick2 = 4;  // header u32 [4]: the colblk queue of launch (3
 // block 0.73 ms, a wave per block 0.47 ms on config 4's 64 Ki colblk blocks).
 // Same parse_block_wave / row_parts / value_ok as the pipeline, so the
 // aggregate is the one the pipeline publishes again in (3).
-__global__ void __launch_bounds__(kWave) mixed_col_size_kernel(Args A, const uint32_t* ids) {
+#ifndef PBL_COL_SIZE_WAVES
+#define PBL_COL_SIZE_WAVES 8  // waves per SIMD (64 VGPRs): config 4 951 at 4 (101 VGPRs), 975 at 8
+#endif
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PBL_COL_SIZE_WAVES)))
+mixed_col_size_kernel(Args A, const uint32_t* ids) {
   __shared__ col::Desc d;
   const uint32_t nb = A.in.n_blocks;
   uint32_t* hdr = reinterpret_cast<uint32_t*>(A.out.workspace);
