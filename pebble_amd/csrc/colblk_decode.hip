@@ -8,7 +8,11 @@
 namespace pbl {
 namespace col {
 
-__global__ void __launch_bounds__(kTPB) colblk_decode_kernel(Args A) {
+#ifndef PBL_COL_SINGLE_WAVES
+#define PBL_COL_SINGLE_WAVES 7  // waves per SIMD (= workgroups per CU: 7 x 21.4 KB LDS); config 5 colblk 4: 433, 5: 524, 6: 643, 7: 690, 8: 466 GiB/s (64 VGPRs spill)
+#endif
+__global__ void __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(PBL_COL_SINGLE_WAVES)))
+colblk_decode_kernel(Args A) {
   __shared__ Lds s;
   __shared__ uint32_t ticket;
   uint32_t* ticket_ctr = reinterpret_cast<uint32_t*>(A.out.workspace);
