@@ -263,23 +263,39 @@ __global__ void __launch_bounds__(kTPB) snappy_len_kernel(const pbl_phys_batch B
   }
 }
 
+// Staged block bytes sit at their global 16-B phase (byte j of the block at
+// src[(block address & 15) + j]) so the staging loads and the output stores
+// are aligned 16-B accesses; 32 bytes of slack cover the phase and the 16-B
+// literal copies that run past an element's end.
+// PBL_SNAPPY_VEC: 16-B staging, literal / long-offset copies and output
+// stores (written this round, not yet run on the GPU: off by default).
+#ifndef PBL_SNAPPY_VEC
+#define PBL_SNAPPY_VEC 0
+#endif
 struct SnapLds {
-  uint8_t src[kSnapCap + 16];
-  uint8_t dst[kSnapCap + 16];
+  uint4 src4[(kSnapCap + 32) / 16];
+  uint4 dst4[(kSnapCap + 32) / 16];
 };
 
+typedef uint32_t su32x4_u __attribute__((ext_vector_type(4), aligned(1)));
 struct LdsBytes {
   lptr<uint8_t> p;
+  static constexpr bool kVec = true;
   __device__ uint8_t operator[](uint32_t i) const { return p[i]; }
+  __device__ su32x4_u get16(uint32_t i) const { return *(lptr<const su32x4_u>)(p + i); }
 };
 struct LdsBytesW {
   lptr<uint8_t> p;
   __device__ uint8_t get(uint32_t i) const { return p[i]; }
   __device__ void set(uint32_t i, uint8_t v) const { p[i] = v; }
+  __device__ su32x4_u get16(uint32_t i) const { return *(lptr<const su32x4_u>)(p + i); }
+  __device__ void set16(uint32_t i, su32x4_u v) const { *(lptr<su32x4_u>)(p + i) = v; }
 };
 struct GlbBytes {
   gptr<const uint8_t> p;
+  static constexpr bool kVec = false;
   __device__ uint8_t operator[](uint32_t i) const { return p[i]; }
+  __device__ su32x4_u get16(uint32_t) const { return su32x4_u{0, 0, 0, 0}; }
 };
 struct GlbBytesW {
   gptr<uint8_t> p;
@@ -344,10 +360,24 @@ __device__ inline uint32_t snappy_wave(Src src, uint32_t n, Dst dst, uint32_t ca
       s += 5;
     }
     if (kind != 0 && (off == 0 || off > d || len > dlen - d)) { ok = false; break; }
-    if (kind == 0) {
-      for (uint32_t i = lane; i < len; i += step) dst.set(d + i, src[lit + i]);
+    if constexpr (Src::kVec && PBL_SNAPPY_VEC) {
+      // LDS -> LDS (the wave): 16 bytes per lane per step.  A chunk may write
+      // up to 15 bytes past the element's end: later elements rewrite them, and
+      // copies read only below d.  A copy whose offset is at least one step's
+      // span (64 x 16 B) never reads what the same step writes.
+      if (kind == 0) {
+        for (uint32_t i = 16 * lane; i < len; i += 16 * step) dst.set16(d + i, src.get16(lit + i));
+      } else if (off >= 16 * kWave) {
+        for (uint32_t i = 16 * lane; i < len; i += 16 * step) dst.set16(d + i, dst.get16(d - off + i));
+      } else {
+        for (uint32_t i = lane; i < len; i += step) dst.set(d + i, dst.get(d - off + (i % off)));
+      }
     } else {
-      for (uint32_t i = lane; i < len; i += step) dst.set(d + i, dst.get(d - off + (i % off)));
+      if (kind == 0) {
+        for (uint32_t i = lane; i < len; i += step) dst.set(d + i, src[lit + i]);
+      } else {
+        for (uint32_t i = lane; i < len; i += step) dst.set(d + i, dst.get(d - off + (i % off)));
+      }
     }
     wave_sync();
     d += len;
@@ -376,14 +406,53 @@ __global__ void __launch_bounds__(kWave) snappy_kernel(const pbl_phys_batch B, u
       if (!uvarint32(src, n, &dl, &used)) st = PBL_CORRUPT_COMPRESSION;
       else if (dl > cap) st = PBL_OVERFLOW;
       else if (n <= kSnapCap && dl <= kSnapCap) {
+#if !PBL_SNAPPY_VEC
         // stage the compressed bytes, decode LDS -> LDS, write the output out
-        for (uint32_t i = lane; i < n; i += kWave) S.src[i] = src[i];
+        lptr<uint8_t> s_src = to_lds_ptr(reinterpret_cast<uint8_t*>(S.src4));
+        lptr<uint8_t> s_dst = to_lds_ptr(reinterpret_cast<uint8_t*>(S.dst4));
+        for (uint32_t i = lane; i < n; i += kWave) s_src[i] = src[i];
         wave_sync();
-        len = snappy_wave(LdsBytes{to_lds_ptr(S.src)}, n, LdsBytesW{to_lds_ptr(S.dst)}, dl, lane, kWave);
+        len = snappy_wave(LdsBytes{s_src}, n, LdsBytesW{s_dst}, dl, lane, kWave);
         wave_sync();
         if (len == ~0u) st = PBL_CORRUPT_COMPRESSION;
         else
-          for (uint32_t i = lane; i < len; i += kWave) dst[i] = S.dst[i];
+          for (uint32_t i = lane; i < len; i += kWave) dst[i] = s_dst[i];
+#else
+        // stage the compressed bytes (aligned 16-B granules: the last one
+        // stays inside the 16-B granule of the block's last byte), decode
+        // LDS -> LDS, write the output as aligned 16-B granules
+        const uint64_t sa = reinterpret_cast<uint64_t>(B.bytes + B.block_off[b]);
+        const uint32_t ssh = uint32_t(sa & 15), ng = (ssh + n + 15) / 16;
+        const gptr<const u32x4> sg = to_glb(reinterpret_cast<const u32x4*>(sa - ssh));
+        lptr<u32x4> sl = to_lds_ptr(reinterpret_cast<u32x4*>(S.src4));
+        for (uint32_t g = lane; g < ng; g += kWave) sl[g] = sg[g];
+        const uint64_t da = reinterpret_cast<uint64_t>(out + out_off[b]);
+        const uint32_t dsh = uint32_t(da & 15);
+        lptr<uint8_t> sdst = to_lds_ptr(reinterpret_cast<uint8_t*>(S.dst4)) + dsh;
+        wave_sync();
+        len = snappy_wave(LdsBytes{to_lds_ptr(reinterpret_cast<uint8_t*>(S.src4)) + ssh}, n, LdsBytesW{sdst}, dl, lane,
+                          kWave);
+        wave_sync();
+        if (len == ~0u) st = PBL_CORRUPT_COMPRESSION;
+        else {
+          const uint32_t nd = (dsh + len + 15) / 16;
+          const gptr<u32x4> dg = to_glb(reinterpret_cast<u32x4*>(da - dsh));
+          const lptr<const u32x4> dl4 = to_lds_ptr(reinterpret_cast<const u32x4*>(S.dst4));
+          for (uint32_t g = lane; g < nd; g += kWave) {
+            const u32x4 v = dl4[g];
+            const uint32_t lo = g == 0 ? dsh : 0u, hi = g + 1 == nd ? dsh + len - 16 * g : 16u;
+            if (lo == 0 && hi == 16) {
+              dg[g] = v;
+            } else {
+              gptr<uint8_t> db = reinterpret_cast<gptr<uint8_t>>(dg + g);
+              for (uint32_t k = lo; k < hi; k++) {
+                const uint32_t w = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
+                db[k] = uint8_t(w >> (8 * (k & 3)));
+              }
+            }
+          }
+        }
+#endif
       } else {
         // large blocks: global -> global, each element's bytes fenced before the next reads them
         len = ~0u;
