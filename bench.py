@@ -64,6 +64,8 @@ def parse():
                    help="A/B: PBL_KERNEL_SINGLE / PBL_KERNEL_PIPE batch flags")
     p.add_argument("--launch-check", action="store_true",
                    help="launcher self-test without a GPU: N gloo ranks report in, rank 0 prints one JSON line")
+    p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                   help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo = CPU rehearsal)")
     return p.parse_args()
 
 
@@ -135,6 +137,74 @@ def alg_bytes(h: dict, nb: int, input_bytes: int) -> int:
     return input_bytes + 12 * nb + out
 
 
+def concat_step(dist, gathered, local_totals, rebase) -> None:
+    """The offset concat of one step: all-gather every rank's
+    4 totals {n_kv, key bytes, value bytes, restarts} and rebase this rank's
+    per-block bases by the exclusive prefix of the lower ranks."""
+    dist.all_gather_into_tensor(gathered, local_totals)
+    rebase(gathered)
+
+
+def plumbing(a, world, rank, dist) -> None:
+    """No GPU here (`--dist-backend gloo` rehearsal on CPU): the rank, timing
+    and offset-concat plumbing of main() on a small synthetic row batch.  The
+    decode itself needs the device, so each step restores the per-block bases a
+    decode would leave (block-relative exclusive scans of the blocks' restart
+    counts and lengths: any per-block aggregate exercises the rebase), then runs
+    concat_step -- the same all-gather + rebase as the GPU step, the rebase as a
+    CPU-tensor add of shard.exclusive_bases.  Rank 0 prints one JSON line with
+    the concat checked against every rank's totals."""
+    from pebble_amd.rowblk import gen_row_blocks
+    from pebble_amd.shard import exclusive_bases
+    nb = a.blocks or 64
+    buf, off, lens, n_kv = gen_row_blocks(a.seed + 7919 * rank, nb, a.block_size, a.restart_interval, a.key_len,
+                                          a.val_len, a.value_prefix, n_threads=4)
+    nres = np.array([int.from_bytes(buf[int(o) + int(l) - 4: int(o) + int(l)].tobytes(), "little")
+                     for o, l in zip(off, lens)], np.int64)
+    per = np.stack([nres, lens.astype(np.int64), lens.astype(np.int64) // 2, nres])  # [4, nb]
+    local = torch.from_numpy(np.concatenate([np.zeros((4, 1), np.int64), np.cumsum(per, 1)], 1))  # [4, nb+1]
+    totals = local[:, -1].contiguous()
+    bases = local.clone()
+    gathered = torch.zeros(world * 4, dtype=torch.int64)
+
+    def step():
+        bases.copy_(local)  # what the decode writes: this rank's own exclusive scan
+        if world > 1:
+            concat_step(dist, gathered, totals, lambda g: bases.add_(exclusive_bases(g, rank).view(4, 1)))
+
+    for _ in range(a.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        firsts = torch.zeros(world * 4, dtype=torch.int64)
+        dist.all_gather_into_tensor(firsts, bases[:, 0].contiguous())
+        tot = gathered.view(world, 4)
+        ok = all(torch.equal(firsts.view(world, 4)[r], tot[:r].sum(0)) for r in range(world))
+    else:
+        ok = True
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
+                          "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+                          "plumbing": True, "dist_backend": a.dist_backend, "concat_ok": bool(ok),
+                          "note": "no GPU: decode not run; rank, timing and offset-concat plumbing only",
+                          "config": {"workload": f"{nb} row blocks per rank (plumbing)",
+                                     "parallelism": f"shard{world}" + ("+offset_concat" if world > 1 else "")}}),
+              flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -149,10 +219,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    if not torch.cuda.is_available():
+        if world > 1:
+            import torch.distributed as dist  # noqa: F811
+            dist.init_process_group("gloo")
+        plumbing(a, world, rank, dist)
+        return
     if world > 1:
         import torch.distributed as dist  # noqa: F811
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -229,13 +308,21 @@ def main():
     out = DecodedBatch.allocate(nb, cap, dev)
     stream = torch.cuda.current_stream(dev)
     gathered = torch.zeros(world * 4, dtype=torch.int64, device=dev) if world > 1 else None
+    if world > 1 and a.dist_backend == "gloo":  # (gloo gathers host tensors)
+        gathered = gathered.cpu()
+
+    def concat():
+        # offset concat: all-gather per-rank totals (n_kv, key, val, restarts), rebase on device
+        tot = out.totals[:32].view(torch.int64)
+        if a.dist_backend == "gloo":
+            concat_step(dist, gathered, tot.cpu(), lambda g: offset_concat(out, g.to(dev), rank, stream))
+        else:
+            concat_step(dist, gathered, tot, lambda g: offset_concat(out, g, rank, stream))
 
     def step():
         decode_into(batch, out, stream)
         if world > 1:
-            # offset concat: all-gather per-rank totals (n_kv, key, val, restarts), rebase
-            dist.all_gather_into_tensor(gathered, out.totals[:32].view(torch.int64))
-            offset_concat(out, gathered, rank, stream)
+            concat()
 
     for _ in range(a.warmup):
         step()
@@ -254,8 +341,7 @@ def main():
         decode_into(batch, out, stream)
         ev[i][1].record(stream)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, out.totals[:32].view(torch.int64))
-            offset_concat(out, gathered, rank, stream)
+            concat()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -296,7 +382,8 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
         "config": {"workload": wl,
                    "blocks_per_gpu": nb, "input_bytes_per_gpu": input_bytes, "kvs_per_gpu": n_kv,
-                   "parallelism": f"shard{world}" + ("+rccl_offset_concat" if world > 1 else "")},
+                   "parallelism": f"shard{world}" + (f"+{'rccl' if a.dist_backend == 'nccl' else 'gloo'}_offset_concat"
+                                                      if world > 1 else "")},
         "roofline": {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "alg_bytes_per_launch": ab, "kernel_ms": round(kern_ms, 4),

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define PBL_ABI_VERSION 4
+#define PBL_ABI_VERSION 5
 
 /* ---- status codes (per block, and OR-ed as bit masks into totals) ---------- */
 enum {
@@ -332,6 +332,14 @@ typedef struct pbl_transforms {
   const uint8_t* prefix;         /* DEVICE bytes of the SyntheticPrefix (transforms.go:120-162) */
   const uint8_t* suffix;         /* DEVICE bytes of the SyntheticSuffix (transforms.go:101-118) */
   uint32_t prefix_len, suffix_len;
+  const pbl_block_batch* blocks; /* REQUIRED: the batch `in` was decoded from (host struct,
+                                    device arrays).  Row blocks are read by rowblk.Iter
+                                    with the prefix inside fullKey (rowblk_iter.go:259-263,
+                                    400): a key shorter than 8 B is re-read from its block
+                                    and decodes as a valid key when prefix ++ key is 8 B or
+                                    longer (:1168-1199), and Split runs on prefix ++ key
+                                    (:1183).  Colblk blocks follow their KeySeeker
+                                    (data_block.go:444-460; cockroachkvs.go:1073-1089).     */
 } pbl_transforms;
 
 /* Device scratch pbl_transform_batch needs in out->workspace. */
@@ -343,9 +351,12 @@ uint64_t pbl_transform_workspace_bytes(uint32_t n_blocks);
  * pbl_transform_workspace_bytes): every visible KV (HideObsoletePoints drops the
  * obsolete ones) keeps its order, flags, entry offset and value; its trailer
  * takes the synthetic sequence number (InternalKey.SetSeqNum); its user key
- * becomes prefix ++ key[:Split(key)] ++ suffix (suffix set) or prefix ++ key;
- * keys of PBL_KV_INVALID_KEY entries stay empty.  Restart words and statuses
- * are the input's.  Three stream-ordered launches (count, scan, scatter); on a
+ * becomes F[:Split(F)] ++ suffix (suffix set) or F, F = prefix ++ key (row
+ * blocks; colblk: prefix ++ key[:Split(key)] ++ suffix); keys of entries that
+ * stay PBL_KV_INVALID_KEY are empty and keep the Invalid trailer.  Restart words
+ * are the input's; statuses too, except a row block whose transformed iteration
+ * would panic (a key made valid by the prefix, kind SET, empty value, value
+ * prefix on): PBL_CORRUPT_BOUNDS.  A block whose decode failed stays failed.  Three stream-ordered launches (count, scan, scatter); on a
  * capacity overflow every decodable block reports PBL_OVERFLOW and only sizes
  * are written.  Replaces the iteration-time transforms of rowblk.Iter
  * (rowblk_iter.go:400,487-517,1168-1187) and colblk.DataBlockIter

@@ -57,6 +57,21 @@ typedef struct orc_batch_out {
   uint32_t status_mask, n_bad_blocks;
 } orc_batch_out;
 
+/* blockiter.Transforms (sstable/blockiter/transforms.go:20-56) for the row
+ * restatement; split is PBL_SPLIT_* (0 default, 1 testkeys, 2 cockroachkvs). */
+typedef struct orc_transforms {
+  uint64_t seq;
+  int hide;
+  int split;
+  const uint8_t* prefix;
+  uint64_t prefix_len;
+  const uint8_t* suffix;
+  uint64_t suffix_len;
+} orc_transforms;
+
+uint64_t orc_split(const uint8_t* k, uint64_t n, int split);
+int orc_rowblk_decode_tf(const uint8_t* blk, uint64_t len, uint32_t flags, const orc_transforms* t,
+                         orc_block_out* o);
 int orc_decode_varint(const uint8_t* p, const uint8_t* end, uint32_t* v);
 int orc_rowblk_decode(const uint8_t* blk, uint64_t len, uint32_t flags, orc_block_out* o);
 uint64_t orc_rowblk_scan_checksum(const uint8_t* blk, uint64_t len, uint32_t flags, uint64_t* n_kv);

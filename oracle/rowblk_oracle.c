@@ -57,9 +57,43 @@ int orc_decode_varint(const uint8_t* p, const uint8_t* end, uint32_t* v) {
 }
 
 
-/* Sequential decode of one row block exactly as rowblk.Iter First/Next sees it. */
-int orc_rowblk_decode(const uint8_t* blk, uint64_t len, uint32_t flags, orc_block_out* o) {
+/* Comparer.Split for the synthetic-suffix transform (PBL_SPLIT_*):
+ * base.DefaultSplit (whole key), testkeys (before the last '@',
+ * internal/testkeys/testkeys.go:144-150), cockroachkvs.Split (last byte = version
+ * length, cockroachkvs/cockroachkvs.go:298-309; a length past the key is taken as
+ * 0 where Go would panic). */
+uint64_t orc_split(const uint8_t* k, uint64_t n, int split) {
+  if (split == 1) {
+    for (uint64_t i = n; i > 0; i--)
+      if (k[i - 1] == '@') return i - 1;
+    return n;
+  }
+  if (split == 2) {
+    if (n == 0) return 0;
+    uint64_t v = k[n - 1];
+    return v <= n ? n - v : 0;
+  }
+  return n;
+}
+
+/*
+ * Sequential decode of one row block exactly as rowblk.Iter First/Next sees it,
+ * under blockiter.Transforms `t` (NULL = NoTransforms):
+ *   Init :259-263           fullKey starts as the synthetic prefix
+ *   readEntry :400-403      shared += PrefixLen(); fullKey = fullKey[:shared] ++ unshared
+ *   Next :1168-1191         the internal key is decoded from prefix ++ key: the
+ *                           len >= 8 test, the trailer and the obsolete bit all see
+ *                           the prefixed key; hidden points are skipped before the
+ *                           value is looked at; SyntheticSeqNum via SetSeqNum; the
+ *                           synthetic suffix replaces key[Split(prefix ++ key):]
+ *   Next :1192-1199         value classification by the (possibly new) kind
+ * RawIter (FLAG_RAW_KEYS) takes no transforms.
+ */
+static int rowblk_decode_impl(const uint8_t* blk, uint64_t len, uint32_t flags, const orc_transforms* t,
+                              orc_block_out* o) {
   o->n_kv = o->key_bytes = o->val_bytes = o->n_restarts = 0;
+  if (flags & FLAG_RAW_KEYS) t = NULL;
+  const uint64_t P = t ? t->prefix_len : 0;
   if (len < 4) return CORRUPT_BOUNDS;
   const uint8_t* end = blk + len;
   int32_t num_restarts = (int32_t)le32(blk + len - 4);       /* :248 */
@@ -74,7 +108,7 @@ int orc_rowblk_decode(const uint8_t* blk, uint64_t len, uint32_t flags, orc_bloc
     if (!n1) return CORRUPT_BOUNDS;
     int n2 = orc_decode_varint(blk + 1 + n1, end, &vl);
     if (!n2) return CORRUPT_BOUNDS;
-    if (unshared < 8) return CORRUPT_FIRST_KEY;               /* :471-476 */
+    if (unshared < 8) return CORRUPT_FIRST_KEY;               /* :471-476 (before the prefix) */
   }
   const uint8_t* rtab = blk + restarts;
 
@@ -85,7 +119,7 @@ int orc_rowblk_decode(const uint8_t* blk, uint64_t len, uint32_t flags, orc_bloc
   for (int pass = 0; pass < 2 && status == OK; pass++) {
     int write = pass == 1;
     uint64_t nkv = 0, kb = 0, vb = 0;
-    full_len = 0;
+    full_len = P;
     int64_t offset = 0;
     uint32_t ri = 0; /* restart cursor for the restart flag */
     while (offset >= 0 && offset < restarts) {                /* Valid :1666 */
@@ -101,9 +135,9 @@ int orc_rowblk_decode(const uint8_t* blk, uint64_t len, uint32_t flags, orc_bloc
       if ((uint64_t)(end - kp) < (uint64_t)unshared) { status = CORRUPT_BOUNDS; break; }
       const uint8_t* vp = kp + unshared;
       if ((uint64_t)(end - vp) < (uint64_t)vlen) { status = CORRUPT_BOUNDS; break; }
-      /* fullKey = append(fullKey[:shared], unshared...) :403 */
-      if ((uint64_t)shared > full_len) { status = CORRUPT_BOUNDS; break; }
-      uint64_t klen = (uint64_t)shared + unshared;
+      /* fullKey = append(fullKey[:shared + P], unshared...) :400-403 */
+      if ((uint64_t)shared + P > full_len) { status = CORRUPT_BOUNDS; break; }
+      uint64_t klen = P + (uint64_t)shared + unshared;
       if (klen > full_cap) {
         uint64_t nc = full_cap ? full_cap : 64;
         while (nc < klen) nc *= 2;
@@ -111,10 +145,13 @@ int orc_rowblk_decode(const uint8_t* blk, uint64_t len, uint32_t flags, orc_bloc
         if (!nf) { status = CORRUPT_BOUNDS; break; }
         full = nf; full_cap = nc;
       }
-      memcpy(full + shared, kp, unshared);
+      if (P) memcpy(full, t->prefix, P); /* full[:P] is always the prefix (Init :259-263) */
+      memcpy(full + P + shared, kp, unshared);
       full_len = klen;
-      /* decodeInternalKey :487-504 */
-      uint64_t trailer, ukl;
+      const int64_t this_off = offset;
+      offset = (int64_t)(vp - blk) + vlen;                     /* nextOffset :415 */
+      /* decodeInternalKey :487-504 on prefix ++ key */
+      uint64_t trailer, ukl, kout_len = 0;
       uint8_t fl = 0;
       if (flags & FLAG_RAW_KEYS) {                             /* RawIter.readEntry :1784-1794 */
         trailer = 0;
@@ -124,10 +161,18 @@ int orc_rowblk_decode(const uint8_t* blk, uint64_t len, uint32_t flags, orc_bloc
         if (raw & TRAILER_OBSOLETE_BIT) fl |= KV_OBSOLETE;
         trailer = raw & TRAILER_OBSOLETE_MASK;
         ukl = klen - 8;
+        if (t && t->hide && (raw & TRAILER_OBSOLETE_BIT)) continue;   /* hiddenPoint: goto start */
+        if (t && t->seq) trailer = t->seq << 8 | (trailer & 0xff);   /* SetSeqNum */
       } else {
         trailer = KIND_INVALID;
         ukl = 0;
         fl |= KV_INVALID_KEY;
+      }
+      uint64_t split_at = ukl; /* user key = full[:split_at] ++ (suffix | full[split_at:ukl]) */
+      kout_len = ukl;
+      if (t && t->suffix_len && klen >= 8) {
+        split_at = orc_split(full, ukl, t->split);
+        kout_len = split_at + t->suffix_len;
       }
       /* value classification :1192-1199 */
       const uint8_t* v = vp;
@@ -144,24 +189,27 @@ int orc_rowblk_decode(const uint8_t* blk, uint64_t len, uint32_t flags, orc_bloc
         }
       }
       /* restart flag: entry offset equals a (masked) restart offset */
-      while (ri < (uint32_t)num_restarts && (int64_t)(le32(rtab + 4 * ri) & 0x7fffffffu) < offset) ri++;
-      if (ri < (uint32_t)num_restarts && (int64_t)(le32(rtab + 4 * ri) & 0x7fffffffu) == offset) {
+      while (ri < (uint32_t)num_restarts && (int64_t)(le32(rtab + 4 * ri) & 0x7fffffffu) < this_off) ri++;
+      if (ri < (uint32_t)num_restarts && (int64_t)(le32(rtab + 4 * ri) & 0x7fffffffu) == this_off) {
         fl |= KV_RESTART;
         if (le32(rtab + 4 * ri) & 0x80000000u) fl |= KV_RESTART_SAMEPFX;
       }
       if (write) {
         if (o->trailer) o->trailer[nkv] = trailer;
         if (o->kv_flags) o->kv_flags[nkv] = fl;
-        if (o->entry_off) o->entry_off[nkv] = (uint32_t)offset;
+        if (o->entry_off) o->entry_off[nkv] = (uint32_t)this_off;
         if (o->key_off) o->key_off[nkv] = (uint32_t)kb;
         if (o->val_off) o->val_off[nkv] = (uint32_t)vb;
-        if (o->keys && ukl) memcpy(o->keys + kb, full, ukl);
+        if (o->keys && split_at) memcpy(o->keys + kb, full, split_at);
+        if (o->keys && kout_len > split_at) {
+          if (t && t->suffix_len && klen >= 8) memcpy(o->keys + kb + split_at, t->suffix, t->suffix_len);
+          else memcpy(o->keys + kb + split_at, full + split_at, kout_len - split_at);
+        }
         if (o->vals && vl) memcpy(o->vals + vb, v, vl);
       }
       nkv++;
-      kb += ukl;
+      kb += kout_len;
       vb += vl;
-      offset = (int64_t)(vp - blk) + vlen;                     /* nextOffset :415 */
     }
     if (status != OK) break;
     if (write) {
@@ -178,6 +226,15 @@ int orc_rowblk_decode(const uint8_t* blk, uint64_t len, uint32_t flags, orc_bloc
   free(full);
   if (status != OK) o->n_kv = o->key_bytes = o->val_bytes = o->n_restarts = 0;
   return status;
+}
+
+int orc_rowblk_decode(const uint8_t* blk, uint64_t len, uint32_t flags, orc_block_out* o) {
+  return rowblk_decode_impl(blk, len, flags, NULL, o);
+}
+
+int orc_rowblk_decode_tf(const uint8_t* blk, uint64_t len, uint32_t flags, const orc_transforms* t,
+                         orc_block_out* o) {
+  return rowblk_decode_impl(blk, len, flags, t, o);
 }
 
 /*

@@ -40,7 +40,7 @@ PBL_TABLE_PEBBLEV1 = 3  # .. PBL_TABLE_PEBBLEV8 = 10
 PBL_CHECKSUM_NONE, PBL_CHECKSUM_CRC32C, PBL_CHECKSUM_XXHASH, PBL_CHECKSUM_XXHASH64 = 0, 1, 2, 3
 PBL_COMPRESSION_NONE, PBL_COMPRESSION_SNAPPY, PBL_COMPRESSION_ZSTD, PBL_COMPRESSION_MINLZ = 0, 1, 7, 8
 
-ABI_VERSION = 4  # include/pebble_amd.h PBL_ABI_VERSION
+ABI_VERSION = 5  # include/pebble_amd.h PBL_ABI_VERSION
 
 PBL_FMT_ROW = 0
 PBL_FMT_COL_DEFAULT = 1
@@ -141,6 +141,7 @@ class TransformsC(ctypes.Structure):
         ("synthetic_seq_num", ctypes.c_uint64), ("hide_obsolete_points", ctypes.c_uint32),
         ("split", ctypes.c_uint32), ("prefix", _vp), ("suffix", _vp),
         ("prefix_len", ctypes.c_uint32), ("suffix_len", ctypes.c_uint32),
+        ("blocks", ctypes.POINTER(BlockBatchC)),
     ]
 
 

@@ -134,6 +134,7 @@ class DecodedBatch:
     workspace: torch.Tensor
     cap: Capacity
     _host_totals: Optional[N.TotalsC] = field(default=None, repr=False)
+    source: Optional[BlockBatch] = field(default=None, repr=False)  # the batch it was decoded from
 
     @classmethod
     def allocate(cls, n_blocks: int, cap: Capacity, device, entry_off: bool = True,
@@ -241,6 +242,7 @@ def decode(batch: BlockBatch, cap: Optional[Capacity] = None, stream=None, entry
     with torch.cuda.stream(st):
         out = DecodedBatch.allocate(batch.n_blocks, cap, batch.device, entry_off, restarts)
     decode_into(batch, out, st)
+    out.source = batch
     st.synchronize()
     t = out.read_totals()
     if t.status_mask & (1 << N.PBL_OVERFLOW):
@@ -249,6 +251,7 @@ def decode(batch: BlockBatch, cap: Optional[Capacity] = None, stream=None, entry
         with torch.cuda.stream(st):
             out = DecodedBatch.allocate(batch.n_blocks, cap, batch.device, entry_off, restarts)
         decode_into(batch, out, st)
+        out.source = batch
         st.synchronize()
         out.read_totals()
     return out

@@ -8,6 +8,7 @@ from __future__ import annotations
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
@@ -18,27 +19,51 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-pthread"]
 
 
-def _stale() -> bool:
-    if not os.path.exists(OUT):
-        return True
-    t = os.path.getmtime(OUT)
-    for f in SOURCES + HEADERS:
-        if os.path.getmtime(os.path.join(CSRC, f)) > t:
-            return True
-    return False
-
-
+OBJ = os.path.join(HERE, ".obj")  # per-source objects (git- and gpurun-ignored)
 DIAG_OUT = os.path.join(HERE, "libpebble_amd_diag.so")
 
 
-def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str:
-    """Build libpebble_amd.so; `diag` builds the phase-stamp diagnostic variant
-    (libpebble_amd_diag.so, -DPBL_STAMPS) used only by scripts/phase_stamps.py."""
+def _newer(a: str, b: str) -> bool:
+    return not os.path.exists(b) or os.path.getmtime(a) > os.path.getmtime(b)
+
+
+def _stale(out: str = OUT) -> bool:
+    if not os.path.exists(out):
+        return True
+    return any(_newer(os.path.join(CSRC, f), out) for f in SOURCES + HEADERS)
+
+
+def build(force: bool = False, verbose: bool = False, diag: bool = False, jobs: int = 8) -> str:
+    """Build libpebble_amd.so: each source compiled to its own object (in
+    parallel; only sources newer than their object, or any header newer), then
+    one link.  `diag` builds the phase-stamp diagnostic variant
+    (libpebble_amd_diag.so, -DPBL_STAMPS) used only by scripts/pipe_stamps.py."""
     out = DIAG_OUT if diag else OUT
-    if not force and not diag and not _stale():
-        return OUT
-    cmd = [HIPCC, *FLAGS, *(["-DPBL_STAMPS"] if diag else []), *[os.path.join(CSRC, s) for s in SOURCES],
-           "-o", out + ".tmp"]
+    if not force and not _stale(out):
+        return out
+    tag = "diag" if diag else "rel"
+    os.makedirs(OBJ, exist_ok=True)
+    hdr_t = max(os.path.getmtime(os.path.join(CSRC, h)) for h in HEADERS)
+    extra = ["-DPBL_STAMPS"] if diag else []
+    cflags = [f for f in FLAGS if f != "-shared"]
+    jobs_todo, objs = [], []
+    for src in SOURCES:
+        sp = os.path.join(CSRC, src)
+        obj = os.path.join(OBJ, f"{os.path.splitext(src)[0]}.{tag}.o")
+        objs.append(obj)
+        if force or _newer(sp, obj) or hdr_t > os.path.getmtime(obj):
+            jobs_todo.append(([HIPCC, *cflags, *extra, "-c", sp, "-o", obj + ".tmp"], obj))
+
+    def compile_one(job):
+        cmd, obj = job
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True, cwd=CSRC)
+        os.replace(obj + ".tmp", obj)
+
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        list(ex.map(compile_one, jobs_todo))
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-pthread", *objs, "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)

@@ -351,6 +351,8 @@ __device__ inline void lb_finish(uint64_t* st, uint32_t n_blocks, uint32_t v, co
   bool timed_out = false;
   int64_t top = int64_t(v) - 1, wait_idx = -1;
   bool done = v == 0 || lb_consume(P, n_blocks, first_win, acc, &top, &wait_idx, &spins, &timed_out);
+  // a lane polling a wide record may have timed out on its own: leave together
+  if (__ballot(timed_out)) timed_out = true;
   while (!done && !timed_out) {
     if (wait_idx >= 0) {
       // Poll the missing predecessor from ONE lane (a whole-window re-read per

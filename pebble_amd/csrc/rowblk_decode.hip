@@ -1271,7 +1271,11 @@ size_t pbl_struct_layout(uint64_t* out, size_t cap) {
       PBL_OFF(pbl_decode_out, blk_val_base), PBL_OFF(pbl_decode_out, blk_rst_base),
       PBL_OFF(pbl_decode_out, blk_status), PBL_OFF(pbl_decode_out, totals), PBL_OFF(pbl_decode_out, kv_cap),
       PBL_OFF(pbl_decode_out, key_cap), PBL_OFF(pbl_decode_out, val_cap), PBL_OFF(pbl_decode_out, rst_cap),
-      PBL_OFF(pbl_decode_out, workspace), PBL_OFF(pbl_decode_out, workspace_bytes)};
+      PBL_OFF(pbl_decode_out, workspace), PBL_OFF(pbl_decode_out, workspace_bytes),
+      sizeof(pbl_transforms), PBL_OFF(pbl_transforms, synthetic_seq_num),
+      PBL_OFF(pbl_transforms, hide_obsolete_points), PBL_OFF(pbl_transforms, split), PBL_OFF(pbl_transforms, prefix),
+      PBL_OFF(pbl_transforms, suffix), PBL_OFF(pbl_transforms, prefix_len), PBL_OFF(pbl_transforms, suffix_len),
+      PBL_OFF(pbl_transforms, blocks)};
 #undef PBL_OFF
   const size_t n = sizeof(v) / sizeof(v[0]);
   for (size_t i = 0; i < n && i < cap && out; i++) out[i] = v[i];

@@ -27,47 +27,172 @@ namespace pbl {
 namespace tf {
 
 constexpr int kTfWs = 64;  // workspace header: overflow flag
+constexpr uint64_t kTfMask = ((1ull << 56) - 1) << 8 | 191u;  // TrailerObsoleteMask (rowblk_writer.go:30-42)
+constexpr uint64_t kTfInvalid = 191u;                          // InternalKeyKindInvalid
 
 struct TfArgs {
   pbl_decode_out in, out;
   pbl_transforms t;
+  pbl_block_batch src;  // the batch `in` was decoded from (row blocks: raw short keys)
   uint32_t n_blocks;
 };
 
-// Comparer.Split of a user key (transforms.go:105-118 needs it for the suffix).
-__device__ inline uint32_t split_len(gptr<const uint8_t> k, uint32_t n, uint32_t split) {
+// Comparer.Split over F = pfx[0:fp] ++ key[0:kn] (transforms.go:105-118 needs it
+// for the suffix; a row key's Split sees the synthetic prefix too,
+// rowblk_iter.go:400,1183).
+struct FKey {
+  gptr<const uint8_t> pfx, key;
+  uint32_t fp, kn;
+  __device__ uint8_t at(uint32_t i) const { return i < fp ? pfx[i] : key[i - fp]; }
+  __device__ uint32_t len() const { return fp + kn; }
+};
+__device__ inline uint32_t split_len(const FKey& k, uint32_t split) {
+  const uint32_t n = k.len();
   if (split == PBL_SPLIT_TESTKEYS) {  // testkeys.Comparer: before the last '@' (internal/testkeys/testkeys.go:144-150)
     for (uint32_t i = n; i > 0; i--)
-      if (k[i - 1] == '@') return i - 1;
+      if (k.at(i - 1) == '@') return i - 1;
     return n;
   }
   if (split == PBL_SPLIT_CRDB) {  // cockroachkvs.Split: the last byte is the version length (+1), 0 if none
     if (n == 0) return 0;
-    const uint32_t v = k[n - 1];
+    const uint32_t v = k.at(n - 1);
     return v <= n ? n - v : 0;
   }
   return n;  // base.DefaultSplit: the whole key
 }
 
+// uint32 varint of rowblk_iter.go:2020-2038 (5th byte << 28); returns bytes read
+__device__ inline uint32_t tf_varint(gptr<const uint8_t> p, uint32_t* v) {
+  uint32_t r = 0;
+  for (uint32_t i = 0; i < 5; i++) {
+    const uint32_t b = p[i];
+    if (i == 4) { *v = r | (b << 28); return 5; }
+    r |= (b & 0x7fu) << (7 * i);
+    if (b < 128) { *v = r; return i + 1; }
+  }
+  return 5;
+}
+
+// The raw internal key (< 8 bytes, byte i at bits 8i) of row entry j, an entry
+// the decode left PBL_KV_INVALID_KEY: its bytes past `shared` from the block,
+// the shared ones from the previous entry -- an invalid one again (its header
+// re-read), or a decoded one, whose raw key is user key ++ LE64(trailer | the
+// obsolete bit).  Entries are in block order and a block's first entry has
+// shared 0, so the walk ends inside the block.
+__device__ inline uint64_t raw_short_key(const TfArgs& A, gptr<const uint8_t> blk, uint64_t kv0, uint64_t kb_in,
+                                         uint32_t b, uint32_t j, uint32_t* kl_out) {
+  const pbl_decode_out& I = A.in;
+  uint32_t s, u, vl;
+  uint32_t e = to_glb(I.entry_off)[kv0 + j];
+  uint32_t h = tf_varint(blk + e, &s);
+  h += tf_varint(blk + e + h, &u);
+  h += tf_varint(blk + e + h, &vl);
+  const uint32_t kl = s + u;
+  *kl_out = kl;
+  uint64_t raw = 0;
+  uint32_t need = kl, k = j, ks = s, kkl = kl;
+  for (;;) {
+    for (uint32_t i = ks; i < need && i < kkl; i++) raw |= uint64_t(blk[e + h + (i - ks)]) << (8 * i);
+    need = need < ks ? need : ks;
+    if (need == 0 || k == 0) break;
+    k--;
+    const uint8_t fk = to_glb(I.kv_flags)[kv0 + k];
+    if (!(fk & PBL_KV_INVALID_KEY)) {
+      const uint64_t o = kv0 + b + k;
+      const uint32_t ko = to_glb(I.key_off)[o], ukl = to_glb(I.key_off)[o + 1] - ko;
+      const uint64_t tk = to_glb(I.trailer)[kv0 + k] | ((fk & PBL_KV_OBSOLETE) ? 64u : 0u);
+      for (uint32_t i = 0; i < need; i++) {
+        const uint64_t x = i < ukl ? uint64_t(to_glb(I.key_bytes)[kb_in + ko + i]) : (tk >> (8 * (i - ukl))) & 0xffu;
+        raw |= x << (8 * i);
+      }
+      break;
+    }
+    e = to_glb(I.entry_off)[kv0 + k];
+    h = tf_varint(blk + e, &ks);
+    h += tf_varint(blk + e + h, &u);
+    h += tf_varint(blk + e + h, &vl);
+    kkl = ks + u;
+  }
+  return raw;
+}
+
 struct KvView {
-  bool vis, valid;
-  uint32_t ko, klen, vo, vlen, p, nk;
+  bool vis, valid, corrupt;
+  uint8_t fl;
+  uint64_t tr;
+  FKey F;        // the user key before the suffix step
+  uint32_t p;    // Split point in F (= F.len() without a suffix)
+  uint32_t vo, vlen, nk;
 };
 
-__device__ inline KvView kv_view(const TfArgs& A, uint32_t b, uint64_t kv0, uint64_t kb_in, uint32_t j) {
+__device__ inline uint32_t block_format(const TfArgs& A, uint32_t b) {
+  return A.src.block_format ? to_glb(A.src.block_format)[b] : A.src.format;
+}
+
+__device__ inline KvView kv_view(const TfArgs& A, uint32_t b, uint64_t kv0, uint64_t kb_in, uint64_t vb_in,
+                                 uint32_t j) {
   const pbl_decode_out& I = A.in;
+  const pbl_transforms& T = A.t;
   KvView v;
-  const uint8_t fl = I.kv_flags ? to_glb(I.kv_flags)[kv0 + j] : uint8_t(0);
-  v.vis = !(A.t.hide_obsolete_points && (fl & PBL_KV_OBSOLETE));
-  v.valid = !(fl & PBL_KV_INVALID_KEY);
+  const bool row = block_format(A, b) == PBL_FMT_ROW && !(A.src.flags & PBL_ROW_RAW_KEYS);
+  v.fl = I.kv_flags ? to_glb(I.kv_flags)[kv0 + j] : uint8_t(0);
+  v.tr = to_glb(I.trailer)[kv0 + j];
+  v.corrupt = false;
+  v.vis = !(T.hide_obsolete_points && (v.fl & PBL_KV_OBSOLETE));
+  v.valid = !(v.fl & PBL_KV_INVALID_KEY);
   const uint64_t o = kv0 + b + j;
-  v.ko = to_glb(I.key_off)[o];
-  v.klen = to_glb(I.key_off)[o + 1] - v.ko;
+  const uint32_t ko = to_glb(I.key_off)[o];
   v.vo = to_glb(I.val_off)[o];
   v.vlen = to_glb(I.val_off)[o + 1] - v.vo;
-  v.p = v.klen;
-  if (v.valid && A.t.suffix_len) v.p = split_len(to_glb(I.key_bytes) + kb_in + v.ko, v.klen, A.t.split);
-  v.nk = v.valid ? A.t.prefix_len + v.p + (A.t.suffix_len ? A.t.suffix_len : v.klen - v.p) : 0u;
+  v.F = FKey{to_glb(T.prefix), to_glb(I.key_bytes) + kb_in + ko, T.prefix_len, to_glb(I.key_off)[o + 1] - ko};
+  if (row && !v.valid && T.prefix_len) {
+    // rowblk_iter.go:400,1168-1199: the prefix is part of the key the trailer
+    // is decoded from, so a raw key shorter than 8 B can become a valid one
+    const gptr<const uint8_t> blk = to_glb(A.src.blocks) + to_glb(A.src.block_off)[b];
+    uint32_t kl;
+    const uint64_t rk = raw_short_key(A, blk, kv0, kb_in, b, j, &kl);
+    if (T.prefix_len + kl >= 8) {
+      const uint32_t ukl = T.prefix_len + kl - 8;  // the user key lies inside the prefix
+      uint64_t raw = rk << (8 * (8 - kl));
+      for (uint32_t i = 0; i < 8 - kl; i++) raw |= uint64_t(to_glb(T.prefix)[ukl + i]) << (8 * i);
+      v.valid = true;
+      v.fl = uint8_t((v.fl & ~PBL_KV_INVALID_KEY) | ((raw & 64u) ? PBL_KV_OBSOLETE : 0u));
+      v.vis = !(T.hide_obsolete_points && (raw & 64u));
+      v.tr = raw & kTfMask;
+      v.F.fp = ukl;
+      v.F.kn = 0;
+      if ((A.src.flags & PBL_ROW_VALUE_PREFIX) && (v.tr & 0xffu) == 1u) {  // kind SET: the value prefix
+        if (v.vlen == 0) {
+          v.corrupt = v.vis;  // Go: i.val[0] panics (only reached for a visible point)
+        } else {
+          const uint32_t pre = to_glb(I.val_bytes)[vb_in + v.vo];
+          if ((pre & 0xC0u) == 0 || (A.src.flags & PBL_ROW_NO_VALUER)) { v.vo++; v.vlen--; }
+          else v.fl |= (pre & 0xC0u) == 0x80u ? PBL_KV_VALBLK_HANDLE : PBL_KV_BLOB_HANDLE;
+        }
+      }
+    }
+  }
+  if (!v.valid) {
+    v.nk = 0;
+    v.p = 0;
+    return v;  // trailer stays InternalKeyKindInvalid (no SetSeqNum: rowblk_iter.go:1189-1191)
+  }
+  if (T.synthetic_seq_num) v.tr = (T.synthetic_seq_num << 8) | (v.tr & 0xffu);  // InternalKey.SetSeqNum
+  const uint32_t flen = v.F.len();
+  if (T.suffix_len) {
+    if (row) {
+      v.p = split_len(v.F, T.split);  // Split(prefix ++ key)
+    } else {
+      // colblk: the KeySeeker keeps the schema's prefix (data_block.go:444-460,
+      // cockroachkvs.go:1073-1089) = Split of the stored key, after the prefix
+      const FKey K{v.F.pfx, v.F.key, 0, v.F.kn};
+      v.p = T.prefix_len + split_len(K, T.split);
+    }
+    v.nk = v.p + T.suffix_len;
+  } else {
+    v.p = flen;
+    v.nk = flen;
+  }
   return v;
 }
 
@@ -77,11 +202,13 @@ __global__ void __launch_bounds__(kTPB) tf_count_kernel(TfArgs A) {
   const uint32_t wpb = kTPB / kWave;
   for (uint32_t b = blockIdx.x * wpb + wave_id(); b < A.n_blocks; b += gridDim.x * wpb) {
     uint32_t c = 0, kb = 0, vb = 0;
+    bool bad = false;
     if (to_glb(A.in.blk_status)[b] == PBL_OK) {
       const uint64_t kv0 = to_glb(A.in.blk_kv_base)[b], n = to_glb(A.in.blk_kv_base)[b + 1] - kv0;
-      const uint64_t kb_in = to_glb(A.in.blk_key_base)[b];
+      const uint64_t kb_in = to_glb(A.in.blk_key_base)[b], vb_in = to_glb(A.in.blk_val_base)[b];
       for (uint32_t j = lane; j < n; j += kWave) {
-        const KvView v = kv_view(A, b, kv0, kb_in, j);
+        const KvView v = kv_view(A, b, kv0, kb_in, vb_in, j);
+        bad = bad || v.corrupt;
         if (v.vis) {
           c++;
           kb += v.nk;
@@ -91,11 +218,13 @@ __global__ void __launch_bounds__(kTPB) tf_count_kernel(TfArgs A) {
       c = wave_sum(c);
       kb = wave_sum(kb);
       vb = wave_sum(vb);
+      bad = __ballot(bad) != 0;
     }
     if (lane == 0) {
-      cnt[3 * uint64_t(b)] = c;
-      cnt[3 * uint64_t(b) + 1] = kb;
-      cnt[3 * uint64_t(b) + 2] = vb;
+      cnt[4 * uint64_t(b)] = bad ? 0u : c;
+      cnt[4 * uint64_t(b) + 1] = bad ? 0u : kb;
+      cnt[4 * uint64_t(b) + 2] = bad ? 0u : vb;
+      cnt[4 * uint64_t(b) + 3] = bad ? 1u : 0u;
     }
   }
 }
@@ -103,15 +232,21 @@ __global__ void __launch_bounds__(kTPB) tf_count_kernel(TfArgs A) {
 // One workgroup of kTPB threads; thread t scans a contiguous chunk of blocks.
 __global__ void __launch_bounds__(kTPB) tf_scan_kernel(TfArgs A) {
   __shared__ uint64_t part[3][kTPB];
+  __shared__ uint32_t n_new_bad;
   const uint32_t* cnt = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(A.out.workspace) + kTfWs);
   uint32_t* flag = reinterpret_cast<uint32_t*>(A.out.workspace);
   const uint32_t nb = A.n_blocks, t = threadIdx.x;
   const uint32_t chunk = (nb + kTPB - 1) / kTPB, b0 = min(nb, t * chunk), b1 = min(nb, b0 + chunk);
   uint64_t s[3] = {0, 0, 0};
-  for (uint32_t b = b0; b < b1; b++)
-    for (int q = 0; q < 3; q++) s[q] += cnt[3 * uint64_t(b) + q];
+  uint32_t nbad = 0;
+  if (t == 0) n_new_bad = 0;
+  for (uint32_t b = b0; b < b1; b++) {
+    for (int q = 0; q < 3; q++) s[q] += cnt[4 * uint64_t(b) + q];
+    nbad += cnt[4 * uint64_t(b) + 3];
+  }
   for (int q = 0; q < 3; q++) part[q][t] = s[q];
   __syncthreads();
+  if (nbad) atomicAdd(&n_new_bad, nbad);
   if (t < 3) {  // serial scan of the kTPB chunk sums (one lane per component)
     uint64_t acc = 0;
     for (uint32_t i = 0; i < kTPB; i++) {
@@ -129,7 +264,7 @@ __global__ void __launch_bounds__(kTPB) tf_scan_kernel(TfArgs A) {
     to_glb(O.blk_key_base)[b] = e[1];
     to_glb(O.blk_val_base)[b] = e[2];
     if (O.blk_rst_base) to_glb(O.blk_rst_base)[b] = to_glb(I.blk_rst_base)[b];
-    for (int q = 0; q < 3; q++) e[q] += cnt[3 * uint64_t(b) + q];
+    for (int q = 0; q < 3; q++) e[q] += cnt[4 * uint64_t(b) + q];
   }
   if (t == kTPB - 1) {
     const uint64_t nr = to_glb(I.blk_rst_base)[nb];
@@ -144,6 +279,10 @@ __global__ void __launch_bounds__(kTPB) tf_scan_kernel(TfArgs A) {
     to.val_bytes = e[2];
     to.n_restarts = nr;
     if (over) to.status_mask |= 1u << PBL_OVERFLOW;
+    if (n_new_bad) {  // row blocks whose transformed iteration would panic
+      to.status_mask |= 1u << PBL_CORRUPT_BOUNDS;
+      to.n_bad_blocks += n_new_bad;
+    }
     *O.totals = to;
     *to_glb(flag) = over ? 1u : 0u;
   }
@@ -152,10 +291,12 @@ __global__ void __launch_bounds__(kTPB) tf_scan_kernel(TfArgs A) {
   const bool over = *to_glb(flag) != 0;
   for (uint32_t b = b0; b < b1; b++) {
     uint32_t st = to_glb(I.blk_status)[b];
+    if (st == PBL_OK && cnt[4 * uint64_t(b) + 3]) st = PBL_CORRUPT_BOUNDS;
     if (over && st == PBL_OK) st = PBL_OVERFLOW;
     to_glb(O.blk_status)[b] = st;
   }
   if (over && t == 0) to_glb(O.totals)->n_bad_blocks = nb;  // (every block is now OVERFLOW or bad)
+  (void)n_new_bad;
 }
 
 __global__ void __launch_bounds__(kTPB) tf_scatter_kernel(TfArgs A) {
@@ -164,10 +305,10 @@ __global__ void __launch_bounds__(kTPB) tf_scatter_kernel(TfArgs A) {
   const pbl_decode_out& O = A.out;
   const uint32_t lane = lane_id();
   const uint32_t wpb = kTPB / kWave;
-  const gptr<const uint8_t> pfx = to_glb(A.t.prefix), sfx = to_glb(A.t.suffix);
+  const gptr<const uint8_t> sfx = to_glb(A.t.suffix);
   for (uint32_t b = blockIdx.x * wpb + wave_id(); b < A.n_blocks; b += gridDim.x * wpb) {
     const uint64_t okv = to_glb(O.blk_kv_base)[b], okb = to_glb(O.blk_key_base)[b], ovb = to_glb(O.blk_val_base)[b];
-    if (to_glb(I.blk_status)[b] != PBL_OK) {
+    if (to_glb(O.blk_status)[b] != PBL_OK) {
       if (lane == 0) {
         to_glb(O.key_off)[okv + b] = 0;
         to_glb(O.val_off)[okv + b] = 0;
@@ -181,7 +322,7 @@ __global__ void __launch_bounds__(kTPB) tf_scatter_kernel(TfArgs A) {
       const uint32_t j = uint32_t(j0) + lane;
       const bool act = j < n;
       KvView v{};
-      if (act) v = kv_view(A, b, kv0, kb_in, j);
+      if (act) v = kv_view(A, b, kv0, kb_in, vb_in, j);
       const bool vis = act && v.vis;
       const uint64_t vm = __ballot(vis);
       const uint32_t rank = __builtin_popcountll(vm & ((1ull << lane) - 1));
@@ -189,24 +330,20 @@ __global__ void __launch_bounds__(kTPB) tf_scatter_kernel(TfArgs A) {
       const uint32_t ko = kcur + kx - (vis ? v.nk : 0u), vo = vcur + vx - (vis ? v.vlen : 0u);
       if (vis) {
         const uint64_t k = okv + jo + rank;
-        uint64_t tr = to_glb(I.trailer)[kv0 + j];
-        if (A.t.synthetic_seq_num) tr = (A.t.synthetic_seq_num << 8) | (tr & 0xffu);  // InternalKey.SetSeqNum
-        to_glb(O.trailer)[k] = tr;
-        if (O.kv_flags) to_glb(O.kv_flags)[k] = I.kv_flags ? to_glb(I.kv_flags)[kv0 + j] : uint8_t(0);
+        to_glb(O.trailer)[k] = v.tr;
+        if (O.kv_flags) to_glb(O.kv_flags)[k] = v.fl;
         if (O.entry_off && I.entry_off) to_glb(O.entry_off)[k] = to_glb(I.entry_off)[kv0 + j];
         to_glb(O.key_off)[okv + b + jo + rank] = ko;
         to_glb(O.val_off)[okv + b + jo + rank] = vo;
-        // key: prefix ++ key[:p] ++ (suffix | key[p:])
+        // key: F[:p] ++ (suffix | F[p:]),  F = prefix ++ key
         if (v.valid) {
-          const gptr<const uint8_t> src = to_glb(I.key_bytes) + kb_in + v.ko;
           gptr<uint8_t> dst = to_glb(O.key_bytes) + okb + ko;
           uint32_t w = 0;
-          for (uint32_t i = 0; i < A.t.prefix_len; i++) dst[w++] = pfx[i];
-          for (uint32_t i = 0; i < v.p; i++) dst[w++] = src[i];
+          for (uint32_t i = 0; i < v.p; i++) dst[w++] = v.F.at(i);
           if (A.t.suffix_len)
             for (uint32_t i = 0; i < A.t.suffix_len; i++) dst[w++] = sfx[i];
           else
-            for (uint32_t i = v.p; i < v.klen; i++) dst[w++] = src[i];
+            for (uint32_t i = v.p; i < v.F.len(); i++) dst[w++] = v.F.at(i);
         }
       }
       // values: each visible KV's bytes by the whole wave
@@ -241,7 +378,7 @@ __global__ void __launch_bounds__(kTPB) tf_scatter_kernel(TfArgs A) {
 extern "C" {
 
 uint64_t pbl_transform_workspace_bytes(uint32_t n_blocks) {
-  return uint64_t(pbl::tf::kTfWs) + 12ull * n_blocks;
+  return uint64_t(pbl::tf::kTfWs) + 16ull * n_blocks;
 }
 
 int pbl_transform_batch(const pbl_decode_out* in, uint32_t n_blocks, const pbl_transforms* t, pbl_decode_out* out,
@@ -258,11 +395,18 @@ int pbl_transform_batch(const pbl_decode_out* in, uint32_t n_blocks, const pbl_t
   if ((t->prefix_len && !t->prefix) || (t->suffix_len && !t->suffix) || t->split > PBL_SPLIT_CRDB)
     return PBL_INVALID_ARG;
   if (t->synthetic_seq_num >> 56) return PBL_INVALID_ARG;  // base.SeqNumMax
+  const pbl_block_batch* src = t->blocks;
+  if (!src || src->n_blocks != n_blocks) return PBL_INVALID_ARG;
+  // row blocks: invalid keys are re-read from the block (entry offsets, flags)
+  const bool rows = src->format == PBL_FMT_ROW || src->block_format;
+  if (rows && !(src->flags & PBL_ROW_RAW_KEYS) && (!in->kv_flags || (t->prefix_len && (!in->entry_off || !src->blocks))))
+    return PBL_INVALID_ARG;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   pbl::tf::TfArgs a;
   a.in = *in;
   a.out = *out;
   a.t = *t;
+  a.src = *src;
   a.n_blocks = n_blocks;
   if (n_blocks == 0) {
     if (hipMemcpyAsync(out->totals, in->totals, sizeof(pbl_totals), hipMemcpyDeviceToDevice, st) != hipSuccess)

@@ -16,7 +16,7 @@ from typing import Optional
 import torch
 
 from . import _native as N
-from .batch import Capacity, DecodedBatch, DecodeError, _stream_handle
+from .batch import BlockBatch, Capacity, DecodedBatch, DecodeError, _stream_handle
 from .rowblk import Transforms
 
 __all__ = ["Transforms", "apply_transforms"]
@@ -28,10 +28,18 @@ def _dev_bytes(b: bytes, device) -> Optional[torch.Tensor]:
     return torch.tensor(list(b), dtype=torch.uint8, device=device)
 
 
-def apply_transforms(d: DecodedBatch, t: Transforms, stream=None, cap: Optional[Capacity] = None) -> DecodedBatch:
+def apply_transforms(d: DecodedBatch, t: Transforms, stream=None, cap: Optional[Capacity] = None,
+                     source: Optional[BlockBatch] = None) -> DecodedBatch:
     """Transform decoded batch `d` (its totals must be final: call after the
-    decode's stream synchronised).  Output capacities default to exact upper
-    bounds: every KV kept, every key grown by prefix + suffix."""
+    decode's stream synchronised).  `source` is the BlockBatch `d` was decoded
+    from (default `d.source`, which `decode()` records): row blocks are re-read
+    where the synthetic prefix turns a key shorter than 8 B into a valid one
+    (rowblk_iter.go:400,1168-1199).  Output capacities default to exact upper
+    bounds: every KV kept, every key grown by prefix + suffix (a key made valid
+    by the prefix has a user key inside the prefix, so the bound holds)."""
+    src = source if source is not None else d.source
+    if src is None:
+        raise DecodeError("apply_transforms needs the BlockBatch the decoded batch came from")
     tot = d.read_totals()
     n_kv, kb, vb, nr = int(tot.n_kv), int(tot.key_bytes), int(tot.val_bytes), int(tot.n_restarts)
     grow = len(t.synthetic_prefix) + len(t.synthetic_suffix)
@@ -46,9 +54,10 @@ def apply_transforms(d: DecodedBatch, t: Transforms, stream=None, cap: Optional[
             out.workspace = torch.empty(ws, dtype=torch.uint8, device=dev)
         pfx = _dev_bytes(t.synthetic_prefix, dev)
         sfx = _dev_bytes(t.synthetic_suffix, dev)
+    sc = src.c_struct()
     tc = N.TransformsC(t.synthetic_seq_num, 1 if t.hide_obsolete_points else 0, t.split,
                        pfx.data_ptr() if pfx is not None else None, sfx.data_ptr() if sfx is not None else None,
-                       len(t.synthetic_prefix), len(t.synthetic_suffix))
+                       len(t.synthetic_prefix), len(t.synthetic_suffix), ctypes.pointer(sc))
     i, o = d.c_struct(), out.c_struct()
     rc = N.lib().pbl_transform_batch(ctypes.byref(i), d.n_blocks, ctypes.byref(tc), ctypes.byref(o),
                                      _stream_handle(st))

@@ -56,7 +56,7 @@ def test_ctypes_struct_layouts_match_library():
     n = L.pbl_struct_layout(ctypes.cast(buf, ctypes.c_void_p), cap)
     v = list(buf[:n])
     exp = []
-    for S in (N.BlockBatchC, N.TotalsC, N.DecodeOutC):
+    for S in (N.BlockBatchC, N.TotalsC, N.DecodeOutC, N.TransformsC):
         exp.append(ctypes.sizeof(S))
         exp += [getattr(S, f).offset for f, _ in S._fields_]
     assert v == exp

@@ -27,3 +27,19 @@ def test_bench_self_launch_yields_n_ranks(n):
     assert all(x[2] == n for x in d["ranks"])
     if n > 1:
         assert d["parallelism"] == f"shard{n}+rccl_offset_concat"
+
+
+def test_bench_multirank_step_on_gloo():
+    """`bench.py --gpus 2 --dist-backend gloo` with no GPU: both ranks run the
+    bench's own step -- its all-gather of per-rank totals and the rebase of the
+    per-block bases (concat_step) -- and rank 0 prints one JSON line with
+    n_gpus 2 and the concat checked against every rank's totals."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--blocks", "16", "--steps", "3", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["plumbing"] and d["concat_ok"] and d["steps"] == 3

@@ -24,11 +24,12 @@ from test_rowblk_gpu import ARRAYS, assert_same, pack, random_block
 pytestmark = pytest.mark.gpu
 
 
-def run(buf, off, lens, fmt, t: Transforms, block_fmt=None):
-    d = decode(BlockBatch.from_host(buf, off, lens, "cuda", fmt, 0, block_format=block_fmt))
+def run(buf, off, lens, fmt, t: Transforms, block_fmt=None, flags=0):
+    d = decode(BlockBatch.from_host(buf, off, lens, "cuda", fmt, flags, block_format=block_fmt))
     g = apply_transforms(d, t).to_host()
-    o = oracle.transform_batch(oracle.decode_batch(buf, off, lens, fmt, block_fmt), t.synthetic_seq_num,
-                               t.hide_obsolete_points, t.synthetic_prefix, t.synthetic_suffix, t.split)
+    o = oracle.transform_batch(oracle.decode_batch(buf, off, lens, fmt, block_fmt, flags), t.synthetic_seq_num,
+                               t.hide_obsolete_points, t.synthetic_prefix, t.synthetic_suffix, t.split,
+                               src=(buf, off, lens, fmt, block_fmt, flags))
     return g, o
 
 
@@ -107,3 +108,42 @@ def test_row_config2_shape_seqnum_property():
     assert np.array_equal(x["trailer"] & np.uint64(0xFF), h["trailer"] & np.uint64(0xFF))
     assert np.all((x["trailer"] >> np.uint64(8)) == 12345)
     assert np.array_equal(x["val_bytes"], h["val_bytes"]) and np.array_equal(x["restarts"], h["restarts"])
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_row_prefix_semantics_short_keys_and_split(seed):
+    """Row blocks under the transforms rowblk.Iter applies with the prefix
+    inside fullKey (rowblk_iter.go:259-263,400,1168-1199): raw keys shorter than
+    8 B made valid by the prefix, Split over prefix ++ key (testkeys '@' in the
+    prefix only, cockroachkvs version-length bytes reaching into the prefix),
+    hidden points and value prefixes of kinds taken from the prefix."""
+    from test_oracle_row_transforms import PREFIXES, raw_block, random_raw_keys, random_values
+    rng = random.Random(500 + seed)
+    flags = [0, N.PBL_ROW_VALUE_PREFIX, N.PBL_ROW_VALUE_PREFIX | N.PBL_ROW_NO_VALUER][seed % 3]
+    blocks = []
+    for _ in range(120):
+        n = rng.randint(1, 80)
+        blocks.append(raw_block(random_raw_keys(rng, n), random_values(rng, n), rng.choice([1, 2, 3, 16])))
+    buf, off, lens = pack(blocks)
+    for prefix in PREFIXES:
+        for suffix, split in ((b"", 0), (b"@9", N.PBL_SPLIT_TESTKEYS), (b"\x00" * 7 + b"\x07\x09", N.PBL_SPLIT_CRDB)):
+            t = Transforms(rng.choice([0, 77]), rng.random() < 0.5, prefix, suffix, split)
+            g, o = run(buf, off, lens, N.PBL_FMT_ROW, t, flags=flags)
+            assert_same(g, o, f"seed={seed} prefix={prefix!r} suffix={suffix!r}")
+
+
+def test_row_short_key_made_valid_on_gpu():
+    from test_oracle_row_transforms import raw_block
+    keys = [b"k" * 8 + (5 << 8 | 1).to_bytes(8, "little"), b"\x07\x08\x09", b"\x07\x08\x09\x0a"]
+    blk = raw_block(keys, [b"\x00v0", b"\x00v1", b""], 2)
+    buf, off, lens = pack([blk, blk])
+    prefix = b"PQR\x01\x01\x00\x00\x00"  # kinds of the short keys: prefix[3] and prefix[4] (SET)
+    g, o = run(buf, off, lens, N.PBL_FMT_ROW, Transforms(synthetic_prefix=prefix), flags=N.PBL_ROW_VALUE_PREFIX)
+    assert_same(g, o, "short key made valid")
+    # the third key becomes SET with an empty value: Go's i.val[0] panics -> corrupt block
+    assert g["n_bad_blocks"] == 2 and g["status_mask"] == 1 << N.PBL_CORRUPT_BOUNDS
+    g, o = run(buf, off, lens, N.PBL_FMT_ROW, Transforms(synthetic_prefix=b"PQR\x02\x02\x00\x00\x00"),
+               flags=N.PBL_ROW_VALUE_PREFIX)
+    assert_same(g, o, "short key made valid (kind MERGE)")
+    assert g["blk_status"].tolist() == [0, 0] and g["key_bytes"][:3].tobytes() == b"PQR"
+    assert g["n_kv"] == 6 and not (g["kv_flags"] & N.PBL_KV_INVALID_KEY).any()
