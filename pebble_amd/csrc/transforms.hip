@@ -308,6 +308,12 @@ __global__ void __launch_bounds__(kTPB) tf_scatter_kernel(TfArgs A) {
   const gptr<const uint8_t> sfx = to_glb(A.t.suffix);
   for (uint32_t b = blockIdx.x * wpb + wave_id(); b < A.n_blocks; b += gridDim.x * wpb) {
     const uint64_t okv = to_glb(O.blk_kv_base)[b], okb = to_glb(O.blk_key_base)[b], ovb = to_glb(O.blk_val_base)[b];
+    // restart words are the block's own (entry offsets never move); kept even
+    // when the transformed iteration turns the block corrupt
+    if (O.restarts && I.restarts) {
+      const uint64_t r0 = to_glb(I.blk_rst_base)[b], r1 = to_glb(I.blk_rst_base)[b + 1];
+      for (uint64_t r = r0 + lane; r < r1; r += kWave) to_glb(O.restarts)[r] = to_glb(I.restarts)[r];
+    }
     if (to_glb(O.blk_status)[b] != PBL_OK) {
       if (lane == 0) {
         to_glb(O.key_off)[okv + b] = 0;
@@ -363,11 +369,6 @@ __global__ void __launch_bounds__(kTPB) tf_scatter_kernel(TfArgs A) {
     if (lane == 0) {
       to_glb(O.key_off)[okv + b + jo] = kcur;
       to_glb(O.val_off)[okv + b + jo] = vcur;
-    }
-    // restart words are the block's own (entry offsets never move)
-    if (O.restarts && I.restarts) {
-      const uint64_t r0 = to_glb(I.blk_rst_base)[b], r1 = to_glb(I.blk_rst_base)[b + 1];
-      for (uint64_t r = r0 + lane; r < r1; r += kWave) to_glb(O.restarts)[r] = to_glb(I.restarts)[r];
     }
   }
 }
