@@ -60,8 +60,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the host->device->host (PCIe-inclusive) pass")
     p.add_argument("--e2e-chunk", type=int, default=2048, help="blocks per PCIe pipeline chunk")
-    p.add_argument("--kernel", choices=["auto", "single", "pipe"], default="auto",
-                   help="A/B: PBL_KERNEL_SINGLE / PBL_KERNEL_PIPE batch flags")
+    p.add_argument("--kernel", choices=["auto", "single", "pipe", "flat"], default="auto",
+                   help="A/B: PBL_KERNEL_SINGLE / PBL_KERNEL_PIPE / PBL_KERNEL_FLAT batch flags")
     p.add_argument("--launch-check", action="store_true",
                    help="launcher self-test without a GPU: N gloo ranks report in, rank 0 prints one JSON line")
     p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
@@ -242,7 +242,7 @@ def main():
 
     nb = a.blocks or (131072 if a.workload == "mixed" else 65536)
     flags = N.PBL_ROW_VALUE_PREFIX if a.value_prefix else 0
-    flags |= {"auto": 0, "single": N.PBL_KERNEL_SINGLE, "pipe": N.PBL_KERNEL_PIPE}[a.kernel]
+    flags |= {"auto": 0, "single": N.PBL_KERNEL_SINGLE, "pipe": N.PBL_KERNEL_PIPE, "flat": N.PBL_KERNEL_FLAT}[a.kernel]
     seed = a.seed + 7919 * rank
     t0 = time.time()
     block_fmt = None
@@ -250,7 +250,7 @@ def main():
         fmt = N.PBL_FMT_ROW
         buf, off, lens, n_kv = gen_row_blocks(seed, nb, a.block_size, a.restart_interval, a.key_len, a.val_len,
                                               a.value_prefix, n_threads=16)
-        kernel = "rowblk_decode_kernel" if a.kernel == "single" else "rowblk_pipe_kernel"
+        kernel = {"single": "rowblk_decode_kernel", "flat": "rowblk_flat_kernel"}.get(a.kernel, "rowblk_pipe_kernel")
         wl = (f"config2: {nb} x {a.block_size // 1024} KiB row-format blocks per GPU, restart interval "
               f"{a.restart_interval}, {a.key_len} B keys / {a.val_len} B values" + (", value prefix" if a.value_prefix else ""))
     elif a.workload == "col":

@@ -86,6 +86,9 @@ enum {
                                      persistent pipelines                          */
 #define PBL_KERNEL_PIPE 0x400u    /* A/B measurement, no effect on results: the
                                      pipelines even for a PBL_BATCH_VARLEN batch   */
+#define PBL_KERNEL_FLAT 0x800u    /* A/B measurement, no effect on results: row
+                                     batches on the one-wave-per-block kernel that
+                                     reads blocks from global memory               */
 
 /* per-KV flag byte (kv_flags[]) */
 #define PBL_KV_RESTART 0x01u       /* entry offset is a restart point            */

@@ -52,6 +52,7 @@ PBL_ROW_RAW_KEYS = 0x4
 PBL_BATCH_VARLEN = 0x100
 PBL_KERNEL_SINGLE = 0x200
 PBL_KERNEL_PIPE = 0x400
+PBL_KERNEL_FLAT = 0x800
 
 PBL_KV_RESTART = 0x01
 PBL_KV_RESTART_SAMEPFX = 0x02

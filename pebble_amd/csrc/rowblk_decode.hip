@@ -799,6 +799,7 @@ __global__ void __launch_bounds__(kTPB, 3) rowblk_decode_kernel(Args A) {
 }
 
 #include "rowblk_pipe.hip.h"
+#include "rowblk_flat.hip.h"
 
 // Mixed row + colblk batch (config 4): per-block format from block_format[];
 // both paths share the ticket order and the look-back state.
@@ -1092,6 +1093,24 @@ uint64_t persistent_grid(hipStream_t st, PersistentKernel k, const void* fn, uin
 }  // namespace pbl
 
 namespace {
+// Row batches on the flat kernel (rowblk_flat.hip.h): blocks past its length
+// limit are sized before it and written after it (values = false: the size pass).
+int launch_row_flat(const pbl::Args& a, hipStream_t st, bool values) {
+  const uint32_t nb = a.in.n_blocks;
+  int cus = 0;
+  const uint64_t grid = pbl::persistent_grid(st, pbl::kKRowFlat,
+                                             reinterpret_cast<const void*>(pbl::row::flat::rowblk_flat_kernel),
+                                             (uint64_t(nb) + pbl::row::flat::kFW - 1) / pbl::row::flat::kFW, &cus,
+                                             pbl::row::flat::kFTPB);
+  if (!grid) return PBL_DEVICE_ERROR;
+  const uint32_t small = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4));
+  hipLaunchKernelGGL(pbl::row::pipe::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+  hipLaunchKernelGGL(pbl::row::flat::rowblk_flat_kernel, dim3(uint32_t(grid)), dim3(pbl::row::flat::kFTPB), 0, st,
+                     a);
+  if (values) hipLaunchKernelGGL(pbl::row::pipe::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+  return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
+}
+
 // Mixed batches: PBL_KERNEL_SINGLE keeps the one-block-per-workgroup kernel
 // (A/B); the default splits the ids by format and runs the mixed pipeline,
 // with the big row blocks' size / value passes around it.
@@ -1174,6 +1193,7 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
     // blocks).  PBL_KERNEL_SINGLE selects the one-block-per-workgroup
     // persistent kernel (kept for A/B measurement); the default is the pipeline.
     const bool single = (batch->flags & PBL_KERNEL_SINGLE) != 0;
+    if (!single && (batch->flags & PBL_KERNEL_FLAT)) return launch_row_flat(a, st, true);
     const void* fn = single ? reinterpret_cast<const void*>(pbl::row::rowblk_decode_kernel)
                             : reinterpret_cast<const void*>(pbl::row::pipe::rowblk_pipe_kernel);
     int cus = 0;
@@ -1235,6 +1255,9 @@ int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stre
     // pointers), minus the big-block value pass
     if (batch->block_format) {
       rc = launch_mixed(batch, a, st, batch->flags & PBL_KERNEL_SINGLE, false);
+      if (rc != PBL_OK) return rc;
+    } else if (batch->flags & PBL_KERNEL_FLAT) {
+      rc = launch_row_flat(a, st, false);
       if (rc != PBL_OK) return rc;
     } else {
       int cus = 0;

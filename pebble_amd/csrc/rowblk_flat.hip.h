@@ -1,35 +1,41 @@
-// rowblk_flat.hip.h — the row-format decode, one wave per block, with the block
-// read from global memory instead of an LDS stage.
+// rowblk_flat.hip.h — the row-format decode with one wave per block and
+// lane-per-KV output, four independent waves per CU.
 //
-// Why: the LDS pipeline (rowblk_pipe.hip.h) stages every block in LDS for its
-// whole life (parse + emit), so LDS caps it at 4 blocks in flight per CU, and
-// each block is a ~30 K-cycle latency chain: 0.29 of HBM peak.  Here a wave
-// owns a block end to end and keeps only its per-KV metadata in LDS (6.5 KB),
-// so ~20 blocks are in flight per CU and the latency of each is hidden by the
-// others:
+// The LDS pipeline (rowblk_pipe.hip.h) splits a block over two stages (a parse
+// wave, three emit waves) and writes outputs granule by granule: ~9 K vector
+// instructions per block, most of them the per-granule lookups of the value
+// copy, and 4 blocks in flight per CU.  Here each wave owns a block end to end:
 //
-//   prefetch   the whole block is pulled towards the CU with LDS-DMA loads into
-//              a dump area that is never read (32 x 1 KB in flight: one HBM
-//              round trip for the block instead of one per restart-run step)
-//   pass 1     lane per restart run (rowblk_writer.go:147-155 cuts the prefix
-//              chain there) walks its entries' headers from global memory (L2
-//              hits after the prefetch): counts and the checks of readEntry;
-//              the block's aggregate is published to the look-back at once
-//   pass 2     the same walk again, writing per-KV metadata at final indices
-//              (entry / key source offsets, shared and key lengths, the prefix
-//              parent of each key, key and value output offsets, flags), then
-//              128-B output bucket tables; then the exclusive prefix is resolved
-//   emit       per-KV arrays, restart words, key bytes (each 16-B output
-//              granule the merge of its keys' prefix-chain segments) and value
-//              bytes (each 16-B output granule one or two unaligned global
-//              loads), all 64 lanes, 16-B aligned stores
+//   stage    the block HBM -> LDS by LDS-DMA (global_load_lds_dwordx4, no
+//            registers), one round trip
+//   pass 1   lane per restart run (rowblk_writer.go:147-155 cuts the prefix
+//            chain there) walks its entries' headers: counts and the checks of
+//            readEntry; the block's aggregate is published, and the look-back
+//            windows are requested at once
+//   pass 2   the same walk writes per-KV metadata at final indices (key source
+//            offset, shared and key length, prefix parent, key / value output
+//            offsets, value source, entry offset, flags) while the look-back
+//            loads are in flight; then the exclusive prefix is resolved
+//   emit     lane per KV: trailer, flags, offsets; the user key as 16-B chunks
+//            merged from its prefix chain's LDS segments; the value as 16-B
+//            chunks read straight from LDS; every store is a plain (unaligned)
+//            global store, exact at each key's and value's tail.  Values longer
+//            than kLongVal are copied by the whole wave, 1 KiB per instruction.
 //
-// Blocks this path does not take (more than kFKv KVs or 128 runs, more than
+// Per block that is a few hundred wave instructions for the outputs instead of
+// thousands.  The wave is alone on its SIMD (4 x 38 KB of LDS per CU), so the
+// loops keep independent work in flight rather than relying on other waves.
+//
+// (A first form read the block from global memory with 20 waves per CU and no
+// stage: every dependent global round trip then cost ~3 us under load and a
+// block took ~240 us; 655 GiB/s against the pipeline's 1034.)
+//
+// Blocks this path does not take (more than kFKv KVs or 2 x 64 runs, more than
 // 64 KiB of user-key bytes, a restart table inconsistent with per-run walks, a
-// value-prefix kind byte inside the shared prefix) run the wave-serial general
-// walk (rowblk_general.hip.h) with the wave's metadata area as its key buffer;
-// blocks past kFMaxLen are sized and written by big_block_{sizes,values}_kernel
-// around this launch, as for the pipeline.  Results are identical on every path.
+// value-prefix kind byte inside the shared prefix) take the wave-serial general
+// walk (rowblk_general.hip.h); blocks past kMaxFastLen are sized and written by
+// big_block_{sizes,values}_kernel around this launch.  Results are identical on
+// every path.
 //
 // Semantics: cockroachdb/pebble sstable/rowblk/rowblk_iter.go — Init :241-276,
 // readFirstKey :418-485, readEntry :333-416, decodeInternalKey :487-504, value
@@ -38,118 +44,109 @@
 
 namespace flat {
 
-#ifndef PBL_FLAT_WAVES
-#define PBL_FLAT_WAVES 4  // waves per workgroup (each an independent block stream)
-#endif
-#ifndef PBL_FLAT_WPE
-#define PBL_FLAT_WPE 5  // waves per SIMD the registers are budgeted for
-#endif
 #ifndef PBL_FLAT_TICKET
-#define PBL_FLAT_TICKET 2  // consecutive blocks per ticket (one atomic per ticket)
+// consecutive blocks per ticket.  Keep 1: a wave publishes its second block
+// only after the first is fully written, so with 2 every ticket's first block
+// waits on the previous ticket's completion and the whole batch serialises
+// (measured 631 ms per launch against 1.9 ms)
+#define PBL_FLAT_TICKET 1
 #endif
-#ifndef PBL_FLAT_PF
-#define PBL_FLAT_PF 1  // whole-block LDS-DMA prefetch
+#ifndef PBL_FLAT_VG
+#define PBL_FLAT_VG 0  // 1: values by 8-lane groups (contiguous stores; measured 932 vs 978 GiB/s lane per KV)
 #endif
-#ifndef PBL_FLAT_VU
-#define PBL_FLAT_VU 4  // value granules per lane per emit step
+#ifndef PBL_FLAT_LONG
+#define PBL_FLAT_LONG 256  // values longer than this are copied by the whole wave
 #endif
 
-constexpr int kFW = PBL_FLAT_WAVES;
+constexpr int kFW = 4;                   // waves per workgroup, one workgroup per CU
 constexpr int kFTPB = kFW * kWave;
 constexpr int kFKv = 320;                // KVs per block on this path
 constexpr int kFRounds = 2;              // restart runs per lane (<= 128 runs)
-constexpr uint32_t kFMaxLen = 32768;     // block length (u16 offsets)
 constexpr uint32_t kFKeyCap = 65535;     // user-key bytes per block (u16 offsets)
-constexpr int kFKBs = 8, kFVBs = 7;      // output bucket sizes: keys 256 B, values 128 B
-constexpr int kFKBkt = (kFKeyCap + 1) >> kFKBs;
-constexpr int kFVBkt = kFMaxLen >> kFVBs;
-constexpr int kFVU = PBL_FLAT_VU;
+constexpr uint32_t kLongVal = PBL_FLAT_LONG;
 
-// One wave's parsed block.  m0[j] = key source offset | shared << 16 | internal
-// key length << 32 | prefix parent << 48.
-struct FMeta {
+// One wave's block: the staged bytes and the per-KV metadata.  m0[j] = key
+// source offset | shared << 16 | internal key length << 32 | prefix parent << 48.
+struct WSlot {
+  uint4 x[kLdsBlkBytes / 16];  // the block, byte i at kPad + (boff & 15) + i
   uint64_t m0[kFKv];
-  uint32_t vp[kFKv + 5];    // value output offset | value source offset << 16; [nkv, nkv+4]: the total
-  uint16_t kout[kFKv + 1];  // user-key output offsets
-  uint16_t eoff[kFKv];      // entry offsets (KVEncoding.Offset)
-  uint16_t kbkt[kFKBkt];    // KV holding key output byte q << kFKBs
-  uint16_t vbkt[kFVBkt];    // KV holding value output byte q << kFVBs
-  uint8_t kvf[kFKv];        // PBL_KV_* (OBSOLETE is added at emit time)
+  uint32_t vp[kFKv + 1];       // value output offset | value source offset << 16
+  uint16_t kout[kFKv + 1];     // user-key output offsets
+  uint16_t eoff[kFKv];         // entry offsets (KVEncoding.Offset)
+  uint8_t kvf[kFKv];           // PBL_KV_* (OBSOLETE is added at emit time)
 };
 struct FLds {
-  FMeta m[kFW];
-  u32x4 dump[kWave];  // LDS-DMA target of the block prefetch (never read)
+  WSlot w[kFW];
 };
+static_assert(sizeof(FLds) <= 163840, "four waves' slots per CU");
 
 __device__ __forceinline__ uint32_t m_ksrc(uint64_t m) { return uint32_t(m) & 0xffffu; }
 __device__ __forceinline__ uint32_t m_sh(uint64_t m) { return uint32_t(m >> 16) & 0xffffu; }
 __device__ __forceinline__ uint32_t m_klen(uint64_t m) { return uint32_t(m >> 32) & 0xffffu; }
 __device__ __forceinline__ uint32_t m_par(uint64_t m) { return uint32_t(m >> 48); }
+__device__ __forceinline__ uint32_t f_vout(const WSlot& M, uint32_t j) { return M.vp[j] & 0xffffu; }
+__device__ __forceinline__ uint32_t f_vsrc(const WSlot& M, uint32_t j) { return M.vp[j] >> 16; }
 
-typedef u32x2 u32x2_ug __attribute__((aligned(1)));
 typedef u32x4 u32x4_ug __attribute__((aligned(1)));
 typedef uint32_t u32_ug __attribute__((aligned(1)));
+typedef uint64_t u64_ug __attribute__((aligned(1)));
+typedef uint16_t u16_ug __attribute__((aligned(1)));
 
-// The block in global memory.  Bytes [0, rlim) are readable (the ABI's 16-B
-// slack after every block); unaligned loads are used where they stay inside.
-struct GView {
-  gptr<const uint8_t> g;
-  uint32_t rlim;
-  __device__ __forceinline__ uint32_t byte(uint32_t i) const { return g[i]; }
-  __device__ __forceinline__ uint32_t le32(uint32_t i) const { return *(gptr<const u32_ug>)(g + i); }
-  __device__ __forceinline__ uint64_t ld8(uint32_t i) const {
-    if (__builtin_expect(i + 8 <= rlim, 1)) {
-      const u32x2 v = *(gptr<const u32x2_ug>)(g + i);
-      return uint64_t(v.y) << 32 | v.x;
-    }
-    uint64_t r = 0;
-    for (uint32_t k = 0; k < 8; k++)
-      if (i + k < rlim) r |= uint64_t(g[i + k]) << (8 * k);
-    return r;
-  }
-  // 16 bytes starting at block offset i (i < rlim)
-  __device__ __forceinline__ uint4 ld16(uint32_t i) const {
-    if (__builtin_expect(i + 16 <= rlim, 1)) {
-      const u32x4 v = *(gptr<const u32x4_ug>)(g + i);
-      return make_uint4(v.x, v.y, v.z, v.w);
-    }
-    const uint64_t a = uint64_t(g) + i, sa = a & ~uint64_t(15), end = uint64_t(g) + rlim;
-    const uint32_t sh = uint32_t(a - sa);
-    const u32x4 x = *(gptr<const u32x4>)(sa);
-    u32x4 y = u32x4{0, 0, 0, 0};
-    if (sh && sa + 16 < end) y = *(gptr<const u32x4>)(sa + 16);
-    return sh ? col::funnel16(make_uint4(x.x, x.y, x.z, x.w), make_uint4(y.x, y.y, y.z, y.w), sh)
-              : make_uint4(x.x, x.y, x.z, x.w);
-  }
-};
-struct GRd {  // init_checks' reader
-  GView V;
-  __device__ uint32_t byte(uint32_t i) const { return V.byte(i); }
-  __device__ uint32_t le32(uint32_t i) const { return V.le32(i); }
-  __device__ uint32_t varint(uint32_t p, uint32_t end, uint32_t* v) const {
-    return g_varint(reinterpret_cast<const uint8_t*>(V.g) + p, reinterpret_cast<const uint8_t*>(V.g) + end, v);
-  }
-};
+// Inclusive wave scan by DPP row shifts and row broadcasts (no ds_bpermute):
+// Hillis-Steele inside each row of 16 lanes, then the last lane of rows 0/2
+// into rows 1/3 (row_bcast:15), then of rows 0-1 into rows 2-3 (row_bcast:31).
+__device__ __forceinline__ uint32_t dpp_incl_scan(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+__device__ __forceinline__ uint32_t last_lane(uint32_t v) { return __builtin_amdgcn_readlane(v, kWave - 1); }
 
-// v placed at byte gq of a granule (bytes below gq zero)
-__device__ __forceinline__ uint4 place16(const uint4& v, uint32_t gq) {
-  return gq ? col::funnel16(make_uint4(0, 0, 0, 0), v, 16u - gq) : v;
+// Bytes [0, n) of w (n <= 16) to p, any alignment: one 16-B store when whole,
+// else the fewest 8/4/2/1-B stores (nothing past n: the next key or value
+// belongs to another lane).
+__device__ __forceinline__ void store_n(gptr<uint8_t> p, const uint4& w, uint32_t n) {
+  if (n == 16) {
+    *(gptr<u32x4_ug>)p = u32x4{w.x, w.y, w.z, w.w};
+    return;
+  }
+  uint64_t lo = uint64_t(w.x) | uint64_t(w.y) << 32, hi = uint64_t(w.z) | uint64_t(w.w) << 32;
+  uint32_t o = 0;
+  if (n & 8) {
+    *(gptr<u64_ug>)p = lo;
+    lo = hi;
+    o = 8;
+  }
+  if (n & 4) {
+    *(gptr<u32_ug>)(p + o) = uint32_t(lo);
+    lo >>= 32;
+    o += 4;
+  }
+  if (n & 2) {
+    *(gptr<u16_ug>)(p + o) = uint16_t(lo);
+    lo >>= 16;
+    o += 2;
+  }
+  if (n & 1) *(p + o) = uint8_t(lo);
 }
 
 struct Acc {
   uint32_t cnt, kb, vb;
 };
 
-// Pass 1 over run r: entry count and output bytes; `ok` clears where the run is
-// not walkable per run, `bad` sets on shared > len(previous key)
-// (rowblk_iter.go:403), `vbad` on a SET value without its prefix byte.
-__device__ __forceinline__ void f_count_run(const GView& V, uint32_t r, uint32_t nres, uint32_t roff, uint32_t flags,
-                                            bool vprefix, Acc& acc, bool& ok, bool& bad, bool& vbad) {
-  const uint32_t st = roff + 4 * r;
-  const uint32_t s0 = V.le32(st) & kRestartMask;
-  const uint32_t e0 = (r + 1 < nres) ? (V.le32(st + 4) & kRestartMask) : roff;
-  if (!((r != 0 || s0 == 0) && s0 < e0 && e0 <= roff)) { ok = false; return; }
-  uint32_t pos = s0, cnt = 0, prev_kl = 0;
+// Pass 1 over entries [pos, e0) of a run whose first `cnt` entries were
+// already counted (prev_kl = the length of the last one): entry count and
+// output bytes; `ok` clears where the run is not walkable per run, `bad` sets
+// on shared > len(previous key) (rowblk_iter.go:403), `vbad` on a SET value
+// without its prefix byte.
+__device__ __forceinline__ void f_count_span(const View& V, uint32_t pos, uint32_t e0, uint32_t cnt, uint32_t prev_kl,
+                                             uint32_t flags, bool vprefix, Acc& acc, bool& ok, bool& bad,
+                                             bool& vbad) {
+  const uint32_t cnt0 = cnt;
   while (pos < e0) {
     uint32_t sh, un, vl, h;
     const bool hok = pipe::hdr2(V.ld8(pos), &sh, &un, &vl, &h);
@@ -171,75 +168,173 @@ __device__ __forceinline__ void f_count_run(const GView& V, uint32_t r, uint32_t
     prev_kl = kl;
     pos = np;
   }
-  acc.cnt += cnt;
+  acc.cnt += cnt - cnt0;
 }
 
-// Pass 2 over run r (validated by pass 1): per-KV metadata at final indices
-// acc.cnt.. (acc = the run's bases).
-__device__ __forceinline__ void f_write_run(FMeta& M, const GView& V, uint32_t r, uint32_t nres, uint32_t roff,
-                                            uint32_t flags, bool vprefix, Acc acc) {
+__device__ __forceinline__ bool run_bounds(const View& V, uint32_t r, uint32_t nres, uint32_t roff, uint32_t* rw,
+                                           uint32_t* e0) {
   const uint32_t st = roff + 4 * r;
-  const uint32_t rw = V.le32(st);
-  const uint32_t e0 = (r + 1 < nres) ? (V.le32(st + 4) & kRestartMask) : roff;
-  uint32_t pos = rw & kRestartMask;
-  uint32_t j = acc.cnt, kb = acc.kb, vb = acc.vb;
-  uint32_t prev_sh = 0, pp = 0, ppsh = 0;
-  bool first = true;
+  *rw = V.le32(st);
+  const uint32_t s0 = *rw & kRestartMask;
+  *e0 = (r + 1 < nres) ? (V.le32(st + 4) & kRestartMask) : roff;
+  return (r != 0 || s0 == 0) && s0 < *e0 && *e0 <= roff;
+}
+
+// Pass 1 over run r, its first kPark entries' headers parked in registers
+// (static indices, no scratch: a wave is alone on its SIMD, so registers are
+// plentiful) for pass 2; a longer run counts its tail unparked.
+constexpr int kPark = 32;
+struct Park {
+  uint32_t ea[kPark];  // entry offset | shared << 16
+  uint32_t eb[kPark];  // unshared | header length << 14 | value length << 17
+  uint32_t cnt, rw, pos, e0, prev_kl;
+};
+
+__device__ __forceinline__ void f_count_park(const View& V, uint32_t r, uint32_t nres, uint32_t roff, uint32_t flags,
+                                             bool vprefix, Park& P, Acc& acc, bool& ok, bool& bad, bool& vbad) {
+  P.cnt = 0;
+  if (!run_bounds(V, r, nres, roff, &P.rw, &P.e0)) { ok = false; return; }
+  const uint32_t e0 = P.e0;
+  uint32_t pos = P.rw & kRestartMask, cnt = 0, prev_kl = 0;
+  bool go = true;
+#pragma unroll
+  for (int k = 0; k < kPark; k++) {
+    if (go && pos < e0) {
+      uint32_t sh, un, vl, h;
+      const bool hok = pipe::hdr2(V.ld8(pos), &sh, &un, &vl, &h);
+      const uint32_t np = pos + h + un + vl;
+      if (!hok || (k == 0 && sh != 0) || np > e0) {
+        ok = false;
+        go = false;
+      } else {
+        bad = bad || (k > 0 && sh > prev_kl);
+        const uint32_t kl = sh + un;
+        uint32_t vlen = vl;
+        if (vprefix && kl >= 8) {
+          if (kl - 8 < sh) { ok = false; go = false; }  // kind byte inside the shared prefix
+          else if ((V.byte(pos + h + (kl - 8 - sh)) & 0xBF) == 1) {
+            if (vl == 0) vbad = true;
+            else if ((V.byte(pos + h + un) & 0xC0) == 0 || (flags & PBL_ROW_NO_VALUER)) vlen--;
+          }
+        }
+        P.ea[k] = pos | (sh << 16);
+        P.eb[k] = un | (h << 14) | (vl << 17);
+        acc.kb += (flags & PBL_ROW_RAW_KEYS) ? kl : (kl >= 8 ? kl - 8 : 0);
+        acc.vb += vlen;
+        cnt++;
+        prev_kl = kl;
+        pos = np;
+      }
+    }
+  }
+  P.cnt = cnt;
+  P.pos = pos;
+  P.prev_kl = prev_kl;
+  acc.cnt += cnt;
+  if (go && pos < e0) f_count_span(V, pos, e0, cnt, prev_kl, flags, vprefix, acc, ok, bad, vbad);
+}
+
+// Pass 1 over run r without parking.
+__device__ __forceinline__ void f_count_run(const View& V, uint32_t r, uint32_t nres, uint32_t roff, uint32_t flags,
+                                            bool vprefix, Acc& acc, bool& ok, bool& bad, bool& vbad) {
+  uint32_t rw, e0;
+  if (!run_bounds(V, r, nres, roff, &rw, &e0)) { ok = false; return; }
+  f_count_span(V, rw & kRestartMask, e0, 0, 0, flags, vprefix, acc, ok, bad, vbad);
+}
+
+// Chain state of pass 2 carried from one entry of a run to the next: output
+// index / key / value offsets, the previous entry's shared length, its prefix
+// parent and that parent's shared length.
+struct WState {
+  uint32_t j, kb, vb, prev_sh, pp, ppsh;
+};
+
+// Per-KV metadata of one entry (pass 2).
+__device__ __forceinline__ void f_meta(WSlot& M, const View& V, uint32_t pos, uint32_t sh, uint32_t un, uint32_t vl,
+                                       uint32_t h, bool first, uint32_t rw, uint32_t flags, bool vprefix, WState& S) {
+  const uint32_t kl = sh + un;
+  uint32_t vs = pos + h + un, vlen = vl;
+  uint8_t fl = 0;
+  if (first) fl = uint8_t(PBL_KV_RESTART | ((rw >> 31) ? PBL_KV_RESTART_SAMEPFX : 0));
+  if (!(flags & PBL_ROW_RAW_KEYS) && kl < 8) fl |= PBL_KV_INVALID_KEY;
+  if (vprefix && kl >= 8 && (V.byte(pos + h + (kl - 8 - sh)) & 0xBF) == 1) {
+    const uint32_t pre = V.byte(vs);
+    if ((pre & 0xC0) == 0 || (flags & PBL_ROW_NO_VALUER)) { vs++; vlen--; }
+    else if ((pre & 0xC0) == 0x80) fl |= PBL_KV_VALBLK_HANDLE;
+    else fl |= PBL_KV_BLOB_HANDLE;
+  }
+  // prefix parent: nearest earlier entry of the run with a smaller shared
+  // length (all-nearest-smaller-values over the parents, amortised O(1)); the
+  // previous entry and its parent are kept in registers
+  uint32_t par = S.j, parsh = 0;
+  if (sh != 0) {
+    uint32_t c = S.j - 1, csh = S.prev_sh;
+    if (csh >= sh) { c = S.pp; csh = S.ppsh; }
+    while (csh >= sh) {
+      c = m_par(M.m0[c]);
+      csh = m_sh(M.m0[c]);
+    }
+    par = c;
+    parsh = csh;
+  }
+  M.m0[S.j] = uint64_t(pos + h) | uint64_t(sh) << 16 | uint64_t(kl) << 32 | uint64_t(par) << 48;
+  M.vp[S.j] = S.vb | (vs << 16);
+  M.kout[S.j] = uint16_t(S.kb);
+  M.eoff[S.j] = uint16_t(pos);
+  M.kvf[S.j] = fl;
+  S.prev_sh = sh;
+  S.pp = par;
+  S.ppsh = parsh;
+  S.kb += (flags & PBL_ROW_RAW_KEYS) ? kl : (kl >= 8 ? kl - 8 : 0);
+  S.vb += vlen;
+  S.j++;
+}
+
+// Pass 2 over entries [pos, e0) of a run (validated by pass 1), re-read from LDS.
+__device__ __forceinline__ void f_write_span(WSlot& M, const View& V, uint32_t pos, uint32_t e0, uint32_t rw,
+                                             bool first, uint32_t flags, bool vprefix, WState& S) {
   while (pos < e0) {
     uint32_t sh, un, vl, h;
     pipe::hdr2(V.ld8(pos), &sh, &un, &vl, &h);
-    const uint32_t kl = sh + un;
-    uint32_t vs = pos + h + un, vlen = vl;
-    uint8_t fl = 0;
-    if (first) fl = uint8_t(PBL_KV_RESTART | ((rw >> 31) ? PBL_KV_RESTART_SAMEPFX : 0));
-    if (!(flags & PBL_ROW_RAW_KEYS) && kl < 8) fl |= PBL_KV_INVALID_KEY;
-    if (vprefix && kl >= 8 && (V.byte(pos + h + (kl - 8 - sh)) & 0xBF) == 1) {
-      const uint32_t pre = V.byte(vs);
-      if ((pre & 0xC0) == 0 || (flags & PBL_ROW_NO_VALUER)) { vs++; vlen--; }
-      else if ((pre & 0xC0) == 0x80) fl |= PBL_KV_VALBLK_HANDLE;
-      else fl |= PBL_KV_BLOB_HANDLE;
-    }
-    // prefix parent: nearest earlier entry of the run with a smaller shared
-    // length (all-nearest-smaller-values over the parents, amortised O(1));
-    // the previous entry and its parent are kept in registers
-    uint32_t par = j, parsh = 0;
-    if (sh != 0) {
-      uint32_t c = j - 1, csh = prev_sh;
-      if (csh >= sh) { c = pp; csh = ppsh; }
-      while (csh >= sh) {
-        const uint64_t m = M.m0[c];
-        c = m_par(m);
-        csh = m_sh(M.m0[c]);
-      }
-      par = c;
-      parsh = csh;
-    }
-    M.m0[j] = uint64_t(pos + h) | uint64_t(sh) << 16 | uint64_t(kl) << 32 | uint64_t(par) << 48;
-    M.vp[j] = vb | (vs << 16);
-    M.kout[j] = uint16_t(kb);
-    M.eoff[j] = uint16_t(pos);
-    M.kvf[j] = fl;
-    prev_sh = sh;
-    pp = par;
-    ppsh = parsh;
-    kb += (flags & PBL_ROW_RAW_KEYS) ? kl : (kl >= 8 ? kl - 8 : 0);
-    vb += vlen;
-    j++;
+    f_meta(M, V, pos, sh, un, vl, h, first, rw, flags, vprefix, S);
     first = false;
     pos = pos + h + un + vl;
   }
 }
 
+// Pass 2 over run r (validated by pass 1): per-KV metadata at final indices
+// from acc (the run's bases).
+__device__ __forceinline__ void f_write_run(WSlot& M, const View& V, uint32_t r, uint32_t nres, uint32_t roff,
+                                            uint32_t flags, bool vprefix, Acc acc) {
+  uint32_t rw, e0;
+  run_bounds(V, r, nres, roff, &rw, &e0);
+  WState S{acc.cnt, acc.kb, acc.vb, 0, 0, 0};
+  f_write_span(M, V, rw & kRestartMask, e0, rw, true, flags, vprefix, S);
+}
+
+// Pass 2 from the parked headers (then the unparked tail, if any).
+__device__ __forceinline__ void f_write_park(WSlot& M, const View& V, const Park& P, uint32_t flags, bool vprefix,
+                                             Acc acc) {
+  WState S{acc.cnt, acc.kb, acc.vb, 0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < kPark; k++) {
+    if (uint32_t(k) < P.cnt)
+      f_meta(M, V, P.ea[k] & 0xffffu, P.ea[k] >> 16, P.eb[k] & 0x3fffu, P.eb[k] >> 17, (P.eb[k] >> 14) & 7u, k == 0,
+             P.rw, flags, vprefix, S);
+  }
+  if (P.pos < P.e0) f_write_span(M, V, P.pos, P.e0, P.rw, false, flags, vprefix, S);
+}
+
 // byte p of the internal key of KV j (source = max{i <= j : shared_i <= p})
-__device__ __forceinline__ uint32_t f_key_byte(const FMeta& M, const GView& V, int j, uint32_t p) {
+__device__ __forceinline__ uint32_t f_key_byte(const WSlot& M, const View& V, int j, uint32_t p) {
   uint64_t m = M.m0[j];
   while (p < m_sh(m)) m = M.m0[--j];
   return V.byte(m_ksrc(m) + p - m_sh(m));
 }
 
-__device__ __forceinline__ uint64_t f_trailer(const FMeta& M, const GView& V, int j, uint8_t* fl, uint32_t flags) {
+__device__ __forceinline__ uint64_t f_trailer(const WSlot& M, const View& V, int j, uint64_t m, uint8_t* fl,
+                                              uint32_t flags) {
   if (flags & PBL_ROW_RAW_KEYS) return 0;
-  const uint64_t m = M.m0[j];
   const uint32_t kl = m_klen(m);
   if (kl < 8) return kKindInvalid;
   const uint32_t sh = m_sh(m);
@@ -254,72 +349,65 @@ __device__ __forceinline__ uint64_t f_trailer(const FMeta& M, const GView& V, in
   return raw & kTrailerObsoleteMask;
 }
 
-// Merge user-key bytes [p_lo, p_hi) of KV j (user-key length ukl) into granule
-// bytes [q, ...) of w: walk the prefix-parent chain, one global load per segment.
-__device__ __forceinline__ void f_key_part(uint4& w, const FMeta& M, const GView& V, int j, uint32_t ukl,
-                                           uint32_t p_lo, uint32_t p_hi, uint32_t q) {
-  uint32_t cur = ukl;
-  int i = j;
-  while (cur > p_lo) {
-    const uint64_t m = M.m0[i];
+// Key bytes [c, c + n) of KV j (a chunk of <= 16 bytes, n > 0) merged from the
+// segments of its prefix chain: each an LDS read that starts where the chunk's
+// first byte would sit in that entry (at most 15 bytes before the block: the
+// stage's front pad), masked to its part of the chunk.
+__device__ __forceinline__ uint4 f_key_chunk(const WSlot& M, const View& V, uint64_t m, uint32_t c, uint32_t n) {
+  const uint32_t ce = c + n;
+  uint32_t cur = ce;  // bytes [c, cur) are still to be found
+  uint4 w = make_uint4(0, 0, 0, 0);
+  for (;;) {
     const uint32_t shi = m_sh(m);
-    const uint32_t lo_i = shi < cur ? shi : cur;
-    const uint32_t a = lo_i > p_lo ? lo_i : p_lo, z = cur < p_hi ? cur : p_hi;
-    if (a < z) {
-      const uint32_t gq = q + (a - p_lo);
-      const uint4 v = V.ld16(m_ksrc(m) - shi + a);
-      if (gq == 0 && z - a == 16) w = v;
-      else merge16(w, place16(v, gq), gq, gq + (z - a));
+    const uint32_t lo_i = shi < cur ? shi : cur;  // this entry supplies [max(sh, c), cur)
+    const uint32_t a = lo_i > c ? lo_i : c;
+    if (a < cur) {
+      const uint4 v = V.ld16(int32_t(m_ksrc(m)) - int32_t(shi) + int32_t(c));
+      if (a == c && cur - a == 16) return v;
+      merge16(w, v, a - c, cur - c);
     }
+    if (lo_i <= c) break;
     cur = lo_i;
-    i = int(m_par(m));
+    m = M.m0[m_par(m)];
   }
+  return w;
 }
 
-__device__ __forceinline__ uint32_t f_vout(const FMeta& M, uint32_t j) { return M.vp[j] & 0xffffu; }
-__device__ __forceinline__ uint32_t f_vsrc(const FMeta& M, uint32_t j) { return M.vp[j] >> 16; }
-
-// The whole block towards the CU: LDS-DMA loads of its 16-B granules into a
-// dump area nobody reads.  Issued before the first header load, so the walk's
-// loads then find their lines in L2.
-__device__ __forceinline__ void f_prefetch(u32x4* dump, const uint8_t* blocks, uint64_t boff, uint32_t blen) {
-#if PBL_FLAT_PF
+// The block HBM -> LDS by LDS-DMA: granule g of the 16-B aligned source range
+// lands at x[1 + g].  The caller waits vmcnt(0) before reading it.
+__device__ __forceinline__ void f_stage(WSlot& M, const uint8_t* blocks, uint64_t boff, uint32_t blen) {
   const uint64_t a0 = boff & ~uint64_t(15), a1 = (boff + blen + 15) & ~uint64_t(15);
   const uint32_t n16 = uint32_t((a1 - a0) >> 4);
   const uint32_t l = lane_id();
   const gptr<const uint8_t> base = to_glb(blocks + a0);
-  lptr<void> d = (lptr<void>)to_lds_ptr(reinterpret_cast<void*>(dump));
   for (uint32_t g0 = 0; g0 < n16; g0 += kWave) {
-    const uint32_t g = g0 + l < n16 ? g0 + l : n16 - 1;
-    __builtin_amdgcn_global_load_lds((gptr<const void>)(base + 16ull * g), d, 16, 0, 0);
+    if (g0 + l < n16)  // (EXEC masks the lanes past the end: nothing lands past the stage)
+      __builtin_amdgcn_global_load_lds((gptr<const void>)(base + 16ull * (g0 + l)),
+                                       (lptr<void>)to_lds_ptr(reinterpret_cast<void*>(&M.x[1 + g0])), 16, 0, 0);
   }
-#else
-  (void)dump; (void)blocks; (void)boff; (void)blen;
-#endif
 }
 
 // One block on one wave.
-__device__ __noinline__ void flat_block(FMeta& M, u32x4* dump, const Args A, uint32_t b) {
+__device__ __forceinline__ void flat_block(WSlot& M, const Args& A, uint32_t b) {
   const int l = lane_id();
   const uint32_t nb = A.in.n_blocks, flags = A.in.flags;
   const uint64_t boff = to_glb(A.in.block_off)[b];
   const uint32_t blen = to_glb(A.in.block_len)[b];
-  const bool fits = blen <= kFMaxLen;
+  const bool fits = blen <= kMaxFastLen;
   const bool vprefix = (flags & PBL_ROW_VALUE_PREFIX) && !(flags & PBL_ROW_RAW_KEYS);
   uint8_t* ws = reinterpret_cast<uint8_t*>(A.out.workspace);
   uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
   const uint8_t* gblk = A.in.blocks + boff;
-  const GView V{to_glb(gblk), uint32_t(((boff + blen + 15) & ~uint64_t(15)) - boff)};
 
   if (!fits) {
-    // a block past kFMaxLen: big_block_sizes_kernel walked it, published its
+    // a block past kMaxFastLen: big_block_sizes_kernel walked it, published its
     // aggregate and left {status, counts} in its block-metadata slots;
     // big_block_values_kernel writes its outputs after this launch
     const uint32_t st0 = to_glb(A.out.blk_status)[b];
     const bool okk = st0 == PBL_OK;
     const uint64_t agg[kNumComp] = {okk ? to_glb(A.out.blk_kv_base)[b] : 0, okk ? to_glb(A.out.blk_key_base)[b] : 0,
                                     okk ? to_glb(A.out.blk_val_base)[b] : 0,
-                                    okk ? uint64_t(V.le32(blen - 4)) : 0};
+                                    okk ? uint64_t(SlowGlb{to_glb(gblk), blen}.le32(blen - 4)) : 0};
     uint64_t excl[kNumComp];
     lb_resolve(lb_state, nb, b, agg, excl, &A.out.totals->status_mask);
     uint32_t st2 = st0;
@@ -334,26 +422,39 @@ __device__ __noinline__ void flat_block(FMeta& M, u32x4* dump, const Args A, uin
     return;
   }
 
-  f_prefetch(dump, A.in.blocks, boff, blen);
+  PSTAMP(A, b, 0, l == 0);
+  f_stage(M, A.in.blocks, boff, blen);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  wave_sync();
+  PSTAMP(A, b, 1, l == 0);
+  const View V = lds_view(M.x, uint32_t(kPad + (boff & 15)));
   uint32_t roff, nres;
-  uint32_t status = pipe::init_checks(GRd{V}, blen, flags, &roff, &nres);
+  uint32_t status = pipe::init_checks(LdsRd{V}, blen, flags, &roff, &nres);
   bool slow = status == PBL_OK && nres > uint32_t(kFRounds * kWave);
   uint32_t nkv = 0, tkb = 0, tvb = 0;
   Acc base[kFRounds];
   bool published = false;
+  LbWindows<kLbWin> G;
   if (status == PBL_OK && !slow && roff > 0) {
     bool ok = true, bad = false, vbad = false;
     uint32_t c0 = 0, k0 = 0, v0 = 0;
+    Park P;
+    P.cnt = 0;
+    P.pos = P.e0 = 0;
 #pragma unroll
     for (int i = 0; i < kFRounds; i++) {
       Acc acc{0, 0, 0};
       const uint32_t r = uint32_t(l + kWave * i);
-      if (uint32_t(kWave * i) < nres && r < nres) f_count_run(V, r, nres, roff, flags, vprefix, acc, ok, bad, vbad);
-      const uint32_t ic = wave_incl_scan(acc.cnt), ik = wave_incl_scan(acc.kb), iv = wave_incl_scan(acc.vb);
+      if (i == 0) {
+        if (r < nres) f_count_park(V, r, nres, roff, flags, vprefix, P, acc, ok, bad, vbad);
+      } else if (uint32_t(kWave * i) < nres && r < nres) {
+        f_count_run(V, r, nres, roff, flags, vprefix, acc, ok, bad, vbad);
+      }
+      const uint32_t ic = dpp_incl_scan(acc.cnt), ik = dpp_incl_scan(acc.kb), iv = dpp_incl_scan(acc.vb);
       base[i] = Acc{c0 + ic - acc.cnt, k0 + ik - acc.kb, v0 + iv - acc.vb};
-      c0 += pipe::wave_bcast_last(ic);
-      k0 += pipe::wave_bcast_last(ik);
-      v0 += pipe::wave_bcast_last(iv);
+      c0 += last_lane(ic);
+      k0 += last_lane(ik);
+      v0 += last_lane(iv);
     }
     nkv = c0;
     tkb = k0;
@@ -362,56 +463,70 @@ __device__ __noinline__ void flat_block(FMeta& M, u32x4* dump, const Args A, uin
     else if (__ballot(!ok) || nkv > uint32_t(kFKv) || tkb > kFKeyCap) slow = true;
     else if (__ballot(vbad)) status = PBL_CORRUPT_BOUNDS;  // Go: i.val[0] on an empty SET value
     if (status == PBL_OK && !slow) {
-      // the sizes are final: publish before the write pass
+      // the sizes are final: publish, request the look-back windows, and write
+      // the metadata while they are in flight
       const uint64_t agg[kNumComp] = {nkv, tkb, tvb, nres};
       lb_publish(lb_state, nb, b, agg);
       published = true;
+      PSTAMP(A, b, 2, l == 0);
+      if (b > 0) G.issue(LbPtrs(lb_state, nb), int64_t(b) - 1);
+      if (uint32_t(l) < nres) f_write_park(M, V, P, flags, vprefix, base[0]);
 #pragma unroll
-      for (int i = 0; i < kFRounds; i++) {
+      for (int i = 1; i < kFRounds; i++) {
         const uint32_t r = uint32_t(l + kWave * i);
         if (uint32_t(kWave * i) < nres && r < nres) f_write_run(M, V, r, nres, roff, flags, vprefix, base[i]);
       }
-      if (l < 5) M.vp[nkv + l] = tvb;
-      if (l == 0) M.kout[nkv] = uint16_t(tkb);
-      wave_sync();
-      // output buckets: the KV holding byte q << kFKBs / q << kFVBs
-      for (uint32_t j = l; j < nkv; j += kWave) {
-        const uint32_t k0b = M.kout[j], k1b = M.kout[j + 1];
-        for (uint32_t q = (k0b + (1u << kFKBs) - 1) >> kFKBs; (q << kFKBs) < k1b; q++) M.kbkt[q] = uint16_t(j);
-        const uint32_t v0b = f_vout(M, j), v1b = f_vout(M, j + 1);
-        for (uint32_t q = (v0b + (1u << kFVBs) - 1) >> kFVBs; (q << kFVBs) < v1b; q++) M.vbkt[q] = uint16_t(j);
+      if (l == 0) {
+        M.vp[nkv] = tvb;
+        M.kout[nkv] = uint16_t(tkb);
       }
       wave_sync();
+      PSTAMP(A, b, 3, l == 0);
     }
   }
 
   if (status == PBL_OK && slow) {
-    // general path: the wave-serial walk, the metadata area as its key buffer
+    // general path (wave-serial Iter.Next) on the staged block, the metadata
+    // area as its key buffer; a key that outgrows it re-runs from global
+    // memory with the whole staging buffer as the key buffer
     SlowState ss;
     uint64_t dummy[kNumComp] = {0, 0, 0, 0}, excl[kNumComp];
-    uint8_t* keybuf = reinterpret_cast<uint8_t*>(&M);
-    const uint32_t keycap = uint32_t(sizeof(FMeta)) & ~3u;
-    slow_walk(gblk, false, blen, flags, keybuf, keycap, kPassCount, A.out, b, dummy, &ss);
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(M.x) + kPad + (boff & 15);
+    bool from_lds = true;
+    uint8_t* keybuf = reinterpret_cast<uint8_t*>(M.m0);
+    uint32_t keycap = uint32_t(sizeof(WSlot) - offsetof(WSlot, m0)) & ~15u;
+    slow_walk(src, true, blen, flags, keybuf, keycap, kPassCount, A.out, b, dummy, &ss);
+    if (ss.status == PBL_UNSUPPORTED) {
+      from_lds = false;
+      src = gblk;
+      keybuf = reinterpret_cast<uint8_t*>(M.x);
+      keycap = uint32_t(kLdsBlkBytes);
+      slow_walk(src, false, blen, flags, keybuf, keycap, kPassCount, A.out, b, dummy, &ss);
+    }
     const bool okk = ss.status == PBL_OK;
     const uint64_t agg[kNumComp] = {okk ? ss.nkv : 0, okk ? ss.kb : 0, okk ? ss.vb : 0, okk ? ss.nr : 0};
     lookback(lb_state, nb, b, agg, excl, &A.out.totals->status_mask);
     uint32_t st2 = ss.status;
     if (okk && overflows(A.out, excl, agg)) st2 = PBL_OVERFLOW;
-    if (st2 == PBL_OK) slow_walk(gblk, false, blen, flags, keybuf, keycap, kPassAll, A.out, b, excl, &ss);
+    if (st2 == PBL_OK) slow_walk(src, from_lds, blen, flags, keybuf, keycap, kPassAll, A.out, b, excl, &ss);
     else if (l == 0 && A.out.key_off && excl[0] + b < A.out.kv_cap + nb) {
       to_glb(A.out.key_off)[excl[0] + b] = 0;
       to_glb(A.out.val_off)[excl[0] + b] = 0;
     }
     if (l == 0) write_block_meta(A.out, b, nb, st2, excl, agg, true);
-    wave_sync();  // (the key buffer is the next block's metadata area)
+    wave_sync();
     return;
   }
 
   const bool okb = status == PBL_OK;
   const uint64_t agg[kNumComp] = {okb ? nkv : 0, okb ? tkb : 0, okb ? tvb : 0, okb ? nres : 0};
-  if (!published) lb_publish(lb_state, nb, b, agg);
   uint64_t excl[kNumComp];
-  lb_resolve(lb_state, nb, b, agg, excl, &A.out.totals->status_mask);
+  if (!published) {
+    lb_publish(lb_state, nb, b, agg);
+    if (b > 0) G.issue(LbPtrs(lb_state, nb), int64_t(b) - 1);
+  }
+  lb_finish(lb_state, nb, b, agg, excl, &A.out.totals->status_mask, G);
+  PSTAMP(A, b, 4, l == 0);
   if (okb && overflows(A.out, excl, agg)) status = PBL_OVERFLOW;
   if (l == 0) {
     if (status != PBL_OK && A.out.key_off && excl[0] + b < A.out.kv_cap + nb) {
@@ -421,149 +536,121 @@ __device__ __noinline__ void flat_block(FMeta& M, u32x4* dump, const Args A, uin
     write_block_meta(A.out, b, nb, status, excl, agg, false);
   }
   if (status != PBL_OK) return;
+  if (nkv == 0) {  // a block with no entries: its lone N+1 offsets
+    if (l == 0) {
+      M.kout[0] = 0;
+      M.vp[0] = 0;
+    }
+    wave_sync();
+  }
 
-  // ---- emit ---------------------------------------------------------------
+  // ---- emit: lane per KV --------------------------------------------------
   const pbl_decode_out& O = A.out;
   const uint64_t kvb = excl[0], kbb = excl[1], vbb = excl[2], rbb = excl[3];
-
-  // value bytes: one 16-B aligned output granule per lane, kFVU per step with
-  // their loads in flight together: (1) bucket -> first KV, (2) a 5-word window
-  // of packed (vout | vsrc) words -> the KV holding the granule's first byte and
-  // the next one, (3) one or two unaligned global loads, merged when the
-  // granule straddles two values.  Granules touching 3+ values (values < 16 B)
-  // or past the window take the general loop.
-  if (tvb) {
-    const uint64_t d0 = vbb, d1 = vbb + tvb;
-    const gptr<uint8_t> vbytes = to_glb(O.val_bytes);
-    for (uint64_t a = (d0 & ~uint64_t(15)) + 16 * uint64_t(l); a < d1; a += 16ull * kFVU * kWave) {
-      uint4 w[kFVU], ga[kFVU], gb[kFVU];
-      uint32_t lo[kFVU], hi[kFVU], o[kFVU], oe[kFVU], j0[kFVU], sa[kFVU], ea[kFVU], sb[kFVU], eb[kFVU];
-      uint32_t srca[kFVU], srcb[kFVU];
-      bool live[kFVU], gen[kFVU], two[kFVU];
-#pragma unroll
-      for (int u = 0; u < kFVU; u++) {
-        const uint64_t g = a + uint64_t(u) * 16 * kWave;
-        live[u] = g < d1;
-        lo[u] = g < d0 ? uint32_t(d0 - g) : 0u;
-        hi[u] = !live[u] ? 0u : (g + 16 <= d1 ? 16u : uint32_t(d1 - g));
-        o[u] = live[u] ? uint32_t(g + lo[u] - d0) : 0u;
-        oe[u] = live[u] ? uint32_t(g + hi[u] - d0) : 0u;
-        j0[u] = M.vbkt[o[u] >> kFVBs];
-      }
-#pragma unroll
-      for (int u = 0; u < kFVU; u++) {
-        uint32_t vw[5];
-#pragma unroll
-        for (int k = 0; k < 5; k++) vw[k] = M.vp[j0[u] + k];
-        const uint32_t q = o[u];
-        const bool s1 = (vw[1] & 0xffff) <= q;
-        const bool s2 = s1 && (vw[2] & 0xffff) <= q;
-        const bool s3 = s2 && (vw[3] & 0xffff) <= q;
-        const uint32_t k = uint32_t(s1) + uint32_t(s2) + uint32_t(s3);
-        const uint32_t A0 = k == 0 ? vw[0] : k == 1 ? vw[1] : k == 2 ? vw[2] : vw[3];
-        const uint32_t A1 = k == 0 ? vw[1] : k == 1 ? vw[2] : k == 2 ? vw[3] : vw[4];
-        const uint32_t A2 = k == 0 ? vw[2] : k == 1 ? vw[3] : k == 2 ? vw[4] : vw[4];
-        const uint32_t v0 = A0 & 0xffff, v1 = A1 & 0xffff, v2 = A2 & 0xffff;
-        gen[u] = live[u] && ((s3 && (vw[4] & 0xffff) <= q) || (oe[u] > v1 && oe[u] > v2) || k == 3);
-        sa[u] = q;
-        ea[u] = oe[u] < v1 ? oe[u] : v1;
-        sb[u] = v1;
-        eb[u] = oe[u] < v2 ? oe[u] : v2;
-        two[u] = live[u] && !gen[u] && oe[u] > v1;
-        srca[u] = (A0 >> 16) + (sa[u] - v0);
-        srcb[u] = A1 >> 16;
-      }
-#pragma unroll
-      for (int u = 0; u < kFVU; u++) {
-        if (live[u] && !gen[u]) ga[u] = V.ld16(srca[u]);
-        if (two[u]) gb[u] = V.ld16(srcb[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < kFVU; u++) {
-        if (!live[u]) continue;
-        const uint64_t g = a + uint64_t(u) * 16 * kWave;
-        if (!gen[u]) {
-          const uint32_t gqa = uint32_t(d0 + sa[u] - g);
-          if (gqa == 0 && ea[u] - sa[u] == 16) {
-            w[u] = ga[u];
-          } else {
-            w[u] = make_uint4(0, 0, 0, 0);
-            merge16(w[u], place16(ga[u], gqa), gqa, gqa + (ea[u] - sa[u]));
-            if (two[u]) {
-              const uint32_t gqb = gqa + (sb[u] - sa[u]);
-              merge16(w[u], place16(gb[u], gqb), gqb, gqb + (eb[u] - sb[u]));
-            }
-          }
-        } else {
-          uint32_t j = j0[u];
-          while (f_vout(M, j + 1) <= o[u]) j++;
-          w[u] = make_uint4(0, 0, 0, 0);
-          for (;;) {
-            const uint32_t x0 = f_vout(M, j), x1 = f_vout(M, j + 1);
-            const uint32_t s_ = o[u] > x0 ? o[u] : x0, e_ = oe[u] < x1 ? oe[u] : x1;
-            if (s_ < e_) {
-              const uint32_t gq = uint32_t(d0 + s_ - g);
-              merge16(w[u], place16(V.ld16(f_vsrc(M, j) + (s_ - x0)), gq), gq, gq + (e_ - s_));
-            }
-            if (x1 >= oe[u]) break;
-            j++;
-          }
-        }
-        pipe::put16(vbytes, g, w[u], lo[u], hi[u]);
-      }
-    }
-  }
-
-  // per-KV arrays (thread per KV) and restart words
-  {
-    const gptr<uint32_t> key_off = to_glb(O.key_off), val_off = to_glb(O.val_off);
-    const gptr<uint64_t> trailer = to_glb(O.trailer);
-    for (uint32_t j = l; j <= nkv; j += kWave) {
-      const uint64_t oi = kvb + b + j;
-      key_off[oi] = M.kout[j];
-      val_off[oi] = f_vout(M, j);
+  const gptr<uint8_t> kbytes = to_glb(O.key_bytes) + kbb, vbytes = to_glb(O.val_bytes) + vbb;
+  const bool raw = (flags & PBL_ROW_RAW_KEYS) != 0;
+  for (uint32_t j0 = 0; j0 <= nkv; j0 += kWave) {
+    const uint32_t j = j0 + l;
+    uint32_t vlen = 0, vsrc = 0, vo = 0;
+    if (j <= nkv) {
+      const uint32_t ko = M.kout[j];
+      vo = f_vout(M, j);
+      to_glb(O.key_off)[kvb + b + j] = ko;
+      to_glb(O.val_off)[kvb + b + j] = vo;
       if (j < nkv) {
+        const uint64_t m = M.m0[j];
         uint8_t fl = M.kvf[j];
-        trailer[kvb + j] = f_trailer(M, V, int(j), &fl, flags);
+#ifndef PBL_FLAT_EXP_NOARR
+        to_glb(O.trailer)[kvb + j] = f_trailer(M, V, int(j), m, &fl, flags);
         if (O.kv_flags) to_glb(O.kv_flags)[kvb + j] = fl;
         if (O.entry_off) to_glb(O.entry_off)[kvb + j] = M.eoff[j];
+#else
+        (void)fl;
+#endif
+        // user key: 16-B chunks of its prefix chain
+        const uint32_t ukl = raw ? m_klen(m) : (m_klen(m) >= 8 ? m_klen(m) - 8 : 0u);
+#ifndef PBL_FLAT_EXP_NOKEY
+        for (uint32_t c = 0; c < ukl; c += 16) {
+          const uint32_t n = ukl - c < 16 ? ukl - c : 16u;
+          store_n(kbytes + ko + c, f_key_chunk(M, V, m, c, n), n);
+        }
+#else
+        (void)ukl;
+#endif
+        // value: 16-B chunks straight from the stage (short values; long ones below)
+        vsrc = f_vsrc(M, j);
+        vlen = f_vout(M, j + 1) - vo;
+#if !PBL_FLAT_VG && !defined(PBL_FLAT_EXP_NOVAL)
+        if (vlen <= kLongVal) {
+          // full 16-B chunks four at a time (their LDS reads together), then the tail
+          const uint32_t nf = vlen & ~15u;
+          for (uint32_t c = 0; c < nf; c += 64) {
+            uint4 x[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+              if (c + 16 * u < nf) x[u] = V.ld16(int32_t(vsrc + c + 16 * u));
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+              if (c + 16 * u < nf)
+                *(gptr<u32x4_ug>)(vbytes + vo + c + 16 * u) = u32x4{x[u].x, x[u].y, x[u].z, x[u].w};
+          }
+          if (vlen & 15u) store_n(vbytes + vo + nf, V.ld16(int32_t(vsrc + nf)), vlen & 15u);
+        }
+#endif
       }
     }
-    if (O.restarts)
-      for (uint32_t r = l; r < nres; r += kWave) to_glb(O.restarts)[rbb + r] = V.le32(roff + 4 * r);
-  }
-
-  // key bytes: one 16-B aligned output granule per lane; each the merge of the
-  // segments of the 1-2 keys it overlaps (each key its prefix chain)
-  if (tkb) {
-    const uint64_t d0 = kbb, d1 = kbb + tkb;
-    for (uint64_t a = (d0 & ~uint64_t(15)) + 16 * uint64_t(l); a < d1; a += 16 * kWave) {
-      const uint32_t lo = a < d0 ? uint32_t(d0 - a) : 0u, hi = a + 16 <= d1 ? 16u : uint32_t(d1 - a);
-      const uint32_t o = uint32_t(a + lo - d0), oe = uint32_t(a + hi - d0);
-      uint32_t j = M.kbkt[o >> kFKBs];
-      while (M.kout[j + 1] <= o) j++;
-      uint4 w = make_uint4(0, 0, 0, 0);
-      for (;;) {
-        const uint32_t k0 = M.kout[j], k1 = M.kout[j + 1];
-        const uint32_t s = o > k0 ? o : k0, e = oe < k1 ? oe : k1;
-        if (s < e) f_key_part(w, M, V, int(j), k1 - k0, s - k0, e - k0, uint32_t(d0 + s - a));
-        if (k1 >= oe) break;
-        j++;
+#if PBL_FLAT_VG
+    vlen = 0;  // (values are copied by the grouped loop below)
+#endif
+    // long values: the whole wave, 16 B per lane per step
+    for (uint64_t lm = __ballot(j < nkv && vlen > kLongVal); lm; lm &= lm - 1) {
+      const int s = __builtin_ctzll(lm);
+      const uint32_t ls = __shfl(vsrc, s, kWave), ll = __shfl(vlen, s, kWave), lo = __shfl(vo, s, kWave);
+      for (uint32_t c = 16u * l; c < ll; c += 16u * kWave) {
+        const uint32_t n = ll - c < 16 ? ll - c : 16u;
+        store_n(vbytes + lo + c, V.ld16(int32_t(ls + c)), n);
       }
-      pipe::put16(to_glb(O.key_bytes), a, w, lo, hi);
     }
   }
-  wave_sync();  // (the metadata area is the next block's)
+#if PBL_FLAT_VG && !defined(PBL_FLAT_EXP_NOVAL)
+  // values: 8 lanes per KV, lane k copying the KV's 16-B chunks k, k+8, ...;
+  // a store instruction then writes 8 contiguous runs instead of 64 scattered
+  // chunks.  Two groups' worth of KVs per lane step, their LDS reads together.
+  {
+    const uint32_t gk = uint32_t(l) & 7u, gi = uint32_t(l) >> 3;
+    for (uint32_t j0 = 0; j0 < nkv; j0 += 16) {
+      uint32_t vo2[2], vl2[2], vs2[2];
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const uint32_t j = j0 + 8 * u + gi;
+        const uint32_t a = j < nkv ? M.vp[j] : 0u, z = j < nkv ? M.vp[j + 1] : 0u;
+        vo2[u] = a & 0xffffu;
+        vl2[u] = (z & 0xffffu) - vo2[u];
+        vs2[u] = a >> 16;
+      }
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        for (uint32_t c = 16u * gk; c < vl2[u]; c += 128u) {
+          const uint32_t n = vl2[u] - c < 16 ? vl2[u] - c : 16u;
+          store_n(vbytes + vo2[u] + c, V.ld16(int32_t(vs2[u] + c)), n);
+        }
+      }
+    }
+  }
+#endif
+  if (O.restarts)
+    for (uint32_t r = l; r < nres; r += kWave) to_glb(O.restarts)[rbb + r] = V.le32(roff + 4 * r);
+  PSTAMP(A, b, 5, l == 0);
+  wave_sync();  // (the slot is the next block's)
 }
 
-// The persistent kernel: each wave takes tickets of PBL_FLAT_TICKET consecutive
-// blocks and decodes them in order.  Deadlock-free for any residency: a block's
-// look-back waits only on smaller tickets, all taken by resident waves that
-// publish before they wait.
-__global__ void __launch_bounds__(kFTPB) __attribute__((amdgpu_waves_per_eu(PBL_FLAT_WPE)))
-rowblk_flat_kernel(Args A) {
+// The persistent kernel: one workgroup per CU, each wave an independent stream
+// of tickets of PBL_FLAT_TICKET consecutive blocks, decoded in order.
+// Deadlock-free for any residency: a block's look-back waits only on smaller
+// tickets, all taken by resident waves that publish before they wait.
+__global__ void __launch_bounds__(kFTPB, 1) rowblk_flat_kernel(Args A) {
   __shared__ FLds L;
-  FMeta& M = L.m[wave_id()];
+  WSlot& M = L.w[wave_id()];
   const uint32_t nb = A.in.n_blocks;
   uint32_t* tick = reinterpret_cast<uint32_t*>(A.out.workspace);
   for (;;) {
@@ -572,7 +659,7 @@ rowblk_flat_kernel(Args A) {
     t0 = __builtin_amdgcn_readfirstlane(__shfl(t0, 0, kWave));
     if (t0 >= nb) break;
     const uint32_t t1 = nb - t0 < uint32_t(PBL_FLAT_TICKET) ? nb : t0 + uint32_t(PBL_FLAT_TICKET);
-    for (uint32_t b = t0; b < t1; b++) flat_block(M, L.dump, A, b);
+    for (uint32_t b = t0; b < t1; b++) flat_block(M, A, b);
   }
 }
 

@@ -50,6 +50,7 @@ elif workload == "mixed":
 else:
     buf, off, lens, n = gen_row_blocks(42, nb, 32768, 16, 16, 100, n_threads=16)
     b = BlockBatch.from_host(buf, off, lens, "cuda")
+b.flags |= int(os.environ.get("PROF_FLAGS", "0"), 0)  # e.g. PBL_KERNEL_FLAT (0x800) for A/B profiles
 h = decode(b).to_host()
 out = DecodedBatch.allocate(nb, Capacity(h["n_kv"], h["key_bytes_total"], h["val_bytes_total"], h["n_restarts"]),
                             "cuda")

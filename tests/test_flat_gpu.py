@@ -1,0 +1,97 @@
+"""The one-wave-per-block row kernel (rowblk_flat.hip.h, batch flag
+PBL_KERNEL_FLAT) against the oracle: bit-exact on every output array, over the
+same inputs as the pipeline's parity tests (reference blocks, synthetic
+configs, random and fuzzed blocks, value prefixes, blocks past the LDS limits,
+the general-path fallbacks)."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+from pebble_amd import _native as N
+from pebble_amd.rowblk import Writer, gen_row_blocks
+from test_rowblk_gpu import GOLDEN, assert_same, pack, random_block
+
+pytestmark = pytest.mark.gpu
+FLAT = N.PBL_KERNEL_FLAT
+
+
+def check(buf, off, lens, flags=0, ctx=""):
+    from pebble_amd.batch import BlockBatch, decode
+    o = oracle.rowblk_decode_batch(buf, off, lens, flags)
+    g = decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, flags | FLAT)).to_host()
+    assert_same(g, o, ctx)
+    return g
+
+
+def test_flat_hamlet_and_golden(golden):
+    g = golden["h_no_compression"]
+    blob = np.fromfile(os.path.join(GOLDEN, "h_no_compression_blocks.bin"), np.uint8)
+    blob = np.concatenate([blob, np.zeros(16, np.uint8)])
+    check(blob, np.array(g["block_off"], np.uint64), np.array(g["block_len"], np.uint32), 0, "hamlet")
+    wp = bytes.fromhex(golden["writer_with_prefix"]["block_hex"])
+    wb = bytes.fromhex(golden["writer_basic"]["block_hex"])
+    for flags in (0, N.PBL_ROW_VALUE_PREFIX, N.PBL_ROW_RAW_KEYS):
+        check(*pack([wp, wb, wp]), flags, f"golden flags={flags}")
+
+
+@pytest.mark.parametrize("ri", [1, 2, 16, 17, 32, 64])
+@pytest.mark.parametrize("kl,vl", [(16, 100), (8, 0), (64, 7), (24, 1000)])
+@pytest.mark.parametrize("vp", [False, True])
+def test_flat_synthetic_batches(ri, kl, vl, vp):
+    for bs in (4096, 32768):
+        buf, off, lens, n = gen_row_blocks(1000 + ri + kl + vl, 48, bs, ri, kl, vl, vp)
+        g = check(buf, off, lens, N.PBL_ROW_VALUE_PREFIX if vp else 0, f"ri={ri} kl={kl} vl={vl} vp={vp} bs={bs}")
+        assert g["n_kv"] == n
+
+
+def test_flat_random_blocks():
+    rng = random.Random(4321)
+    for flags in (0, N.PBL_ROW_VALUE_PREFIX, N.PBL_ROW_VALUE_PREFIX | N.PBL_ROW_NO_VALUER, N.PBL_ROW_RAW_KEYS):
+        blocks = [random_block(rng)[0] for _ in range(300)]
+        for align in (8, 1):
+            check(*pack(blocks, align), flags, f"random flags={flags} align={align}")
+
+
+def test_flat_fuzzed_blocks():
+    rng = random.Random(98)
+    blocks = []
+    for _ in range(400):
+        b = bytearray(random_block(rng)[0])
+        r = rng.random()
+        if r < 0.3 and len(b) > 4:
+            for _ in range(rng.randint(1, 4)):
+                b[rng.randrange(len(b))] ^= 1 << rng.randrange(8)
+        elif r < 0.4:
+            b = b[: rng.randint(0, len(b))]
+        elif r < 0.45:
+            b[-4:] = (0).to_bytes(4, "little")
+        blocks.append(bytes(b))
+    blocks += [b"", b"\x00", b"\x00\x00\x00\x00", Writer(16).finish()]
+    for flags in (0, N.PBL_ROW_VALUE_PREFIX):
+        g = check(*pack(blocks, 8), flags, f"fuzz flags={flags}")
+        assert g["n_bad_blocks"] > 0
+
+
+@pytest.mark.parametrize("bs", [65536, 200000])
+def test_flat_blocks_past_the_limit(bs):
+    buf, off, lens, n = gen_row_blocks(5, 6, bs, 16, 16, 100)
+    small = gen_row_blocks(6, 10, 32768, 16, 16, 100)
+    blocks = [bytes(buf[o:o + l]) for o, l in zip(off, lens)] + [bytes(small[0][o:o + l]) for o, l in zip(small[1], small[2])]
+    rng = random.Random(bs)
+    rng.shuffle(blocks)
+    check(*pack(blocks), 0, f"bs={bs}")
+
+
+def test_flat_config2_full_size_sha():
+    import hashlib
+    from pebble_amd.batch import BlockBatch, decode
+    buf, off, lens, n = gen_row_blocks(42, 65536, 32768, 16, 16, 100, n_threads=16)
+    gp = decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, N.PBL_KERNEL_PIPE)).to_host()
+    gf = decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, FLAT)).to_host()
+    for k in ("trailer", "kv_flags", "entry_off", "key_off", "val_off", "key_bytes", "val_bytes", "restarts",
+              "blk_kv_base", "blk_key_base", "blk_val_base", "blk_rst_base", "blk_status"):
+        assert hashlib.sha256(gp[k].tobytes()).digest() == hashlib.sha256(gf[k].tobytes()).digest(), k
+    assert gf["n_kv"] == n
