@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define PBL_ABI_VERSION 5
+#define PBL_ABI_VERSION 6
 
 /* ---- status codes (per block, and OR-ed as bit masks into totals) ---------- */
 enum {
@@ -57,7 +57,9 @@ enum {
   PBL_CORRUPT_CHECKSUM = 10,     /* block.go:177-195 "checksum mismatch"        */
   PBL_CORRUPT_COMPRESSION = 11,  /* snappy.ErrCorrupt -> base.MarkCorruptionError (block.go:550-565) */
   PBL_CORRUPT_FOOTER = 12,       /* parseFooter's CorruptionErrorf sites (sstable/table.go:328-404) */
-  PBL_CORRUPT_INDEX = 13         /* DecodeHandleWithProperties "invalid block.Handle" (block/block.go:94-104) */
+  PBL_CORRUPT_INDEX = 13,        /* DecodeHandleWithProperties "invalid block.Handle" (block/block.go:94-104) */
+  PBL_CORRUPT_VALUE_HANDLE = 14  /* valblk handle/index entry out of bounds (valblk/valblk.go:370-393,
+                                    valblk/reader.go:280-302) */
 };
 
 /* ---- block formats ---------------------------------------------------------- */
@@ -196,7 +198,9 @@ int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stre
  * (ctypes, cgo): writes up to `cap` u64 values and returns how many it has:
  *   sizeof(pbl_block_batch), the offsets of its 8 fields in declaration order,
  *   sizeof(pbl_totals), the offsets of its 8 fields,
- *   sizeof(pbl_decode_out), the offsets of its 20 fields.
+ *   sizeof(pbl_decode_out), the offsets of its 20 fields,
+ *   then likewise pbl_transforms, pbl_footer, pbl_index_out, pbl_kv_out and
+ *   pbl_value_out (sizeof, then every field's offset in declaration order).
  */
 size_t pbl_struct_layout(uint64_t* out, size_t cap);
 
@@ -251,15 +255,19 @@ int pbl_verify_checksums(const pbl_phys_batch* batch, uint32_t checksum_type, ui
                          void* stream);
 /*
  * Decompressor.DecompressedLen (block.go:549-556) of every block: out_len[b];
- * status[b] = PBL_OK, PBL_CORRUPT_COMPRESSION or PBL_UNSUPPORTED (zstd, minlz and
- * the legacy codecs are not decoded on the device).
+ * status[b] = PBL_OK, PBL_CORRUPT_COMPRESSION or PBL_UNSUPPORTED (minlz and the
+ * legacy codecs are not decoded on the device).  Snappy: its uvarint header;
+ * zstd: the uvarint Pebble prefixes (zstd_cgo.go:111-119).
  */
 int pbl_decompressed_lengths(const pbl_phys_batch* batch, uint32_t* out_len, uint32_t* status, void* stream);
 /*
  * DecompressInto (block.go:557-565): block b's decoded bytes at out + out_off[b]
  * (out_cap[b] bytes available; DEVICE arrays), its length in out_len[b] and
  * status[b] = PBL_OK / PBL_CORRUPT_COMPRESSION / PBL_OVERFLOW / PBL_UNSUPPORTED.
- * Uncompressed blocks are copied.  The outputs form a pbl_block_batch {out,
+ * Uncompressed blocks are copied; snappy (golang/snappy block format) and zstd
+ * (RFC 8878 frames after Pebble's uvarint length, zstd_cgo.go:86-108: the frames
+ * must decode to exactly that length; a frame naming a dictionary is
+ * PBL_UNSUPPORTED) are decoded on the device.  The outputs form a pbl_block_batch {out,
  * out_off, out_len} for pbl_decode_batch (keep out_off 8-B aligned for colblk).
  */
 int pbl_decompress_blocks(const pbl_phys_batch* batch, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
@@ -320,6 +328,68 @@ int pbl_index_handles_row(const pbl_decode_out* decoded, uint32_t n_blocks, pbl_
  * PBL_OVERFLOW for the blocks that do not fit and writes none of their entries.
  */
 int pbl_index_handles_col(const pbl_block_batch* batch, pbl_index_out* out, void* stream);
+
+typedef struct pbl_kv_out {
+  uint64_t* key_off;     /* [cap] where KeyAt(i) starts in the batch's block bytes      */
+  uint32_t* key_len;     /* [cap]                                                        */
+  uint64_t* val_off;     /* [cap] where ValueAt(i) starts in the batch's block bytes    */
+  uint32_t* val_len;     /* [cap]                                                        */
+  uint64_t* blk_base;    /* [n_blocks + 1] first entry of each block; [n_blocks] = total */
+  uint32_t* blk_status;  /* [n_blocks] PBL_OK / PBL_CORRUPT_COLBLK_HEADER /
+                            PBL_CORRUPT_BOUNDS / PBL_OVERFLOW                            */
+  uint64_t cap;          /* entries the arrays hold                                       */
+} pbl_kv_out;
+/*
+ * colblk.KeyValueBlockDecoder (colblk/key_value_block.go:76-89) over a batch of
+ * key-value blocks -- the metaindex of Pebblev6+ tables and the properties
+ * block of Pebblev7+ tables (sstable/reader.go:536-545,601-617;
+ * layout.go:789-824): no custom header, column 0 the keys and column 1 the
+ * values (RawBytes).  Every row's key and value are reported as slices of the
+ * batch's bytes (zero-copy, as KeyAt / ValueAt).  Column layout checks as for
+ * data blocks; a slice past its block is PBL_CORRUPT_BOUNDS.  Sized, scanned,
+ * then written; a total past cap reports PBL_OVERFLOW for the blocks that do
+ * not fit.
+ */
+int pbl_kv_blocks(const pbl_block_batch* batch, pbl_kv_out* out, void* stream);
+
+/*
+ * The value-block index (valblk/valblk.go:338-393) on the device: `vbi` holds
+ * the decompressed index block (vbi_len bytes, DEVICE memory), rows of
+ * num_w + off_w + len_w little-endian bytes (valblk.IndexHandle widths, each
+ * 1..8).  Writes the handle of value block i to handle_off[i] / handle_len[i]
+ * for i < min(rows, cap) and *n_blocks = rows (DEVICE u32; rows = vbi_len / row
+ * width).  *status (DEVICE u32) = PBL_OK, or PBL_CORRUPT_VALUE_HANDLE when a
+ * row's block number is not its index, the block has a partial row, or a
+ * width is 0 or > 8 (DecodeIndex's errors).
+ */
+int pbl_valblk_index(const uint8_t* vbi, uint64_t vbi_len, uint32_t num_w, uint32_t off_w, uint32_t len_w,
+                     uint64_t* handle_off, uint64_t* handle_len, uint32_t cap, uint32_t* n_blocks,
+                     uint32_t* status, void* stream);
+
+typedef struct pbl_value_out {
+  uint32_t* val_off;     /* [kv_cap + n_blocks] block-relative value offsets (as pbl_decode_out) */
+  uint8_t* val_bytes;    /* [val_cap]                                                            */
+  uint64_t* blk_val_base;/* [n_blocks + 1]; [n_blocks] = total                                   */
+  uint32_t* blk_status;  /* [n_blocks] the decode's status, else PBL_OK /
+                            PBL_CORRUPT_VALUE_HANDLE / PBL_OVERFLOW                              */
+  uint64_t val_cap;
+} pbl_value_out;
+/*
+ * Resolve value-block handles (valueBlockFetcher.Fetch, valblk/reader.go:251-302)
+ * for every KV of a decoded batch: a KV whose kv_flags has PBL_KV_VALBLK_HANDLE
+ * holds the value prefix byte + valblk.Handle (uvarint ValueLen, BlockNum,
+ * OffsetInBlock; valblk.go:218-279); its value becomes
+ * value_blocks[BlockNum][OffsetInBlock : OffsetInBlock + ValueLen] of the
+ * batch of (decompressed) value blocks.  Every other value is copied as is
+ * (blob handles stay handles, as a reader without blob files reports them).
+ * `decoded` needs kv_flags, val_off, val_bytes, blk_kv_base, blk_val_base and
+ * blk_status.  A handle past its value block, or naming a block past the
+ * batch, makes its block PBL_CORRUPT_VALUE_HANDLE.  Sized, scanned, then
+ * written; a total past val_cap reports PBL_OVERFLOW for the blocks that do
+ * not fit.
+ */
+int pbl_resolve_values(const pbl_decode_out* decoded, uint32_t n_blocks, const pbl_block_batch* value_blocks,
+                       pbl_value_out* out, void* stream);
 
 /* ---- blockiter.Transforms on the device ------------------ */
 /* Comparer.Split used to find the suffix a SyntheticSuffix replaces. */

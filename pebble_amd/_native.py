@@ -28,19 +28,21 @@ PBL_CORRUPT_CHECKSUM = 10
 PBL_CORRUPT_COMPRESSION = 11
 PBL_CORRUPT_FOOTER = 12
 PBL_CORRUPT_INDEX = 13
+PBL_CORRUPT_VALUE_HANDLE = 14
 STATUS_NAMES = {
     0: "OK", 1: "CORRUPT_NO_RESTARTS", 2: "CORRUPT_FIRST_KEY", 3: "CORRUPT_BOUNDS",
     4: "CORRUPT_COLBLK_HEADER", 5: "UNSUPPORTED", 6: "OVERFLOW", 7: "INVALID_ARG",
     8: "DEVICE_ERROR", 9: "TIMEOUT", 10: "CORRUPT_CHECKSUM", 11: "CORRUPT_COMPRESSION",
-    12: "CORRUPT_FOOTER", 13: "CORRUPT_INDEX",
+    12: "CORRUPT_FOOTER", 13: "CORRUPT_INDEX", 14: "CORRUPT_VALUE_HANDLE",
 }
 # TableFormat (footer magic, version)
 PBL_TABLE_LEVELDB, PBL_TABLE_ROCKSDBV2 = 1, 2
 PBL_TABLE_PEBBLEV1 = 3  # .. PBL_TABLE_PEBBLEV8 = 10
+PBL_TABLE_PEBBLEV5, PBL_TABLE_PEBBLEV6, PBL_TABLE_PEBBLEV7 = 7, 8, 9
 PBL_CHECKSUM_NONE, PBL_CHECKSUM_CRC32C, PBL_CHECKSUM_XXHASH, PBL_CHECKSUM_XXHASH64 = 0, 1, 2, 3
 PBL_COMPRESSION_NONE, PBL_COMPRESSION_SNAPPY, PBL_COMPRESSION_ZSTD, PBL_COMPRESSION_MINLZ = 0, 1, 7, 8
 
-ABI_VERSION = 5  # include/pebble_amd.h PBL_ABI_VERSION
+ABI_VERSION = 6  # include/pebble_amd.h PBL_ABI_VERSION
 
 PBL_FMT_ROW = 0
 PBL_FMT_COL_DEFAULT = 1
@@ -137,6 +139,16 @@ class IndexOutC(ctypes.Structure):
                 ("blk_base", _vp), ("blk_status", _vp), ("cap", ctypes.c_uint64)]
 
 
+class KvOutC(ctypes.Structure):
+    _fields_ = [("key_off", _vp), ("key_len", _vp), ("val_off", _vp), ("val_len", _vp), ("blk_base", _vp),
+                ("blk_status", _vp), ("cap", ctypes.c_uint64)]
+
+
+class ValueOutC(ctypes.Structure):
+    _fields_ = [("val_off", _vp), ("val_bytes", _vp), ("blk_val_base", _vp), ("blk_status", _vp),
+                ("val_cap", ctypes.c_uint64)]
+
+
 class TransformsC(ctypes.Structure):
     _fields_ = [
         ("synthetic_seq_num", ctypes.c_uint64), ("hide_obsolete_points", ctypes.c_uint32),
@@ -161,6 +173,11 @@ SIGNATURES = {
     "pbl_index_handles_row": (ctypes.c_int, [ctypes.POINTER(DecodeOutC), ctypes.c_uint32, ctypes.POINTER(IndexOutC),
                                              _vp]),
     "pbl_index_handles_col": (ctypes.c_int, [ctypes.POINTER(BlockBatchC), ctypes.POINTER(IndexOutC), _vp]),
+    "pbl_kv_blocks": (ctypes.c_int, [ctypes.POINTER(BlockBatchC), ctypes.POINTER(KvOutC), _vp]),
+    "pbl_valblk_index": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                        _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp]),
+    "pbl_resolve_values": (ctypes.c_int, [ctypes.POINTER(DecodeOutC), ctypes.c_uint32, ctypes.POINTER(BlockBatchC),
+                                          ctypes.POINTER(ValueOutC), _vp]),
     "pbl_transform_batch": (ctypes.c_int, [ctypes.POINTER(DecodeOutC), ctypes.c_uint32, ctypes.POINTER(TransformsC),
                                            ctypes.POINTER(DecodeOutC), _vp]),
     "pbl_rebase_blocks": (ctypes.c_int, [ctypes.POINTER(DecodeOutC), ctypes.c_uint32, ctypes.c_uint64,

@@ -18,13 +18,16 @@
 //                         lane 0 walks the elements, the wave copies each one
 //                         (an overlapping copy repeats its period: byte i of a
 //                         copy reads dst[d - off + i % off], all before d)
-// Zstd (indicator 7) and the other codecs report PBL_UNSUPPORTED.
+//   zstd_kernel           (zstd.hip) the blocks whose indicator is zstd
+// MinLZ (indicator 8) and unknown indicators report PBL_UNSUPPORTED.
 #include <algorithm>
 
 #include "common.hip.h"
 #include "colblk_block.hip.h"
 
 namespace pbl {
+hipError_t launch_zstd(const pbl_phys_batch& batch, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                       uint32_t* out_len, uint32_t* status, hipStream_t st);
 namespace phys {
 
 constexpr uint32_t kPoly = 0x82F63B78u;  // reflected Castagnoli
@@ -256,7 +259,8 @@ __global__ void __launch_bounds__(kTPB) snappy_len_kernel(const pbl_phys_batch B
     const uint32_t ind = p[n];
     uint32_t st = PBL_OK, len = 0, used = 0;
     if (ind == PBL_COMPRESSION_NONE) len = n;
-    else if (ind == PBL_COMPRESSION_SNAPPY) st = uvarint32(p, n, &len, &used) ? PBL_OK : PBL_CORRUPT_COMPRESSION;
+    else if (ind == PBL_COMPRESSION_SNAPPY || ind == PBL_COMPRESSION_ZSTD)  // (zstd_cgo.go:111-119)
+      st = uvarint32(p, n, &len, &used) ? PBL_OK : PBL_CORRUPT_COMPRESSION;
     else st = PBL_UNSUPPORTED;
     out_len[b] = st == PBL_OK ? len : 0u;
     status[b] = st;
@@ -394,6 +398,7 @@ __global__ void __launch_bounds__(kWave) snappy_kernel(const pbl_phys_batch B, u
     const uint32_t n = B.block_len[b];
     const gptr<const uint8_t> src = to_glb(B.bytes + B.block_off[b]);
     const uint32_t ind = src[n];
+    if (ind == PBL_COMPRESSION_ZSTD) continue;  // zstd_kernel's
     gptr<uint8_t> dst = to_glb(out + out_off[b]);
     const uint32_t cap = out_cap[b];
     uint32_t st = PBL_OK, len = 0;
@@ -519,7 +524,9 @@ int pbl_decompress_blocks(const pbl_phys_batch* batch, uint8_t* out, const uint6
   const uint32_t grid = std::min<uint32_t>(batch->n_blocks, 2048);
   hipLaunchKernelGGL(pbl::phys::snappy_kernel, dim3(grid), dim3(pbl::kWave), 0, st, *batch, out, out_off, out_cap,
                      out_len, status);
-  return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
+  if (hipGetLastError() != hipSuccess) return PBL_DEVICE_ERROR;
+  return pbl::launch_zstd(*batch, out, out_off, out_cap, out_len, status, st) == hipSuccess ? PBL_OK
+                                                                                              : PBL_DEVICE_ERROR;
 }
 
 }  // extern "C"

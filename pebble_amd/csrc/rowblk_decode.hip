@@ -1298,7 +1298,19 @@ size_t pbl_struct_layout(uint64_t* out, size_t cap) {
       sizeof(pbl_transforms), PBL_OFF(pbl_transforms, synthetic_seq_num),
       PBL_OFF(pbl_transforms, hide_obsolete_points), PBL_OFF(pbl_transforms, split), PBL_OFF(pbl_transforms, prefix),
       PBL_OFF(pbl_transforms, suffix), PBL_OFF(pbl_transforms, prefix_len), PBL_OFF(pbl_transforms, suffix_len),
-      PBL_OFF(pbl_transforms, blocks)};
+      PBL_OFF(pbl_transforms, blocks),
+      sizeof(pbl_footer), PBL_OFF(pbl_footer, table_format), PBL_OFF(pbl_footer, checksum_type),
+      PBL_OFF(pbl_footer, metaindex_off), PBL_OFF(pbl_footer, metaindex_len), PBL_OFF(pbl_footer, index_off),
+      PBL_OFF(pbl_footer, index_len), PBL_OFF(pbl_footer, footer_off), PBL_OFF(pbl_footer, footer_len),
+      PBL_OFF(pbl_footer, attributes), PBL_OFF(pbl_footer, reserved),
+      sizeof(pbl_index_out), PBL_OFF(pbl_index_out, handle_off), PBL_OFF(pbl_index_out, handle_len),
+      PBL_OFF(pbl_index_out, props_off), PBL_OFF(pbl_index_out, props_len), PBL_OFF(pbl_index_out, blk_base),
+      PBL_OFF(pbl_index_out, blk_status), PBL_OFF(pbl_index_out, cap),
+      sizeof(pbl_kv_out), PBL_OFF(pbl_kv_out, key_off), PBL_OFF(pbl_kv_out, key_len), PBL_OFF(pbl_kv_out, val_off),
+      PBL_OFF(pbl_kv_out, val_len), PBL_OFF(pbl_kv_out, blk_base), PBL_OFF(pbl_kv_out, blk_status),
+      PBL_OFF(pbl_kv_out, cap),
+      sizeof(pbl_value_out), PBL_OFF(pbl_value_out, val_off), PBL_OFF(pbl_value_out, val_bytes),
+      PBL_OFF(pbl_value_out, blk_val_base), PBL_OFF(pbl_value_out, blk_status), PBL_OFF(pbl_value_out, val_cap)};
 #undef PBL_OFF
   const size_t n = sizeof(v) / sizeof(v[0]);
   for (size_t i = 0; i < n && i < cap && out; i++) out[i] = v[i];

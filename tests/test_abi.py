@@ -51,12 +51,13 @@ def test_ctypes_struct_layouts_match_library():
     """sizeof/offsetof of the ctypes mirrors equal the compiled library's
     (pbl_struct_layout), field by field."""
     L = N.lib()
-    cap = 64
+    cap = 256
     buf = (ctypes.c_uint64 * cap)()
     n = L.pbl_struct_layout(ctypes.cast(buf, ctypes.c_void_p), cap)
     v = list(buf[:n])
     exp = []
-    for S in (N.BlockBatchC, N.TotalsC, N.DecodeOutC, N.TransformsC):
+    for S in (N.BlockBatchC, N.TotalsC, N.DecodeOutC, N.TransformsC, N.FooterC, N.IndexOutC, N.KvOutC,
+              N.ValueOutC):
         exp.append(ctypes.sizeof(S))
         exp += [getattr(S, f).offset for f, _ in S._fields_]
     assert v == exp

@@ -3,7 +3,10 @@ the oracle and the reference's own SSTs: every stored CRC32C of the three test
 files verifies on the device, corrupted blocks are caught, snappy blocks
 decompress on the device and decode to exactly h.txt's KVs, XXH64 and snappy
 agree with the oracle on random inputs (single-wave LDS path and the >32 KiB
-global path), zstd reports PBL_UNSUPPORTED, corrupt snappy is rejected."""
+global path), corrupt snappy is rejected; zstd blocks (h-zstd-compression-sst)
+decompress on the device to exactly h.txt's KVs, and random zstd frames made
+by facebook/zstd (pyarrow's codec) at levels -5..19 decode to the oracle's
+bytes on both the LDS and the global path, corrupt ones as the oracle says."""
 import os
 import random
 
@@ -118,10 +121,92 @@ def test_decompress_then_decode_is_hamlet(name, golden):
     assert hamlet_kvs(bb) == [tuple(x) for x in golden["hamlet_kvs"]]
 
 
-def test_zstd_unsupported():
-    bb, st = decompress(file_batch("h_zstd"))
-    assert list(st) == [N.PBL_UNSUPPORTED] * len(st)
-    assert list(bb.block_len.cpu().numpy()) == [0] * len(st)
+@pytest.mark.parametrize("name", ["h_zstd"])
+def test_zstd_blocks_decode_to_hamlet(name, golden):
+    bb, st = decompress(file_batch(name))
+    assert list(st) == [0] * bb.n_blocks
+    assert list(bb.block_len.cpu().numpy()) == [b["decompressed_len"] for b in PHYS[name]["blocks"]]
+    assert hamlet_kvs(bb) == [tuple(x) for x in golden["hamlet_kvs"]]
+
+
+def zstd_block(raw: bytes, level: int) -> bytes:
+    """Pebble's zstd block: uvarint decoded length + a zstd frame (zstd_cgo.go:45-66)."""
+    import pyarrow as pa
+    n, pre = len(raw), bytearray()
+    while n >= 0x80:
+        pre.append(n & 0x7F | 0x80)
+        n >>= 7
+    pre.append(n)
+    return bytes(pre) + pa.Codec("zstd", compression_level=level).compress(raw, asbytes=True)
+
+
+def zstd_corpus(rng, i, n):
+    if i % 4 == 0:
+        return rng.randbytes(n)
+    if i % 4 == 1:
+        return bytes([rng.choice(b"xy")]) * n
+    return compressible(rng, n)
+
+
+def test_zstd_random_frames_lds_and_global_paths():
+    rng = random.Random(21)
+    sizes = [1, 2, 5, 64, 65, 1000, 4096, 28000, 32768, 36864, 36865, 40_000, 131_072, 300_000]
+    sizes += [rng.randrange(1, 37_000) for _ in range(120)]
+    raw = [zstd_corpus(rng, i, n) for i, n in enumerate(sizes)]
+    comp = [zstd_block(r, rng.choice([-5, 1, 3, 9, 19])) for r in raw]
+    buf, off, lens = pack_phys(comp, lambda b: 0, rng, indicator=7)
+    bb, st = decompress(PhysBatch.from_host(buf, off, lens))
+    assert list(st) == [0] * len(comp)
+    out, bo, bl = bb.blocks.cpu().numpy(), bb.block_off.cpu().numpy(), bb.block_len.cpu().numpy()
+    for i, want in enumerate(raw):
+        assert bl[i] == len(want), i
+        assert bytes(out[bo[i]: bo[i] + bl[i]]) == want, i
+        if i < 30:
+            assert oracle.zstd_block(comp[i]) == want
+
+
+def test_zstd_mixed_with_snappy_and_raw():
+    rng = random.Random(22)
+    raw = [compressible(rng, rng.randrange(1, 30_000)) for _ in range(60)]
+    blocks, inds = [], []
+    for i, r in enumerate(raw):
+        k = i % 3
+        blocks.append(zstd_block(r, 3) if k == 0 else snappy(r) if k == 1 else r)
+        inds.append(7 if k == 0 else k)
+    it = iter(inds)
+    buf, off, lens = pack_phys(blocks, lambda b: 0, rng, indicator=lambda b: next(it))
+    bb, st = decompress(PhysBatch.from_host(buf, off, lens))
+    assert list(st) == [0] * len(blocks)
+    out, bo, bl = bb.blocks.cpu().numpy(), bb.block_off.cpu().numpy(), bb.block_len.cpu().numpy()
+    for i, want in enumerate(raw):
+        assert bytes(out[bo[i]: bo[i] + bl[i]]) == want, i
+
+
+def test_zstd_corrupt_matches_oracle():
+    rng = random.Random(23)
+    blocks = []
+    for i in range(80):
+        r = zstd_corpus(rng, i % 3 + 1, rng.randrange(1, 30_000))
+        b = bytearray(zstd_block(r, rng.choice([1, 3, 19])))
+        m = i % 5
+        if m == 0:
+            b = b[: rng.randrange(1, len(b))]                  # truncated
+        elif m == 1:
+            b[rng.randrange(4, len(b))] ^= 1 << rng.randrange(8)  # one bit flipped past the length
+        elif m == 2:
+            b = bytearray(b"\xff" * 11)                        # unterminated length varint
+        elif m == 3:
+            b[0] = (b[0] + 1) & 0x7F if b[0] < 0x80 else b[0]   # wrong decoded length
+        blocks.append(bytes(b))
+    buf, off, lens = pack_phys(blocks, lambda b: 0, rng, indicator=7)
+    bb, st = decompress(PhysBatch.from_host(buf, off, lens))
+    out, bo, bl = bb.blocks.cpu().numpy(), bb.block_off.cpu().numpy(), bb.block_len.cpu().numpy()
+    for i, b in enumerate(blocks):
+        want = oracle.zstd_block(b)
+        if isinstance(want, int):
+            assert st[i] in (N.PBL_CORRUPT_COMPRESSION, N.PBL_UNSUPPORTED), (i, st[i], want)
+        else:
+            assert st[i] == 0 and bytes(out[bo[i]: bo[i] + bl[i]]) == want, i
 
 
 def snappy(b: bytes) -> bytes:
