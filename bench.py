@@ -10,7 +10,9 @@ values); `--workload mixed` is config 4's per-GPU shard (128 Ki blocks, even
 ids row / odd ids colblk, 1 Mi blocks over 8 GPUs); `--workload zipf` is
 config 5 per GPU (64 Ki variable-length blocks targeting 32 KiB, Zipf(1.1) key
 lengths 8-1024 B and value lengths 0-64 KiB, `--restart-interval` 1/16/32,
-`--zipf-format row|col`).  With
+`--zipf-format row|col`); `--workload transform` times pbl_transform_batch
+(SyntheticSeqNum + HideObsoletePoints + a 12-byte SyntheticPrefix) over
+config 2 already decoded in HBM.  With
 N > 1 (torch.distributed.run, one rank per GPU, RCCL) every rank decodes its own
 64 Ki-block shard (weak scaling) and each step also performs the offset concat:
 an all-gather of per-rank totals and the rebase of the per-block bases.
@@ -43,7 +45,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", choices=["row", "col", "mixed", "zipf", "cfg1"], default="row")
+    p.add_argument("--workload", choices=["row", "col", "mixed", "zipf", "transform", "cfg1"], default="row")
     p.add_argument("--blocks", type=int, default=0, help="blocks per GPU (0 = the workload's config)")
     p.add_argument("--block-size", type=int, default=32768)
     p.add_argument("--restart-interval", type=int, default=16)
@@ -246,12 +248,15 @@ def main():
     seed = a.seed + 7919 * rank
     t0 = time.time()
     block_fmt = None
-    if a.workload == "row":
+    if a.workload in ("row", "transform"):
         fmt = N.PBL_FMT_ROW
         buf, off, lens, n_kv = gen_row_blocks(seed, nb, a.block_size, a.restart_interval, a.key_len, a.val_len,
                                               a.value_prefix, n_threads=16)
         kernel = {"single": "rowblk_decode_kernel", "flat": "rowblk_flat_kernel"}.get(a.kernel, "rowblk_pipe_kernel")
-        wl = (f"config2: {nb} x {a.block_size // 1024} KiB row-format blocks per GPU, restart interval "
+        if a.workload == "transform":
+            kernel = "tf_count_kernel+tf_scan_kernel+tf_scatter_kernel"
+        wl = ("transform pass (SyntheticSeqNum, HideObsoletePoints, 12 B SyntheticPrefix) over " if a.workload ==
+              "transform" else "") + (f"config2: {nb} x {a.block_size // 1024} KiB row-format blocks per GPU, restart interval "
               f"{a.restart_interval}, {a.key_len} B keys / {a.val_len} B values" + (", value prefix" if a.value_prefix else ""))
     elif a.workload == "col":
         fmt = N.PBL_FMT_COL_CRDB1
@@ -304,9 +309,19 @@ def main():
     h = first.to_host()
     assert h["n_kv"] == n_kv and h["status_mask"] == 0, (h["n_kv"], n_kv, h["status_mask"])
     cap = Capacity(kv=h["n_kv"], key=h["key_bytes_total"], val=h["val_bytes_total"], rst=h["n_restarts"])
-    del first, h
-    out = DecodedBatch.allocate(nb, cap, dev)
     stream = torch.cuda.current_stream(dev)
+    plan = None
+    if a.workload == "transform":
+        # the decoded config-2 batch stays resident; each step transforms it
+        from pebble_amd.transforms import TransformPlan, Transforms
+        plan = TransformPlan(first, Transforms(synthetic_seq_num=12345, hide_obsolete_points=True,
+                                               synthetic_prefix=b"tenant-0042/"), stream)
+        out = plan.out
+        h_in = h
+    else:
+        del first
+        out = DecodedBatch.allocate(nb, cap, dev)
+    del h
     gathered = torch.zeros(world * 4, dtype=torch.int64, device=dev) if world > 1 else None
     if world > 1 and a.dist_backend == "gloo":  # (gloo gathers host tensors)
         gathered = gathered.cpu()
@@ -319,8 +334,14 @@ def main():
         else:
             concat_step(dist, gathered, tot, lambda g: offset_concat(out, g, rank, stream))
 
+    def launch():
+        if plan is not None:
+            plan.launch(stream)
+        else:
+            decode_into(batch, out, stream)
+
     def step():
-        decode_into(batch, out, stream)
+        launch()
         if world > 1:
             concat()
 
@@ -338,7 +359,7 @@ def main():
     t_start = time.perf_counter()
     for i in range(a.steps):
         ev[i][0].record(stream)
-        decode_into(batch, out, stream)
+        launch()
         ev[i][1].record(stream)
         if world > 1:
             concat()
@@ -358,6 +379,8 @@ def main():
     total_input = input_bytes * world
     value = total_input * a.steps / elapsed / 2**30
     ab = alg_bytes(hres, nb, input_bytes)
+    if plan is not None:  # the decoded arrays read once, the transformed ones written once
+        ab = alg_bytes(h_in, nb, 0) + alg_bytes(hres, nb, 0) - 24 * nb
     achieved = ab / (kern_ms * 1e-3) / 1e9
     traffic = None
     tname = ("pmc_traffic.json" if a.workload == "row" else
@@ -390,10 +413,10 @@ def main():
                      "input_GiB_per_s_kernel": round(input_bytes / (kern_ms * 1e-3) / 2**30, 1)},
     }
 
-    if rank == 0 and not a.no_cpu_baseline:
+    if rank == 0 and not a.no_cpu_baseline and plan is None:
         res["cpu_baseline"] = cpu_baseline(a, buf, off, lens, fmt, block_fmt, flags & 0xFF)
 
-    if not a.no_e2e and rank == 0:
+    if not a.no_e2e and rank == 0 and plan is None:
         del out  # (HBM for the pipeline's slots)
         torch.cuda.empty_cache()
         res["e2e_pcie"] = e2e_rate(buf, off, lens, flags & ~N.PBL_BATCH_VARLEN, dev, cap, fmt, block_fmt, hres,

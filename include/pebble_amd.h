@@ -121,6 +121,12 @@ typedef struct pbl_block_batch {
   uint32_t reserved;
   const uint8_t* block_format; /* optional [n_blocks] PBL_FMT_* per block (mixed
                                 row + colblk batches); NULL = `format` for all   */
+  uint64_t synthetic_seq_num;  /* blockiter.SyntheticSeqNum fused into the decode
+                                (transforms.go:90-99; 0 = unset, < 2^56): every
+                                decodable key's trailer becomes seq << 8 | kind
+                                (rowblk_iter.go:1168-1191, data_block.go:1693-
+                                1695); invalid row keys keep the Invalid trailer;
+                                ignored with PBL_ROW_RAW_KEYS                    */
 } pbl_block_batch;
 
 /* ---- batch totals (device struct, written by the decode kernel) -------------- */
@@ -196,7 +202,7 @@ int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stre
 /*
  * Layout of the ABI structs as this library was compiled, for binding checks
  * (ctypes, cgo): writes up to `cap` u64 values and returns how many it has:
- *   sizeof(pbl_block_batch), the offsets of its 8 fields in declaration order,
+ *   sizeof(pbl_block_batch), the offsets of its 9 fields in declaration order,
  *   sizeof(pbl_totals), the offsets of its 8 fields,
  *   sizeof(pbl_decode_out), the offsets of its 20 fields,
  *   then likewise pbl_transforms, pbl_footer, pbl_index_out, pbl_kv_out and

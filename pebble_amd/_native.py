@@ -73,7 +73,7 @@ class BlockBatchC(ctypes.Structure):
         ("blocks", _vp), ("block_off", _vp), ("block_len", _vp),
         ("n_blocks", ctypes.c_uint32), ("format", ctypes.c_uint32),
         ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
-        ("block_format", _vp),
+        ("block_format", _vp), ("synthetic_seq_num", ctypes.c_uint64),
     ]
 
 

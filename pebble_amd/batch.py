@@ -48,6 +48,7 @@ class BlockBatch:
     format: int = N.PBL_FMT_ROW
     flags: int = 0
     block_format: Optional[torch.Tensor] = None  # uint8 [n] per-block PBL_FMT_* (mixed batches)
+    synthetic_seq_num: int = 0  # blockiter.SyntheticSeqNum fused into the decode (0 = unset)
 
     @property
     def n_blocks(self) -> int:
@@ -92,7 +93,8 @@ class BlockBatch:
     def c_struct(self) -> N.BlockBatchC:
         return N.BlockBatchC(self.blocks.data_ptr(), self.block_off.data_ptr(), self.block_len.data_ptr(),
                              self.n_blocks, self.format, self.flags, 0,
-                             self.block_format.data_ptr() if self.block_format is not None else None)
+                             self.block_format.data_ptr() if self.block_format is not None else None,
+                             self.synthetic_seq_num)
 
     def input_bytes(self) -> int:
         return int(self.block_len.to(torch.int64).sum().item()) if self.n_blocks else 0

@@ -247,7 +247,7 @@ __device__ __forceinline__ void col_emit_rows(CLds& L, const Slot& E, const Args
     const uint32_t v = vo.w ? uint32_t(S.le(vo.at + r * vo.w, vo.w)) : 0;
     val_off[kvb + b + r] = v - d.v_lo;
     if (r < rows) {
-      trailer[kvb + r] = u_at<F>(S, d.trailers, r);
+      trailer[kvb + r] = with_seq(u_at<F>(S, d.trailers, r), A.in.synthetic_seq_num, 0u);
       if (O.kv_flags) {
         uint8_t fl = 0;
         if (d.pc_at && ((S.le(d.pc_at + 8 * (r >> 6), 8) >> (r & 63)) & 1)) fl |= PBL_KV_PREFIX_CHANGED;

@@ -42,6 +42,17 @@ constexpr int kLbWin = PBL_LB_WIN;
 // R2 granules).  A resolve normally costs ONE round trip: the windows of
 // predecessor records carry packed inclusive prefixes, so the nearest one ends
 // the walk without a second fetch.
+constexpr uint64_t kKindInvalidTrailer = 191u;  // base.InternalKeyKindInvalid, seq 0
+
+// blockiter.SyntheticSeqNum fused into the decode (pbl_block_batch.
+// synthetic_seq_num, 0 = unset): SetSeqNum on every decodable key after the
+// obsolete bit is masked (rowblk_iter.go:1168-1191; colblk data_block.go:
+// 1693-1695).  An invalid row key keeps the Invalid trailer (its kind byte has
+// bit 7 set, which no masked trailer has); raw-key batches carry no seqnums.
+__device__ __forceinline__ uint64_t with_seq(uint64_t tr, uint64_t seq, uint32_t flags) {
+  return (seq && !(flags & PBL_ROW_RAW_KEYS) && tr != kKindInvalidTrailer) ? (seq << 8) | (tr & 0xff) : tr;
+}
+
 constexpr uint64_t kWsHeader = 256;
 constexpr int kWsBigCount = 1;  // header u32 [1]: blocks past the LDS stage (row pipeline)
 constexpr int kWsColTick = 2;   // header u32 [2]: the colblk queue's ticket counter (mixed batches)

@@ -42,7 +42,7 @@ constexpr uint32_t kMaxFastKeyBytes = 65535;  // user-key bytes per block on the
 constexpr int kBkt = 256;                 // bytes per output bucket of the granule -> KV index
 constexpr uint32_t kRestartMask = 0x7fffffffu;
 constexpr uint64_t kTrailerObsoleteMask = ((((uint64_t)1 << 56) - 1) << 8) | 191u;
-constexpr uint64_t kKindInvalid = 191u;
+constexpr uint64_t kKindInvalid = kKindInvalidTrailer;
 
 // aux (u16) area: run-walk slots, per-run prefixes, output buckets
 constexpr int kSlotPos = 0;                          // [kKvCap] entry offset of slot q
@@ -592,7 +592,7 @@ __device__ __forceinline__ void row_process(Lds& s, const Args& A, const uint32_
     uint32_t status = PBL_OK;
     if (wave_id() == 0) {
       uint64_t dummy[kNumComp] = {0, 0, 0, 0};
-      slow_walk(src, fits, blen, flags, keybuf, keycap, 0, A.out, b, dummy, &ss);
+      slow_walk(src, fits, blen, flags, A.in.synthetic_seq_num, keybuf, keycap, 0, A.out, b, dummy, &ss);
       bool ok = ss.status == PBL_OK;
       agg[0] = ok ? ss.nkv : 0;
       agg[1] = ok ? ss.kb : 0;
@@ -610,7 +610,7 @@ __device__ __forceinline__ void row_process(Lds& s, const Args& A, const uint32_
     }
     if (wave_id() != 0) return;
     if (status == PBL_OK) {
-      slow_walk(src, fits, blen, flags, keybuf, keycap, 1, A.out, b, excl, &ss);
+      slow_walk(src, fits, blen, flags, A.in.synthetic_seq_num, keybuf, keycap, 1, A.out, b, excl, &ss);
     } else if (lane_id() == 0 && O.key_off && excl[0] + b < O.kv_cap + nb) {
       O.key_off[excl[0] + b] = 0;
       O.val_off[excl[0] + b] = 0;
@@ -711,7 +711,7 @@ __device__ __forceinline__ void row_process(Lds& s, const Args& A, const uint32_
     O.val_off[o] = s.vout[j];
     if (j < nkv) {
       uint8_t fl = s.kvf[j];
-      O.trailer[kvb + j] = entry_trailer(s, V, j, &fl, flags);
+      O.trailer[kvb + j] = with_seq(entry_trailer(s, V, j, &fl, flags), A.in.synthetic_seq_num, flags);
       if (O.kv_flags) O.kv_flags[kvb + j] = fl;
       if (O.entry_off) O.entry_off[kvb + j] = s.eoff[j];
     }
@@ -1169,7 +1169,7 @@ uint64_t pbl_workspace_bytes(uint32_t n_blocks) { return pbl::ws_alloc_bytes(n_b
 int pbl_decode_batch_colblk(const pbl_block_batch* batch, pbl_decode_out* out, void* stream);
 
 int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stream) {
-  if (!batch || !out) return PBL_INVALID_ARG;
+  if (!batch || !out || (batch->synthetic_seq_num >> 56)) return PBL_INVALID_ARG;  // (base.SeqNumMax)
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (!out->totals || !out->blk_kv_base || !out->blk_key_base || !out->blk_val_base || !out->blk_status)
     return PBL_INVALID_ARG;
@@ -1221,7 +1221,7 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
 }
 
 int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stream) {
-  if (!batch || !out) return PBL_INVALID_ARG;
+  if (!batch || !out || (batch->synthetic_seq_num >> 56)) return PBL_INVALID_ARG;
   if (!out->totals || !out->blk_kv_base || !out->blk_key_base || !out->blk_val_base || !out->blk_status)
     return PBL_INVALID_ARG;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -1284,6 +1284,7 @@ size_t pbl_struct_layout(uint64_t* out, size_t cap) {
       sizeof(pbl_block_batch), PBL_OFF(pbl_block_batch, blocks), PBL_OFF(pbl_block_batch, block_off),
       PBL_OFF(pbl_block_batch, block_len), PBL_OFF(pbl_block_batch, n_blocks), PBL_OFF(pbl_block_batch, format),
       PBL_OFF(pbl_block_batch, flags), PBL_OFF(pbl_block_batch, reserved), PBL_OFF(pbl_block_batch, block_format),
+      PBL_OFF(pbl_block_batch, synthetic_seq_num),
       sizeof(pbl_totals), PBL_OFF(pbl_totals, n_kv), PBL_OFF(pbl_totals, key_bytes), PBL_OFF(pbl_totals, val_bytes),
       PBL_OFF(pbl_totals, n_restarts), PBL_OFF(pbl_totals, status_mask), PBL_OFF(pbl_totals, n_bad_blocks),
       PBL_OFF(pbl_totals, n_slow_blocks), PBL_OFF(pbl_totals, pad),

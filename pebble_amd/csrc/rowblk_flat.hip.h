@@ -495,20 +495,20 @@ __device__ __forceinline__ void flat_block(WSlot& M, const Args& A, uint32_t b) 
     bool from_lds = true;
     uint8_t* keybuf = reinterpret_cast<uint8_t*>(M.m0);
     uint32_t keycap = uint32_t(sizeof(WSlot) - offsetof(WSlot, m0)) & ~15u;
-    slow_walk(src, true, blen, flags, keybuf, keycap, kPassCount, A.out, b, dummy, &ss);
+    slow_walk(src, true, blen, flags, A.in.synthetic_seq_num, keybuf, keycap, kPassCount, A.out, b, dummy, &ss);
     if (ss.status == PBL_UNSUPPORTED) {
       from_lds = false;
       src = gblk;
       keybuf = reinterpret_cast<uint8_t*>(M.x);
       keycap = uint32_t(kLdsBlkBytes);
-      slow_walk(src, false, blen, flags, keybuf, keycap, kPassCount, A.out, b, dummy, &ss);
+      slow_walk(src, false, blen, flags, A.in.synthetic_seq_num, keybuf, keycap, kPassCount, A.out, b, dummy, &ss);
     }
     const bool okk = ss.status == PBL_OK;
     const uint64_t agg[kNumComp] = {okk ? ss.nkv : 0, okk ? ss.kb : 0, okk ? ss.vb : 0, okk ? ss.nr : 0};
     lookback(lb_state, nb, b, agg, excl, &A.out.totals->status_mask);
     uint32_t st2 = ss.status;
     if (okk && overflows(A.out, excl, agg)) st2 = PBL_OVERFLOW;
-    if (st2 == PBL_OK) slow_walk(src, from_lds, blen, flags, keybuf, keycap, kPassAll, A.out, b, excl, &ss);
+    if (st2 == PBL_OK) slow_walk(src, from_lds, blen, flags, A.in.synthetic_seq_num, keybuf, keycap, kPassAll, A.out, b, excl, &ss);
     else if (l == 0 && A.out.key_off && excl[0] + b < A.out.kv_cap + nb) {
       to_glb(A.out.key_off)[excl[0] + b] = 0;
       to_glb(A.out.val_off)[excl[0] + b] = 0;
@@ -561,7 +561,7 @@ __device__ __forceinline__ void flat_block(WSlot& M, const Args& A, uint32_t b) 
         const uint64_t m = M.m0[j];
         uint8_t fl = M.kvf[j];
 #ifndef PBL_FLAT_EXP_NOARR
-        to_glb(O.trailer)[kvb + j] = f_trailer(M, V, int(j), m, &fl, flags);
+        to_glb(O.trailer)[kvb + j] = with_seq(f_trailer(M, V, int(j), m, &fl, flags), A.in.synthetic_seq_num, flags);
         if (O.kv_flags) to_glb(O.kv_flags)[kvb + j] = fl;
         if (O.entry_off) to_glb(O.entry_off)[kvb + j] = M.eoff[j];
 #else

@@ -99,7 +99,7 @@ enum { kPassCount = 0, kPassAll = 1 };
 
 // U: value granules per lane in flight.
 template <class Src, int U>
-__device__ __forceinline__ void slow_walk_t(const Src S, uint64_t len, uint32_t flags, lptr<uint8_t> kbuf,
+__device__ __forceinline__ void slow_walk_t(const Src S, uint64_t len, uint32_t flags, uint64_t seq, lptr<uint8_t> kbuf,
                                             uint32_t keycap, int pass, const pbl_decode_out& O, uint32_t b,
                                             const uint64_t bases[kNumComp], SlowState* st) {
   const int l = lane_id();
@@ -178,7 +178,7 @@ __device__ __forceinline__ void slow_walk_t(const Src S, uint64_t len, uint32_t 
       }
       const uint64_t kv = bases[0] + nkv, o = bases[0] + b + nkv;
       if (l == 0) {
-        o_trailer[kv] = trailer;
+        o_trailer[kv] = with_seq(trailer, seq, flags);
         if (O.kv_flags) o_flags[kv] = fl;
         if (O.entry_off) o_entry[kv] = uint32_t(offset);
         o_koff[o] = uint32_t(kb);
@@ -231,7 +231,7 @@ __device__ __forceinline__ void slow_walk_t(const Src S, uint64_t len, uint32_t 
 
 // blk: the block's first byte, in LDS (staged, blk_lds) or global memory;
 // keybuf: LDS (dword aligned) of keycap bytes.
-__device__ __noinline__ void slow_walk(const uint8_t* blk, bool blk_lds, uint64_t len, uint32_t flags,
+__device__ __noinline__ void slow_walk(const uint8_t* blk, bool blk_lds, uint64_t len, uint32_t flags, uint64_t seq,
                                        uint8_t* keybuf, uint32_t keycap, int pass, const pbl_decode_out O,
                                        uint32_t b, const uint64_t* bases_p, SlowState* st) {
   const uint64_t bases[kNumComp] = {bases_p[0], bases_p[1], bases_p[2], bases_p[3]};
@@ -242,9 +242,9 @@ __device__ __noinline__ void slow_walk(const uint8_t* blk, bool blk_lds, uint64_
     const uint32_t a = uint32_t(uint64_t(to_lds_ptr(blk)));
     const uint32_t base = 16u + (a & 15u);
     slow_walk_t<SlowLds, PBL_SLOW_U>(SlowLds{lds_view(reinterpret_cast<const void*>(blk - base), base)}, len, flags,
-                                     kbuf, keycap, pass, O, b, bases, st);
+                                     seq, kbuf, keycap, pass, O, b, bases, st);
   } else {
-    slow_walk_t<SlowGlb, PBL_SLOW_U>(SlowGlb{to_glb(blk), len}, len, flags, kbuf, keycap, pass, O, b, bases, st);
+    slow_walk_t<SlowGlb, PBL_SLOW_U>(SlowGlb{to_glb(blk), len}, len, flags, seq, kbuf, keycap, pass, O, b, bases, st);
   }
 }
 

@@ -4,7 +4,9 @@ data: 64 Ki x 32 KiB row blocks with 5-byte trailers.  The trailers' checksums
 are produced by the device itself (a first verify pass reports `computed`,
 which is written into the trailers; the timed passes then verify them all OK).
 Snappy: the same blocks compressed on the host (pyarrow), decompressed on the
-device.  Prints one JSON line.  Usage: bench_physical.py [n_blocks] [reps]"""
+device; also a text-like corpus (~2x for snappy) and zstd (level 3, Pebble's
+uvarint length prefix) on both.  Prints one JSON line.
+Usage: bench_physical.py [n_blocks] [reps] [codecs, e.g. snappy,zstd]"""
 import json
 import os
 import sys
@@ -59,30 +61,78 @@ for name, ct in (("crc32c", N.PBL_CHECKSUM_CRC32C), ("xxhash64", N.PBL_CHECKSUM_
                                                       _stream_handle(None)))
     res[name] = {"GB_per_s": round((int(lens.sum()) + nb) / sec / 1e9, 1), "ms": round(sec * 1e3, 3)}
 
-import pyarrow as pa  # noqa: E402
-codec = pa.Codec("snappy")
-comp = [codec.compress(buf[int(o):int(o) + int(ln)].tobytes(), asbytes=True) for o, ln in zip(off, lens)]
-cl = np.array([len(x) for x in comp], np.uint32)
-coff = np.zeros(nb, np.uint64)
-coff[1:] = np.cumsum((cl.astype(np.uint64) + 5 + 7) // 8 * 8)[:-1]
-cbuf = np.zeros(int(coff[-1]) + int(cl[-1]) + 32, np.uint8)
-for i, x in enumerate(comp):
-    cbuf[int(coff[i]):int(coff[i]) + len(x)] = np.frombuffer(x, np.uint8)
-    cbuf[int(coff[i]) + len(x)] = 1  # snappy indicator
-pb = PhysBatch.from_host(cbuf, coff, cl)
-bb, st = decompress(pb)
-assert not st.any() and int(bb.block_len.to(torch.int64).sum()) == int(lens.sum())
-assert np.array_equal(bb.blocks[: int(lens[0])].cpu().numpy(), buf[: int(lens[0])])
 import ctypes  # noqa: E402
+
+import pyarrow as pa  # noqa: E402
+
 from pebble_amd.batch import _stream_handle  # noqa: E402
-c = pb.c_struct()
-o_len = torch.empty(nb, dtype=torch.int32, device="cuda")
-o_st = torch.empty(nb, dtype=torch.int32, device="cuda")
-cap = bb.block_len.clone()
-sec = timed(lambda: N.lib().pbl_decompress_blocks(ctypes.byref(c), ctypes.c_void_p(bb.blocks.data_ptr()),
-                                                  ctypes.c_void_p(bb.block_off.data_ptr()),
-                                                  ctypes.c_void_p(cap.data_ptr()), ctypes.c_void_p(o_len.data_ptr()),
-                                                  ctypes.c_void_p(o_st.data_ptr()), _stream_handle(None)))
-res["snappy"] = {"decoded_GB_per_s": round(int(lens.sum()) / sec / 1e9, 1), "ms": round(sec * 1e3, 3),
-                 "compressed_bytes": int(cl.sum()), "ratio": round(float(lens.sum()) / float(cl.sum()), 2)}
+
+
+def uvarint(n):
+    out = bytearray()
+    while n >= 0x80:
+        out.append(n & 0x7F | 0x80)
+        n >>= 7
+    out.append(n)
+    return bytes(out)
+
+
+def words_blocks(n_distinct=256, vocab=512, seed=5):
+    """Text-like 32 KiB blocks (a 512-word vocabulary: snappy ~2x, zstd ~3x)."""
+    rng = np.random.default_rng(seed)
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789", np.uint8)
+    words = [bytes(alpha[rng.integers(0, len(alpha), int(k))]) + b" " for k in rng.integers(2, 9, vocab)]
+    out = []
+    for _ in range(n_distinct):
+        ids = rng.integers(0, vocab, 8000)
+        out.append(b"".join(words[i] for i in ids)[:32768])
+    return out
+
+
+def codec_run(raw_blocks, codec, n):
+    """Compress the distinct raw blocks (zstd with Pebble's uvarint prefix),
+    lay out n physical blocks cycling through them, decompress on the device
+    (checked), time pbl_decompress_blocks."""
+    ind = 1 if codec == "snappy" else 7
+    c = pa.Codec(codec) if codec == "snappy" else pa.Codec("zstd", compression_level=3)
+    comp = [c.compress(b, asbytes=True) if codec == "snappy" else uvarint(len(b)) + c.compress(b, asbytes=True)
+            for b in raw_blocks]
+    k = len(comp)
+    cl = np.array([len(comp[i % k]) for i in range(n)], np.uint32)
+    coff = np.zeros(n, np.uint64)
+    coff[1:] = np.cumsum((cl.astype(np.uint64) + 5 + 7) // 8 * 8)[:-1]
+    cbuf = np.zeros(int(coff[-1]) + int(cl[-1]) + 32, np.uint8)
+    for i in range(n):
+        x = comp[i % k]
+        cbuf[int(coff[i]):int(coff[i]) + len(x)] = np.frombuffer(x, np.uint8)
+        cbuf[int(coff[i]) + len(x)] = ind
+    pb = PhysBatch.from_host(cbuf, coff, cl)
+    bb, st = decompress(pb)
+    raw_total = sum(len(raw_blocks[i % k]) for i in range(n))
+    assert not st.any() and int(bb.block_len.to(torch.int64).sum()) == raw_total, (codec, st[:8])
+    out = bb.blocks.cpu().numpy()
+    bo, bl = bb.block_off.cpu().numpy(), bb.block_len.cpu().numpy()
+    for i in list(range(min(n, 64))) + [n - 1]:
+        assert out[bo[i]:bo[i] + bl[i]].tobytes() == raw_blocks[i % k], (codec, i)
+    cs = pb.c_struct()
+    o_len = torch.empty(n, dtype=torch.int32, device="cuda")
+    o_st = torch.empty(n, dtype=torch.int32, device="cuda")
+    cap = bb.block_len.clone()
+    sec = timed(lambda: N.lib().pbl_decompress_blocks(ctypes.byref(cs), ctypes.c_void_p(bb.blocks.data_ptr()),
+                                                      ctypes.c_void_p(bb.block_off.data_ptr()),
+                                                      ctypes.c_void_p(cap.data_ptr()),
+                                                      ctypes.c_void_p(o_len.data_ptr()),
+                                                      ctypes.c_void_p(o_st.data_ptr()), _stream_handle(None)))
+    return {"decoded_GB_per_s": round(raw_total / sec / 1e9, 1), "ms": round(sec * 1e3, 3),
+            "decoded_bytes": raw_total, "compressed_bytes": int(cl.sum()),
+            "ratio": round(raw_total / float(cl.sum()), 2), "distinct_blocks": k}
+
+
+cfg2 = [buf[int(o):int(o) + int(ln)].tobytes() for o, ln in zip(off, lens)]
+codecs = sys.argv[3].split(",") if len(sys.argv) > 3 else ["snappy", "zstd"]
+words = words_blocks()
+for codec in codecs:
+    # config-2 blocks (random values: ratio ~1.0) and text-like blocks (ratio ~2-3)
+    res[codec] = codec_run(cfg2 if codec == "snappy" else cfg2[:4096], codec, nb)
+    res[codec + "_words"] = codec_run(words, codec, nb)
 print(json.dumps(res), flush=True)

@@ -51,6 +51,17 @@ else:
     buf, off, lens, n = gen_row_blocks(42, nb, 32768, 16, 16, 100, n_threads=16)
     b = BlockBatch.from_host(buf, off, lens, "cuda")
 b.flags |= int(os.environ.get("PROF_FLAGS", "0"), 0)  # e.g. PBL_KERNEL_FLAT (0x800) for A/B profiles
+if workload == "transform":
+    # the config-2 batch decoded once, then transformed `iters` times
+    from pebble_amd.transforms import TransformPlan, Transforms
+    d = decode(b)
+    plan = TransformPlan(d, Transforms(synthetic_seq_num=12345, hide_obsolete_points=True,
+                                       synthetic_prefix=b"tenant-0042/"))
+    for _ in range(iters):
+        plan.launch()
+    torch.cuda.synchronize()
+    print("ok", n)
+    sys.exit(0)
 h = decode(b).to_host()
 out = DecodedBatch.allocate(nb, Capacity(h["n_kv"], h["key_bytes_total"], h["val_bytes_total"], h["n_restarts"]),
                             "cuda")

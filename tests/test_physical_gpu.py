@@ -172,7 +172,7 @@ def test_zstd_mixed_with_snappy_and_raw():
     for i, r in enumerate(raw):
         k = i % 3
         blocks.append(zstd_block(r, 3) if k == 0 else snappy(r) if k == 1 else r)
-        inds.append(7 if k == 0 else k)
+        inds.append(7 if k == 0 else 1 if k == 1 else 0)
     it = iter(inds)
     buf, off, lens = pack_phys(blocks, lambda b: 0, rng, indicator=lambda b: next(it))
     bb, st = decompress(PhysBatch.from_host(buf, off, lens))

@@ -1,7 +1,8 @@
 """Whole tables through the device (pebble_amd/sstable.py): footer -> index
 blocks (physical step + decode + pbl_index_handles_row, one or two levels) ->
 data-block handles as device arrays -> checksums, decompression, decode; the
-handles equal the fixture's independent walk and the KVs equal h.txt.  Columnar
+handles equal the fixture's independent walk and the KVs equal h.txt (the
+zstd-compressed table too: its index and data blocks decompress on the device).  Columnar
 index blocks (pbl_index_handles_col) against the reference's index_block dumps
 and the oracle, with corrupt blocks and a capacity overflow."""
 import json
@@ -27,7 +28,7 @@ def table(name):
     return Table(open(os.path.join(GOLDEN, "sst", FIX["tables"][name]["file"]), "rb").read())
 
 
-@pytest.mark.parametrize("name", ["hamlet_snappy", "h_no_compression", "h_two_level"])
+@pytest.mark.parametrize("name", ["hamlet_snappy", "h_no_compression", "h_two_level", "h_zstd"])
 def test_tables_decode_to_hamlet(name, golden):
     t = table(name)
     assert t.footer.index == tuple(FIX["tables"][name]["index"])
@@ -41,12 +42,6 @@ def test_tables_decode_to_hamlet(name, golden):
     for b in range(len(got)):
         kvs += kvs_of_block(r, b)
     assert [(kv.user_key.decode(), kv.value.decode()) for kv in kvs] == [tuple(x) for x in golden["hamlet_kvs"]]
-
-
-def test_zstd_table_reports_unsupported():
-    t = table("h_zstd")
-    with pytest.raises(Exception, match="UNSUPPORTED"):
-        t.data_block_handles()
 
 
 def test_corrupt_table_block_is_caught():
