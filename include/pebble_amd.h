@@ -435,9 +435,13 @@ uint64_t pbl_transform_workspace_bytes(uint32_t n_blocks);
  * stay PBL_KV_INVALID_KEY are empty and keep the Invalid trailer.  Restart words
  * are the input's; statuses too, except a row block whose transformed iteration
  * would panic (a key made valid by the prefix, kind SET, empty value, value
- * prefix on): PBL_CORRUPT_BOUNDS.  A block whose decode failed stays failed.  Three stream-ordered launches (count, scan, scatter); on a
- * capacity overflow every decodable block reports PBL_OVERFLOW and only sizes
- * are written.  Replaces the iteration-time transforms of rowblk.Iter
+ * prefix on): PBL_CORRUPT_BOUNDS.  A block whose decode failed stays failed.
+ * Keys and values are copied in 16-byte chunks: in->key_bytes, in->val_bytes,
+ * t->prefix and t->suffix must be readable 16 bytes past their capacity /
+ * length (pebble_amd's allocations pad them).  A workspace memset and three
+ * stream-ordered launches (count; scan: tiles of 1024 blocks with decoupled
+ * look-back; scatter); on a capacity overflow every decodable block reports
+ * PBL_OVERFLOW and only sizes are written.  Replaces the iteration-time transforms of rowblk.Iter
  * (rowblk_iter.go:400,487-517,1168-1187) and colblk.DataBlockIter
  * (data_block.go:1299-1303,1437-1462,1680-1697) for a whole batch.
  */

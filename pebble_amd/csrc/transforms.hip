@@ -26,7 +26,14 @@
 namespace pbl {
 namespace tf {
 
-constexpr int kTfWs = 64;  // workspace header: overflow flag
+// Workspace: [0, 64) header (u32 overflow flag, u32 tile ticket), then the
+// tile look-back state (tf_scan_kernel, 80 B per tile), then 4 u32 counts per
+// block (tf_count_kernel).  The header and the look-back state are zeroed per launch.
+constexpr int kTfWs = 64;
+constexpr uint32_t kTfTile = 1024;  // blocks per scan tile (256 threads x 4)
+__host__ __device__ inline uint64_t tf_tiles(uint32_t nb) { return (uint64_t(nb) + kTfTile - 1) / kTfTile; }
+__host__ __device__ inline uint64_t tf_lb_bytes(uint32_t nb) { return 80ull * tf_tiles(nb); }
+__host__ __device__ inline uint64_t tf_cnt_offset(uint32_t nb) { return kTfWs + tf_lb_bytes(nb); }
 constexpr uint64_t kTfMask = ((1ull << 56) - 1) << 8 | 191u;  // TrailerObsoleteMask (rowblk_writer.go:30-42)
 constexpr uint64_t kTfInvalid = 191u;                          // InternalKeyKindInvalid
 
@@ -197,7 +204,7 @@ __device__ inline KvView kv_view(const TfArgs& A, uint32_t b, uint64_t kv0, uint
 }
 
 __global__ void __launch_bounds__(kTPB) tf_count_kernel(TfArgs A) {
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(A.out.workspace) + kTfWs);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(A.out.workspace) + tf_cnt_offset(A.n_blocks));
   const uint32_t lane = lane_id();
   const uint32_t wpb = kTPB / kWave;
   for (uint32_t b = blockIdx.x * wpb + wave_id(); b < A.n_blocks; b += gridDim.x * wpb) {
@@ -229,78 +236,155 @@ __global__ void __launch_bounds__(kTPB) tf_count_kernel(TfArgs A) {
   }
 }
 
-// One workgroup of kTPB threads; thread t scans a contiguous chunk of blocks.
+// Tiles of kTfTile blocks, one workgroup each, in ticket order: the tile's
+// counts are loaded (4 blocks per thread), scanned in the workgroup, the tile's
+// aggregate {KVs, key bytes, value bytes, newly corrupt blocks} published and
+// its exclusive prefix resolved by decoupled look-back; then every block's
+// bases and status.  The last tile writes the batch totals and the overflow
+// flag (the scatter turns OK blocks into PBL_OVERFLOW when it is set).
 __global__ void __launch_bounds__(kTPB) tf_scan_kernel(TfArgs A) {
-  __shared__ uint64_t part[3][kTPB];
-  __shared__ uint32_t n_new_bad;
-  const uint32_t* cnt = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(A.out.workspace) + kTfWs);
-  uint32_t* flag = reinterpret_cast<uint32_t*>(A.out.workspace);
-  const uint32_t nb = A.n_blocks, t = threadIdx.x;
-  const uint32_t chunk = (nb + kTPB - 1) / kTPB, b0 = min(nb, t * chunk), b1 = min(nb, b0 + chunk);
-  uint64_t s[3] = {0, 0, 0};
-  uint32_t nbad = 0;
-  if (t == 0) n_new_bad = 0;
-  for (uint32_t b = b0; b < b1; b++) {
-    for (int q = 0; q < 3; q++) s[q] += cnt[4 * uint64_t(b) + q];
-    nbad += cnt[4 * uint64_t(b) + 3];
-  }
-  for (int q = 0; q < 3; q++) part[q][t] = s[q];
-  __syncthreads();
-  if (nbad) atomicAdd(&n_new_bad, nbad);
-  if (t < 3) {  // serial scan of the kTPB chunk sums (one lane per component)
-    uint64_t acc = 0;
-    for (uint32_t i = 0; i < kTPB; i++) {
-      const uint64_t x = part[t][i];
-      part[t][i] = acc;
-      acc += x;
-    }
-  }
-  __syncthreads();
+  __shared__ uint32_t s_tile;
+  __shared__ uint64_t s_wsum[kTPB / kWave][4];
+  __shared__ uint64_t s_excl[4];
+  uint8_t* ws = reinterpret_cast<uint8_t*>(A.out.workspace);
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(ws);
+  uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kTfWs);
+  const uint4* cnt4 = reinterpret_cast<const uint4*>(ws + tf_cnt_offset(A.n_blocks));
+  const uint32_t nb = A.n_blocks, nt = uint32_t(tf_tiles(nb)), t = threadIdx.x;
   const pbl_decode_out& I = A.in;
   const pbl_decode_out& O = A.out;
-  uint64_t e[3] = {part[0][t], part[1][t], part[2][t]};
-  for (uint32_t b = b0; b < b1; b++) {
-    to_glb(O.blk_kv_base)[b] = e[0];
-    to_glb(O.blk_key_base)[b] = e[1];
-    to_glb(O.blk_val_base)[b] = e[2];
-    if (O.blk_rst_base) to_glb(O.blk_rst_base)[b] = to_glb(I.blk_rst_base)[b];
-    for (int q = 0; q < 3; q++) e[q] += cnt[4 * uint64_t(b) + q];
-  }
-  if (t == kTPB - 1) {
-    const uint64_t nr = to_glb(I.blk_rst_base)[nb];
-    to_glb(O.blk_kv_base)[nb] = e[0];
-    to_glb(O.blk_key_base)[nb] = e[1];
-    to_glb(O.blk_val_base)[nb] = e[2];
-    if (O.blk_rst_base) to_glb(O.blk_rst_base)[nb] = nr;
-    const bool over = e[0] > O.kv_cap || e[1] > O.key_cap || e[2] > O.val_cap || (O.restarts && nr > O.rst_cap);
-    pbl_totals to = *I.totals;  // (one thread: a generic access is fine here)
-    to.n_kv = e[0];
-    to.key_bytes = e[1];
-    to.val_bytes = e[2];
-    to.n_restarts = nr;
-    if (over) to.status_mask |= 1u << PBL_OVERFLOW;
-    if (n_new_bad) {  // row blocks whose transformed iteration would panic
-      to.status_mask |= 1u << PBL_CORRUPT_BOUNDS;
-      to.n_bad_blocks += n_new_bad;
+  for (;;) {
+    if (t == 0) s_tile = g_atomic_add(hdr + 1, 1u);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    __syncthreads();  // (s_tile is rewritten next iteration)
+    if (tile >= nt) return;
+    const uint32_t b0 = tile * kTfTile + 4 * t;
+    uint4 c[4];
+    uint64_t s4[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      c[k] = make_uint4(0, 0, 0, 0);
+      if (b0 + k < nb) c[k] = cnt4[b0 + k];
+      s4[0] += c[k].x;
+      s4[1] += c[k].y;
+      s4[2] += c[k].z;
+      s4[3] += c[k].w;
     }
-    *O.totals = to;
-    *to_glb(flag) = over ? 1u : 0u;
+    // workgroup exclusive scan of the per-thread sums
+    uint64_t in4[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) in4[q] = wave_incl_scan(s4[q]);
+    if (lane_id() == kWave - 1)
+      for (int q = 0; q < 4; q++) s_wsum[wave_id()][q] = in4[q];
+    __syncthreads();
+    uint64_t before[4] = {0, 0, 0, 0}, agg[4] = {0, 0, 0, 0};
+    for (int w = 0; w < kTPB / kWave; w++)
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        if (w < wave_id()) before[q] += s_wsum[w][q];
+        agg[q] += s_wsum[w][q];
+      }
+    if (wave_id() == 0) {
+      uint64_t excl[4];
+      lb_publish(lb_state, nt, tile, agg);
+      lb_resolve(lb_state, nt, tile, agg, excl, &O.totals->status_mask);
+      if (lane_id() == 0)
+        for (int q = 0; q < 4; q++) s_excl[q] = excl[q];
+    }
+    __syncthreads();
+    uint64_t e[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) e[q] = s_excl[q] + before[q] + in4[q] - s4[q];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t b = b0 + k;
+      if (b < nb) {
+        to_glb(O.blk_kv_base)[b] = e[0];
+        to_glb(O.blk_key_base)[b] = e[1];
+        to_glb(O.blk_val_base)[b] = e[2];
+        if (O.blk_rst_base) to_glb(O.blk_rst_base)[b] = to_glb(I.blk_rst_base)[b];
+        uint32_t st = to_glb(I.blk_status)[b];
+        if (st == PBL_OK && c[k].w) st = PBL_CORRUPT_BOUNDS;
+        to_glb(O.blk_status)[b] = st;
+        e[0] += c[k].x;
+        e[1] += c[k].y;
+        e[2] += c[k].z;
+      }
+    }
+    if (tile == nt - 1 && t == 0) {
+      uint64_t tot[4];
+      for (int q = 0; q < 4; q++) tot[q] = s_excl[q] + agg[q];
+      const uint64_t nr = to_glb(I.blk_rst_base)[nb];
+      to_glb(O.blk_kv_base)[nb] = tot[0];
+      to_glb(O.blk_key_base)[nb] = tot[1];
+      to_glb(O.blk_val_base)[nb] = tot[2];
+      if (O.blk_rst_base) to_glb(O.blk_rst_base)[nb] = nr;
+      const bool over = tot[0] > O.kv_cap || tot[1] > O.key_cap || tot[2] > O.val_cap || (O.restarts && nr > O.rst_cap);
+      pbl_totals to = *I.totals;  // (one thread: a generic access is fine here)
+      to.n_kv = tot[0];
+      to.key_bytes = tot[1];
+      to.val_bytes = tot[2];
+      to.n_restarts = nr;
+      if (over) to.status_mask |= 1u << PBL_OVERFLOW;
+      if (tot[3]) {  // row blocks whose transformed iteration would panic
+        to.status_mask |= 1u << PBL_CORRUPT_BOUNDS;
+        to.n_bad_blocks += uint32_t(tot[3]);
+      }
+      if (over) to.n_bad_blocks = nb;  // (every block is now OVERFLOW or bad)
+      to.status_mask |= __hip_atomic_load(&O.totals->status_mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *O.totals = to;
+      __hip_atomic_store(hdr, over ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
-  __syncthreads();
-  // statuses: the decode's, PBL_OVERFLOW for the blocks that would have been written
-  const bool over = *to_glb(flag) != 0;
-  for (uint32_t b = b0; b < b1; b++) {
-    uint32_t st = to_glb(I.blk_status)[b];
-    if (st == PBL_OK && cnt[4 * uint64_t(b) + 3]) st = PBL_CORRUPT_BOUNDS;
-    if (over && st == PBL_OK) st = PBL_OVERFLOW;
-    to_glb(O.blk_status)[b] = st;
+}
+
+// dst[0, n) = src[0, n) by 16-B chunks (unaligned global loads / stores; the
+// sources are readable 15 bytes past their end), exact at the tail.
+typedef u32x4 u32x4_u __attribute__((aligned(1)));
+typedef uint64_t u64_u __attribute__((aligned(1)));
+typedef uint32_t u32_u __attribute__((aligned(1)));
+typedef uint16_t u16_u __attribute__((aligned(1)));
+__device__ __forceinline__ void copy_chunks(gptr<uint8_t> dst, gptr<const uint8_t> src, uint32_t n) {
+  uint32_t c = 0;
+  for (; c + 64 <= n; c += 64) {
+    u32x4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) x[u] = *(gptr<const u32x4_u>)(src + c + 16 * u);
+#pragma unroll
+    for (int u = 0; u < 4; u++) *(gptr<u32x4_u>)(dst + c + 16 * u) = x[u];
   }
-  if (over && t == 0) to_glb(O.totals)->n_bad_blocks = nb;  // (every block is now OVERFLOW or bad)
-  (void)n_new_bad;
+  for (; c + 16 <= n; c += 16) *(gptr<u32x4_u>)(dst + c) = *(gptr<const u32x4_u>)(src + c);
+  if (c < n) {
+    const u32x4 w = *(gptr<const u32x4_u>)(src + c);
+    const uint32_t r = n - c;
+    uint64_t lo = uint64_t(w.x) | uint64_t(w.y) << 32, hi = uint64_t(w.z) | uint64_t(w.w) << 32;
+    uint32_t o = c;
+    if (r & 8) {
+      *(gptr<u64_u>)(dst + o) = lo;
+      lo = hi;
+      o += 8;
+    }
+    if (r & 4) {
+      *(gptr<u32_u>)(dst + o) = uint32_t(lo);
+      lo >>= 32;
+      o += 4;
+    }
+    if (r & 2) {
+      *(gptr<u16_u>)(dst + o) = uint16_t(lo);
+      lo >>= 16;
+      o += 2;
+    }
+    if (r & 1) dst[o] = uint8_t(lo);
+  }
 }
 
 __global__ void __launch_bounds__(kTPB) tf_scatter_kernel(TfArgs A) {
-  if (*to_glb(reinterpret_cast<const uint32_t*>(A.out.workspace)) != 0) return;  // overflow: sizes only
+  if (*to_glb(reinterpret_cast<const uint32_t*>(A.out.workspace)) != 0) {  // overflow: sizes and statuses only
+    for (uint32_t b = blockIdx.x * kTPB + threadIdx.x; b < A.n_blocks; b += gridDim.x * kTPB)
+      if (to_glb(A.out.blk_status)[b] == PBL_OK) to_glb(A.out.blk_status)[b] = PBL_OVERFLOW;
+    return;
+  }
   const pbl_decode_out& I = A.in;
   const pbl_decode_out& O = A.out;
   const uint32_t lane = lane_id();
@@ -343,24 +427,32 @@ __global__ void __launch_bounds__(kTPB) tf_scatter_kernel(TfArgs A) {
         to_glb(O.val_off)[okv + b + jo + rank] = vo;
         // key: F[:p] ++ (suffix | F[p:]),  F = prefix ++ key
         if (v.valid) {
+          // F[:p] ++ (suffix | F[p:]), F = prefix[:fp] ++ key[:kn]: up to four
+          // contiguous copies by 16-B chunks
           gptr<uint8_t> dst = to_glb(O.key_bytes) + okb + ko;
-          uint32_t w = 0;
-          for (uint32_t i = 0; i < v.p; i++) dst[w++] = v.F.at(i);
-          if (A.t.suffix_len)
-            for (uint32_t i = 0; i < A.t.suffix_len; i++) dst[w++] = sfx[i];
-          else
-            for (uint32_t i = v.p; i < v.F.len(); i++) dst[w++] = v.F.at(i);
+          const uint32_t fp = v.F.fp, kn = v.F.kn, p = v.p;
+          const uint32_t a1 = p < fp ? p : fp;  // prefix bytes before the split
+          copy_chunks(dst, v.F.pfx, a1);
+          copy_chunks(dst + a1, v.F.key, p - a1);
+          if (A.t.suffix_len) {
+            copy_chunks(dst + p, sfx, A.t.suffix_len);
+          } else {
+            copy_chunks(dst + p, v.F.pfx + a1, fp - a1);
+            const uint32_t k0 = p > fp ? p - fp : 0u;
+            copy_chunks(dst + p + (fp - a1), v.F.key + k0, kn - k0);
+          }
         }
+        // value: lane per KV (long values by the whole wave below)
+        if (v.vlen <= 512) copy_chunks(to_glb(O.val_bytes) + ovb + vo, to_glb(I.val_bytes) + vb_in + v.vo, v.vlen);
       }
-      // values: each visible KV's bytes by the whole wave
-      for (uint64_t m = vm; m; m &= m - 1) {
+      for (uint64_t m = __ballot(vis && v.vlen > 512); m; m &= m - 1) {
         const int src_lane = __builtin_ctzll(m);
         const uint32_t so = uint32_t(__shfl(int(v.vo), src_lane, kWave));
         const uint32_t sl = uint32_t(__shfl(int(v.vlen), src_lane, kWave));
         const uint32_t dofs = uint32_t(__shfl(int(vo), src_lane, kWave));
         const gptr<const uint8_t> s = to_glb(I.val_bytes) + vb_in + so;
         gptr<uint8_t> d = to_glb(O.val_bytes) + ovb + dofs;
-        for (uint32_t i = lane; i < sl; i += kWave) d[i] = s[i];
+        for (uint32_t i = 16 * lane; i < sl; i += 16 * kWave) copy_chunks(d + i, s + i, sl - i < 16 ? sl - i : 16u);
       }
       jo += __builtin_popcountll(vm);
       kcur += uint32_t(__shfl(int(kx), kWave - 1, kWave));
@@ -379,7 +471,7 @@ __global__ void __launch_bounds__(kTPB) tf_scatter_kernel(TfArgs A) {
 extern "C" {
 
 uint64_t pbl_transform_workspace_bytes(uint32_t n_blocks) {
-  return uint64_t(pbl::tf::kTfWs) + 16ull * n_blocks;
+  return pbl::tf::tf_cnt_offset(n_blocks) + 16ull * n_blocks;
 }
 
 int pbl_transform_batch(const pbl_decode_out* in, uint32_t n_blocks, const pbl_transforms* t, pbl_decode_out* out,
@@ -416,8 +508,10 @@ int pbl_transform_batch(const pbl_decode_out* in, uint32_t n_blocks, const pbl_t
   }
   const uint32_t wpb = pbl::kTPB / pbl::kWave;
   const uint32_t grid = uint32_t(std::min<uint64_t>((n_blocks + wpb - 1) / wpb, 8192));
+  if (hipMemsetAsync(out->workspace, 0, pbl::tf::tf_cnt_offset(n_blocks), st) != hipSuccess) return PBL_DEVICE_ERROR;
   hipLaunchKernelGGL(pbl::tf::tf_count_kernel, dim3(grid), dim3(pbl::kTPB), 0, st, a);
-  hipLaunchKernelGGL(pbl::tf::tf_scan_kernel, dim3(1), dim3(pbl::kTPB), 0, st, a);
+  const uint32_t nt = uint32_t(pbl::tf::tf_tiles(n_blocks));
+  hipLaunchKernelGGL(pbl::tf::tf_scan_kernel, dim3(std::min<uint32_t>(nt, 1024)), dim3(pbl::kTPB), 0, st, a);
   hipLaunchKernelGGL(pbl::tf::tf_scatter_kernel, dim3(grid), dim3(pbl::kTPB), 0, st, a);
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }

@@ -23,9 +23,11 @@ __all__ = ["Transforms", "TransformPlan", "apply_transforms"]
 
 
 def _dev_bytes(b: bytes, device) -> Optional[torch.Tensor]:
+    """Device copy of b, readable 16 bytes past its end (pbl_transform_batch
+    copies by 16-B chunks)."""
     if not b:
         return None
-    return torch.tensor(list(b), dtype=torch.uint8, device=device)
+    return torch.tensor(list(b) + [0] * 16, dtype=torch.uint8, device=device)
 
 
 class TransformPlan:
