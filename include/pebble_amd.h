@@ -81,16 +81,18 @@ enum {
                                      lengths vary widely (e.g. Zipf value sizes), so a
                                      colblk batch takes the one-block-per-workgroup
                                      kernel, whose look-back does not convoy behind
-                                     long blocks.  The caller knows the lengths on the
-                                     host (block handles carry them).              */
+                                     long blocks, and a row batch the one-wave-per-
+                                     block kernel (config 5: 1.1-1.5x the pipeline).
+                                     The caller knows the lengths on the host
+                                     (block handles carry them).                   */
 #define PBL_KERNEL_SINGLE 0x200u  /* A/B measurement, no effect on results: the
                                      one-block-per-workgroup kernels instead of the
                                      persistent pipelines                          */
 #define PBL_KERNEL_PIPE 0x400u    /* A/B measurement, no effect on results: the
                                      pipelines even for a PBL_BATCH_VARLEN batch   */
 #define PBL_KERNEL_FLAT 0x800u    /* A/B measurement, no effect on results: row
-                                     batches on the one-wave-per-block kernel that
-                                     reads blocks from global memory               */
+                                     batches on the one-wave-per-block kernel
+                                     (rowblk_flat.hip.h) even without VARLEN        */
 
 /* per-KV flag byte (kv_flags[]) */
 #define PBL_KV_RESTART 0x01u       /* entry offset is a restart point            */

@@ -195,6 +195,21 @@ __device__ inline void block_excl_scan2(uint32_t a, uint32_t b, uint32_t* ea, ui
   *tot_b = tb;
 }
 
+// Stage n16 16-byte granules src[0, n16) (global, 16-B aligned) into LDS
+// dst[0, n16) by LDS-DMA (global_load_lds_dwordx4: no registers, every granule
+// in flight at once), then wait for them.  One wave; lanes past n16 are masked
+// off (nothing lands past the stage).  A register round trip per granule
+// (load, wait, ds_write) serialises the block's HBM latency instead.
+__device__ inline void lds_stage16(lptr<u32x4> dst, gptr<const u32x4> src, uint32_t n16) {
+  const uint32_t l = lane_id();
+  for (uint32_t g0 = 0; g0 < n16; g0 += kWave) {
+    if (g0 + l < n16)
+      __builtin_amdgcn_global_load_lds((gptr<const void>)(src + (g0 + l)), (lptr<void>)(dst + g0), 16, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  wave_sync();
+}
+
 // Decoupled look-back (single-pass scan across blocks), in two halves so a
 // workgroup can publish its aggregate as soon as it is known and resolve its
 // exclusive prefix later.  Tickets are handed out in launch order, so every

@@ -13,12 +13,14 @@
 //                         ChecksumTypeXXHash64 of block.go:155-160): one lane
 //                         per block (XXH64's stripes are sequential)
 //   snappy_len_kernel     the decoded length (uvarint header, snappy.DecodedLen)
-//   snappy2_kernel        snappy.Decode (golang/snappy block format): one wave
-//                         per block, 4 per CU: lane 0 queues element
+//   snappy3_kernel        snappy.Decode (golang/snappy block format): one wave
+//                         per block, 2 per CU: lane 0 queues element
 //                         descriptors from the LDS-staged input, literals are
-//                         copied lane per element, copies in groups of
-//                         independent ones (see below)
-//   snappy_kernel         (PBL_SNAPPY_V1 A/B) the first form: input and output
+//                         copied lane per element into an LDS output window,
+//                         copies by the wave in order, the window written out
+//                         once (snappy2_kernel: the same with the output in
+//                         HBM, copies in groups of independent ones)
+//   snappy_kernel         (PBL_SNAPPY_VER 1 A/B) the first form: input and output
 //                         staged in LDS, the wave copies one element at a time
 //   zstd_kernel           (zstd.hip) the blocks whose indicator is zstd
 // MinLZ (indicator 8) and unknown indicators report PBL_UNSUPPORTED.
@@ -483,7 +485,7 @@ __global__ void __launch_bounds__(kWave) snappy_kernel(const pbl_phys_batch B, u
 }
 
 
-// ---- snappy v2 (the default; PBL_SNAPPY_V1 = 1 keeps snappy_kernel) ----------
+// ---- snappy v2 (PBL_SNAPPY_VER 2; also v3's path for blocks past its window) ----
 // One wave per block, four blocks per CU (38 KB of LDS each: the compressed
 // bytes and a queue of element descriptors; the output goes straight to HBM):
 //   parse     lane 0 walks the element tags from LDS (8 bytes per element in
@@ -498,185 +500,21 @@ __global__ void __launch_bounds__(kWave) snappy_kernel(const pbl_phys_batch B, u
 //             once), others 16-B chunks.  A workgroup fence between groups.
 // Blocks past the LDS stage (or decoding past 64 KiB) take snappy_wave on one
 // lane from global memory.
-#ifndef PBL_SNAPPY_V1
-#define PBL_SNAPPY_V1 0
+#ifndef PBL_SNAPPY_VER
+#define PBL_SNAPPY_VER 2  // 1: snappy_kernel, 2: snappy2_kernel, 3: snappy3_kernel (67.7 vs 88.9 GB/s: rejected)
 #endif
 constexpr uint32_t kSnIn = 32768;
-constexpr uint32_t kSnQ = 760;
-struct Snap2Lds {
-  uint32_t in[(kSnIn + 64) / 4];  // compressed bytes at their 16-B phase (+ slack)
-  uint64_t q[kSnQ];               // dst | len << 16 | (src or offset) << 32 | copy << 63
-};
-
-// bytes [a, a + 16) of the staged LDS words, any alignment
-__device__ __forceinline__ uint4 sn_lds16(lptr<const uint32_t> W, uint32_t a) {
-  const uint32_t q = a >> 2, r = a & 3;
-  const uint32_t x0 = W[q], x1 = W[q + 1], x2 = W[q + 2], x3 = W[q + 3], x4 = W[q + 4];
-  return make_uint4(__builtin_amdgcn_alignbyte(x1, x0, r), __builtin_amdgcn_alignbyte(x2, x1, r),
-                    __builtin_amdgcn_alignbyte(x3, x2, r), __builtin_amdgcn_alignbyte(x4, x3, r));
-}
-__device__ __forceinline__ uint64_t sn_lds8(lptr<const uint32_t> W, uint32_t a) {
-  const uint32_t q = a >> 2, r = a & 3;
-  const uint32_t x0 = W[q], x1 = W[q + 1], x2 = W[q + 2];
-  return uint64_t(__builtin_amdgcn_alignbyte(x2, x1, r)) << 32 | __builtin_amdgcn_alignbyte(x1, x0, r);
-}
-
-typedef u32x4 sn_u32x4_u __attribute__((aligned(1)));
-typedef uint64_t sn_u64_u __attribute__((aligned(1)));
-typedef uint32_t sn_u32_u __attribute__((aligned(1)));
-typedef uint16_t sn_u16_u __attribute__((aligned(1)));
-// bytes [0, n) of w (n <= 16) to p, nothing past n
-__device__ __forceinline__ void sn_store_n(gptr<uint8_t> p, const uint4& w, uint32_t n) {
-  if (n == 16) {
-    *(gptr<sn_u32x4_u>)p = u32x4{w.x, w.y, w.z, w.w};
-    return;
-  }
-  uint64_t lo = uint64_t(w.x) | uint64_t(w.y) << 32, hi = uint64_t(w.z) | uint64_t(w.w) << 32;
-  uint32_t o = 0;
-  if (n & 8) { *(gptr<sn_u64_u>)p = lo; lo = hi; o = 8; }
-  if (n & 4) { *(gptr<sn_u32_u>)(p + o) = uint32_t(lo); lo >>= 32; o += 4; }
-  if (n & 2) { *(gptr<sn_u16_u>)(p + o) = uint16_t(lo); lo >>= 16; o += 2; }
-  if (n & 1) *(p + o) = uint8_t(lo);
-}
-
-__device__ __forceinline__ void sn_fence() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-// Lane 0: queue the elements starting at input offset *s (output offset *d)
-// until the queue or the input is full.  Returns the count; *ok clears on a
-// corrupt element (snappy.Decode's ErrCorrupt cases).
-__device__ __forceinline__ uint32_t sn_parse(lptr<const uint32_t> W, uint32_t ib, lptr<uint64_t> Q, uint32_t n,
-                                             uint32_t D, uint32_t* s_io, uint32_t* d_io, bool* ok) {
-  uint32_t s = *s_io, d = *d_io, c = 0;
-  while (s < n && c < kSnQ) {
-    const uint64_t w = sn_lds8(W, ib + s);
-    const uint32_t t = uint32_t(w) & 0xff, kind = t & 3;
-    uint32_t len, x, h;
-    if (kind == 0) {
-      x = t >> 2;
-      h = 1;
-      if (x >= 60) {
-        const uint32_t nb = x - 59;
-        h = 1 + nb;
-        x = uint32_t(w >> 8) & (nb == 4 ? 0xffffffffu : (1u << (8 * nb)) - 1u);
-      }
-      if (h > n - s) { *ok = false; break; }
-      len = x + 1;  // (x = 2^32 - 1 wraps to 0: rejected below as longer than the input)
-      if (len == 0 || len > n - s - h || len > D - d) { *ok = false; break; }
-      Q[c++] = uint64_t(d) | uint64_t(len) << 16 | uint64_t(s + h) << 32;
-      s += h + len;
-      d += len;
-    } else {
-      uint32_t off;
-      if (kind == 1) {
-        h = 2;
-        len = 4 + ((t >> 2) & 7);
-        off = ((t & 0xe0) << 3) | (uint32_t(w >> 8) & 0xff);
-      } else if (kind == 2) {
-        h = 3;
-        len = 1 + (t >> 2);
-        off = uint32_t(w >> 8) & 0xffff;
-      } else {
-        h = 5;
-        len = 1 + (t >> 2);
-        off = uint32_t(w >> 8);
-      }
-      if (h > n - s || off == 0 || off > d || len > D - d) { *ok = false; break; }
-      Q[c++] = uint64_t(d) | uint64_t(len) << 16 | uint64_t(off) << 32 | (1ull << 63);
-      s += h;
-      d += len;
-    }
-  }
-  *s_io = s;
-  *d_io = d;
-  return c;
-}
-
-// One snappy block: compressed bytes staged at byte ib of W (n bytes, the
-// uvarint header included), D decoded bytes to dst.  Uniform result: false = corrupt.
-__device__ bool sn_decode(Snap2Lds& S, uint32_t ib, uint32_t n, uint32_t used, uint32_t D, gptr<uint8_t> dst) {
-  const uint32_t lane = lane_id();
-  lptr<const uint32_t> W = to_lds_ptr(static_cast<const uint32_t*>(S.in));
-  lptr<uint64_t> Q = to_lds_ptr(S.q);
-  const lptr<const uint64_t> QR = to_lds_ptr(static_cast<const uint64_t*>(S.q));
-  uint32_t s = used, d = 0;
-  bool ok = true;
-  while (s < n) {
-    uint32_t qc = 0;
-    if (lane == 0) qc = sn_parse(W, ib, Q, n, D, &s, &d, &ok);
-    qc = __shfl(qc, 0, kWave);
-    s = __shfl(s, 0, kWave);
-    d = __shfl(d, 0, kWave);
-    if (!__shfl(int(ok), 0, kWave)) return false;
-    wave_sync();
-    // literals: lane per element
-    for (uint32_t i0 = 0; i0 < qc; i0 += kWave) {
-      const uint32_t i = i0 + lane;
-      uint64_t e = 0;
-      uint32_t len = 0;
-      if (i < qc) {
-        e = QR[i];
-        len = (e >> 63) ? 0u : uint32_t(e >> 16) & 0xffffu;
-      }
-      const uint32_t o = uint32_t(e) & 0xffffu, src = uint32_t(e >> 32) & 0x7fffffffu;
-      if (len && len <= 256)
-        for (uint32_t c = 0; c < len; c += 16) {
-          const uint32_t k = len - c < 16 ? len - c : 16u;
-          sn_store_n(dst + o + c, sn_lds16(W, ib + src + c), k);
-        }
-      for (uint64_t m = __ballot(len > 256); m; m &= m - 1) {
-        const int sl = __builtin_ctzll(m);
-        const uint32_t lo = __shfl(o, sl, kWave), ls = __shfl(src, sl, kWave), ll = __shfl(len, sl, kWave);
-        for (uint32_t c = 16 * lane; c < ll; c += 16 * kWave) {
-          const uint32_t k = ll - c < 16 ? ll - c : 16u;
-          sn_store_n(dst + lo + c, sn_lds16(W, ib + ls + c), k);
-        }
-      }
-    }
-    sn_fence();
-    // copies: groups of independent ones, lane per copy
-    uint32_t i = 0;
-    while (i < qc) {
-      const uint32_t j = i + lane;
-      uint64_t e = 0;
-      if (j < qc) e = QR[j];
-      const bool isc = j < qc && (e >> 63);
-      const uint64_t cm = __ballot(isc);
-      if (!cm) {  // (no copy among the next 64)
-        i += kWave;
-        continue;
-      }
-      const int first = __builtin_ctzll(cm);
-      const uint32_t o = uint32_t(e) & 0xffffu, len = uint32_t(e >> 16) & 0xffffu,
-                     off = uint32_t(e >> 32) & 0x7fffffffu;
-      const uint32_t d0 = __shfl(o, first, kWave);
-      // bytes read below its own output: [o - off, o - off + min(len, off))
-      const bool indep = isc && (o - off + (len < off ? len : off) <= d0);
-      const uint64_t stop = first == 63 ? 0ull : (__ballot(isc && !indep) & ~((2ull << first) - 1));
-      const uint32_t end = stop ? uint32_t(__builtin_ctzll(stop)) : uint32_t(kWave);  // lanes [first, end) run
-      if (isc && uint32_t(lane) >= uint32_t(first) && uint32_t(lane) < end) {
-        const gptr<const uint8_t> sp = dst + (o - off);
-        if (off >= 16) {
-          for (uint32_t c = 0; c < len; c += 16) {
-            const u32x4 v = *(gptr<const sn_u32x4_u>)(sp + c);
-            sn_store_n(dst + o + c, make_uint4(v.x, v.y, v.z, v.w), len - c < 16 ? len - c : 16u);
-          }
-        } else {
-          // the period: bytes [o - off, o), final
-          uint8_t per[16];
-          for (uint32_t k = 0; k < off; k++) per[k] = sp[k];
-          for (uint32_t k = 0; k < len; k++) dst[o + k] = per[k % off];
-        }
-      }
-      sn_fence();
-      i += end;
-    }
-  }
-  return d == D;
-}
+constexpr uint32_t kSnQ = 592;  // (4 blocks per CU: 40 KB of LDS each)
+#ifdef PBL_SNAP_STAMPS  // diagnostic builds: per-block phase cycles (scripts/snap_stamps.py)
+__device__ uint64_t g_snap_stamps[65536 * 8];
+#define SN_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define SN_ACC(i, v) if (lane_id() == 0 && g_sn_b < 65536) g_snap_stamps[8 * g_sn_b + (i)] += __builtin_amdgcn_s_memtime() - (v)
+__device__ uint32_t g_sn_dummy;
+#else
+#define SN_T(v)
+#define SN_ACC(i, v)
+#endif
+#include "snappy_dec.hip.h"
 
 __global__ void __launch_bounds__(kWave) snappy2_kernel(const pbl_phys_batch B, uint8_t* out, const uint64_t* out_off,
                                                         const uint32_t* out_cap, uint32_t* out_len, uint32_t* status) {
@@ -710,11 +548,168 @@ __global__ void __launch_bounds__(kWave) snappy2_kernel(const pbl_phys_batch B, 
         const uint64_t sa = reinterpret_cast<uint64_t>(B.bytes + boff);
         const uint32_t ssh = uint32_t(sa & 15), ng = (ssh + n + 15) / 16;
         const gptr<const u32x4> sg = to_glb(reinterpret_cast<const u32x4*>(sa - ssh));
-        lptr<u32x4> sl = to_lds_ptr(reinterpret_cast<u32x4*>(S.in));
-        for (uint32_t g = lane; g < ng; g += kWave) sl[g] = sg[g];
-        wave_sync();
+        SN_T(ts);
+        lds_stage16(to_lds_ptr(reinterpret_cast<u32x4*>(S.in)), sg, ng);
+        {
+          const uint32_t g_sn_b = b;
+          SN_ACC(0, ts);
+          (void)g_sn_b;
+        }
         len = dl;
-        if (!sn_decode(S, ssh, n, used, dl, dst)) st = PBL_CORRUPT_COMPRESSION;
+        if (!sn_decode(S, ssh, n, used, dl, dst, b)) st = PBL_CORRUPT_COMPRESSION;
+      } else {
+        len = ~0u;
+        if (lane == 0) len = snappy_wave(GlbBytes{src}, n, GlbBytesW{dst}, dl, 0, 1);
+        len = __shfl(len, 0, kWave);
+        if (len == ~0u) st = PBL_CORRUPT_COMPRESSION;
+      }
+    } else {
+      st = PBL_UNSUPPORTED;
+    }
+    if (lane == 0) {
+      to_glb(out_len)[b] = st == PBL_OK ? len : 0u;
+      to_glb(status)[b] = st;
+    }
+    wave_sync();
+  }
+}
+
+// ---- snappy v3 (PBL_SNAPPY_VER 3): the output staged in LDS -------------------
+// As v2 (lane 0 queues the elements, literals lane per element), but the block
+// is decoded into an LDS window (D <= kS3Out) and written out once as aligned
+// 16-B granules, so a copy whose source another copy produced costs an LDS
+// round trip instead of an HBM one: the wave walks the queued copies in order
+// (descriptors read 64 at a time, one per lane, then taken by readlane), every
+// lane one byte of the copy (an overlapping copy repeats its period).  Two
+// blocks per CU (72 KB of LDS each).  Blocks decoding past the window take v2.
+constexpr uint32_t kS3Out = 32768;
+constexpr uint32_t kS3Pad = 16;  // front pad of the input stage (literal words may start 3 bytes early)
+struct Snap3Lds {
+  Snap2Lds s2;                      // (the input stage is shifted by kS3Pad here)
+  uint32_t out[(kS3Out + 32) / 4];  // decoded bytes, byte i at dsh + i
+};
+
+__device__ __forceinline__ uint32_t sn_lds4(lptr<const uint32_t> W, uint32_t a) {
+  const uint32_t q = a >> 2, r = a & 3;
+  return __builtin_amdgcn_alignbyte(W[q + 1], W[q], r);
+}
+
+__device__ bool sn3_decode(Snap3Lds& S, uint32_t ib, uint32_t n, uint32_t used, uint32_t D, uint32_t ob) {
+  const uint32_t lane = lane_id();
+  lptr<const uint32_t> W = to_lds_ptr(static_cast<const uint32_t*>(S.s2.in));
+  lptr<uint64_t> Q = to_lds_ptr(S.s2.q);
+  const lptr<const uint64_t> QR = to_lds_ptr(static_cast<const uint64_t*>(S.s2.q));
+  lptr<uint32_t> OW = to_lds_ptr(S.out);
+  lptr<uint8_t> OB = to_lds_ptr(reinterpret_cast<uint8_t*>(S.out));
+  uint32_t s = used, d = 0;
+  bool ok = true;
+  while (s < n) {
+    uint32_t qc = 0;
+    qc = sn_parse(W, ib, Q, n, D, &s, &d, &ok);
+    if (!ok) return false;
+    wave_sync();
+    // literals, lane per element: whole output words, the edge bytes one by one
+    for (uint32_t i0 = 0; i0 < qc; i0 += kWave) {
+      const uint32_t i = i0 + lane;
+      if (i < qc) {
+        const uint64_t e = QR[i];
+        if (!(e >> 63)) {
+          const uint32_t o = ob + (uint32_t(e) & 0xffffu), len = uint32_t(e >> 16) & 0xffffu;
+          const uint32_t src = ib + (uint32_t(e >> 32) & 0x7fffffffu);
+          const uint32_t o_end = o + len, w0 = (o + 3) >> 2, w1 = o_end >> 2;
+          if (w0 >= w1) {  // within one word: bytes
+            for (uint32_t x = o; x < o_end; x++) OB[x] = uint8_t(sn_lds4(W, src + (x - o)));
+          } else {
+            for (uint32_t x = o; x < 4 * w0; x++) OB[x] = uint8_t(sn_lds4(W, src + (x - o)));
+            for (uint32_t w = w0; w < w1; w++) OW[w] = sn_lds4(W, src + (4 * w - o));
+            for (uint32_t x = 4 * w1; x < o_end; x++) OB[x] = uint8_t(sn_lds4(W, src + (x - o)));
+          }
+        }
+      }
+    }
+    wave_sync();
+    // copies in order, the wave per copy (a lane per byte, len <= 64)
+    for (uint32_t i0 = 0; i0 < qc; i0 += kWave) {
+      const uint32_t i = i0 + lane;
+      const uint64_t e = i < qc ? QR[i] : 0ull;
+      uint64_t cm = __ballot(e >> 63);
+      const uint32_t ex = uint32_t(e), ey = uint32_t(e >> 32);
+      while (cm) {
+        const int k = __builtin_ctzll(cm);
+        cm &= cm - 1;
+        const uint32_t x = __builtin_amdgcn_readlane(ex, k), y = __builtin_amdgcn_readlane(ey, k);
+        const uint32_t o = ob + (x & 0xffffu), len = x >> 16, off = y & 0x7fffffffu;
+        if (lane < len) {
+          const uint32_t from = o - off + (off >= len ? lane : lane % off);
+          OB[o + lane] = OB[from];
+        }
+      }
+    }
+    wave_sync();
+  }
+  return d == D;
+}
+
+__global__ void __launch_bounds__(kWave) snappy3_kernel(const pbl_phys_batch B, uint8_t* out, const uint64_t* out_off,
+                                                        const uint32_t* out_cap, uint32_t* out_len, uint32_t* status) {
+  __shared__ Snap3Lds S;
+  const uint32_t lane = lane_id();
+  for (uint32_t b = blockIdx.x; b < B.n_blocks; b += gridDim.x) {
+    const uint32_t n = to_glb(B.block_len)[b];
+    const uint64_t boff = to_glb(B.block_off)[b];
+    const gptr<const uint8_t> src = to_glb(B.bytes + boff);
+    const uint32_t ind = src[n];
+    if (ind == PBL_COMPRESSION_ZSTD) continue;  // zstd_kernel's
+    uint8_t* dptr = out + to_glb(out_off)[b];
+    gptr<uint8_t> dst = to_glb(dptr);
+    const uint32_t cap = to_glb(out_cap)[b];
+    uint32_t st = PBL_OK, len = 0;
+    if (ind == PBL_COMPRESSION_NONE) {
+      if (n > cap) {
+        st = PBL_OVERFLOW;
+      } else {
+        const uint32_t nf = n & ~15u;
+        for (uint32_t c = 16 * lane; c < nf; c += 16 * kWave)
+          *(gptr<sn_u32x4_u>)(dst + c) = *(gptr<const sn_u32x4_u>)(src + c);
+        for (uint32_t c = nf + lane; c < n; c += kWave) dst[c] = src[c];
+      }
+      len = n;
+    } else if (ind == PBL_COMPRESSION_SNAPPY) {
+      uint32_t dl = 0, used = 0;
+      if (!uvarint32(src, n, &dl, &used)) st = PBL_CORRUPT_COMPRESSION;
+      else if (dl > cap) st = PBL_OVERFLOW;
+      else if (n <= kSnIn - kS3Pad && dl <= 0xffffu) {
+        const uint64_t sa = reinterpret_cast<uint64_t>(B.bytes + boff);
+        const uint32_t ssh = uint32_t(sa & 15), ng = (ssh + n + 15) / 16;
+        const gptr<const u32x4> sg = to_glb(reinterpret_cast<const u32x4*>(sa - ssh));
+        lds_stage16(to_lds_ptr(reinterpret_cast<u32x4*>(S.s2.in)) + kS3Pad / 16, sg, ng);
+        len = dl;
+        if (dl <= kS3Out) {
+          const uint64_t da = reinterpret_cast<uint64_t>(dptr);
+          const uint32_t dsh = uint32_t(da & 15);
+          if (!sn3_decode(S, kS3Pad + ssh, n, used, dl, dsh)) {
+            st = PBL_CORRUPT_COMPRESSION;
+          } else {
+            const uint32_t nd = (dsh + dl + 15) / 16;
+            const gptr<u32x4> dg = to_glb(reinterpret_cast<u32x4*>(da - dsh));
+            const lptr<const u32x4> dl4 = to_lds_ptr(reinterpret_cast<const u32x4*>(S.out));
+            for (uint32_t g = lane; g < nd; g += kWave) {
+              const u32x4 v = dl4[g];
+              const uint32_t lo = g == 0 ? dsh : 0u, hi = g + 1 == nd ? dsh + dl - 16 * g : 16u;
+              if (lo == 0 && hi == 16) {
+                dg[g] = v;
+              } else {
+                gptr<uint8_t> db = reinterpret_cast<gptr<uint8_t>>(dg + g);
+                for (uint32_t k = lo; k < hi; k++) {
+                  const uint32_t w = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
+                  db[k] = uint8_t(w >> (8 * (k & 3)));
+                }
+              }
+            }
+          }
+        } else if (!sn_decode(S.s2, kS3Pad + ssh, n, used, dl, dst)) {
+          st = PBL_CORRUPT_COMPRESSION;
+        }
       } else {
         len = ~0u;
         if (lane == 0) len = snappy_wave(GlbBytes{src}, n, GlbBytesW{dst}, dl, 0, 1);
@@ -736,6 +731,16 @@ __global__ void __launch_bounds__(kWave) snappy2_kernel(const pbl_phys_batch B, 
 }  // namespace pbl
 
 extern "C" {
+
+#ifdef PBL_SNAP_STAMPS
+int pbl_diag_snap_stamps(uint64_t* host, uint64_t n, int clear) {
+  if (clear) {
+    static uint64_t zero[65536 * 8];
+    return hipMemcpyToSymbol(HIP_SYMBOL(pbl::phys::g_snap_stamps), zero, sizeof(zero)) == hipSuccess ? 0 : 8;
+  }
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(pbl::phys::g_snap_stamps), n * 8) == hipSuccess ? 0 : 8;
+}
+#endif
 
 int pbl_verify_checksums(const pbl_phys_batch* batch, uint32_t checksum_type, uint32_t* status, uint32_t* computed,
                          void* stream) {
@@ -773,13 +778,17 @@ int pbl_decompress_blocks(const pbl_phys_batch* batch, uint8_t* out, const uint6
   if (batch->n_blocks == 0) return PBL_OK;
   if (!batch->bytes || !batch->block_off || !batch->block_len) return PBL_INVALID_ARG;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-#if PBL_SNAPPY_V1
+#if PBL_SNAPPY_VER == 1
   const uint32_t grid = std::min<uint32_t>(batch->n_blocks, 2048);
   hipLaunchKernelGGL(pbl::phys::snappy_kernel, dim3(grid), dim3(pbl::kWave), 0, st, *batch, out, out_off, out_cap,
                      out_len, status);
-#else
+#elif PBL_SNAPPY_VER == 2
   const uint32_t grid = std::min<uint32_t>(batch->n_blocks, 4096);
   hipLaunchKernelGGL(pbl::phys::snappy2_kernel, dim3(grid), dim3(pbl::kWave), 0, st, *batch, out, out_off, out_cap,
+                     out_len, status);
+#else
+  const uint32_t grid = std::min<uint32_t>(batch->n_blocks, 2048);
+  hipLaunchKernelGGL(pbl::phys::snappy3_kernel, dim3(grid), dim3(pbl::kWave), 0, st, *batch, out, out_off, out_cap,
                      out_len, status);
 #endif
   if (hipGetLastError() != hipSuccess) return PBL_DEVICE_ERROR;

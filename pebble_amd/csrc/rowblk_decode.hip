@@ -1093,6 +1093,14 @@ uint64_t persistent_grid(hipStream_t st, PersistentKernel k, const void* fn, uin
 }  // namespace pbl
 
 namespace {
+// Row batches take the flat kernel when asked (PBL_KERNEL_FLAT) or when their
+// block lengths vary widely (PBL_BATCH_VARLEN, unless PBL_KERNEL_PIPE): on
+// config 5 it measured 542 / 499 / 619 GiB/s against the pipeline's 495 / 340 /
+// 598 at restart intervals 16 / 32 / 1 (profiles/r03/zipf_ab_*.json).
+bool use_flat(uint32_t flags) {
+  return (flags & PBL_KERNEL_FLAT) || ((flags & PBL_BATCH_VARLEN) && !(flags & PBL_KERNEL_PIPE));
+}
+
 // Row batches on the flat kernel (rowblk_flat.hip.h): blocks past its length
 // limit are sized before it and written after it (values = false: the size pass).
 int launch_row_flat(const pbl::Args& a, hipStream_t st, bool values) {
@@ -1193,7 +1201,7 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
     // blocks).  PBL_KERNEL_SINGLE selects the one-block-per-workgroup
     // persistent kernel (kept for A/B measurement); the default is the pipeline.
     const bool single = (batch->flags & PBL_KERNEL_SINGLE) != 0;
-    if (!single && (batch->flags & PBL_KERNEL_FLAT)) return launch_row_flat(a, st, true);
+    if (!single && use_flat(batch->flags)) return launch_row_flat(a, st, true);
     const void* fn = single ? reinterpret_cast<const void*>(pbl::row::rowblk_decode_kernel)
                             : reinterpret_cast<const void*>(pbl::row::pipe::rowblk_pipe_kernel);
     int cus = 0;
@@ -1256,7 +1264,7 @@ int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stre
     if (batch->block_format) {
       rc = launch_mixed(batch, a, st, batch->flags & PBL_KERNEL_SINGLE, false);
       if (rc != PBL_OK) return rc;
-    } else if (batch->flags & PBL_KERNEL_FLAT) {
+    } else if (use_flat(batch->flags)) {
       rc = launch_row_flat(a, st, false);
       if (rc != PBL_OK) return rc;
     } else {

@@ -74,11 +74,9 @@ __global__ void __launch_bounds__(kWave) zstd_kernel(const pbl_phys_batch B, uin
         const uint64_t sa = reinterpret_cast<uint64_t>(B.bytes + boff + used);
         const uint32_t ssh = uint32_t(sa & 15), ng = (ssh + cn + 15) / 16;
         const gptr<const u32x4> sg = to_glb(reinterpret_cast<const u32x4*>(sa - ssh));
-        lptr<u32x4> sl = to_lds_ptr(reinterpret_cast<u32x4*>(L.in));
-        for (uint32_t g = lane; g < ng; g += kWave) sl[g] = sg[g];
+        lds_stage16(to_lds_ptr(reinterpret_cast<u32x4*>(L.in)), sg, ng);
         const uint64_t da = reinterpret_cast<uint64_t>(dptr);
         const uint32_t dsh = uint32_t(da & 15);
-        wave_sync();
         r = decode_frames(L, LIn{to_lds_ptr(static_cast<const uint8_t*>(L.in))}, ssh, cn,
                           LOut{to_lds_ptr(static_cast<uint8_t*>(L.out)) + dsh}, D);
         if (r == kOk) {

@@ -15,7 +15,7 @@ constexpr uint32_t kSeq = 256;    // sequences decoded per execution round
 enum : uint32_t { kOk = 0, kCorrupt = 1, kUnsupported = 2 };
 
 struct Lds {
-  uint8_t in[kIn + 48];
+  alignas(16) uint8_t in[kIn + 48];
   uint8_t out[kOut + 32];
   uint32_t fse[3][512];  // LL, OF, ML: sym | nb << 8 | base << 16
   uint32_t wt[64];       // the Huffman weights' FSE table

@@ -1,0 +1,52 @@
+"""The device snappy decoder's code (pebble_amd/csrc/snappy_dec.hip.h: element
+walk, copy-chain resolution by pointer jumping, literal and copy phases) run on
+the host by scripts/snappy_emu.cpp -- 64 threads in lockstep at every wave
+primitive -- against the oracle: hamlet-sst's snappy blocks, config-2-shaped
+blocks and text-like blocks.  CPU-only: it checks the source the GPU build
+compiles before the GPU runs it."""
+import os
+import random
+import subprocess
+
+import pytest
+
+import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLANG = "/opt/rocm/lib/llvm/bin/clang++"
+
+
+@pytest.fixture(scope="module")
+def emu(tmp_path_factory):
+    if not os.path.exists(CLANG):
+        pytest.skip("no clang++")
+    exe = str(tmp_path_factory.mktemp("semu") / "snappy_emu")
+    subprocess.run([CLANG, "-O1", "-std=c++20", "-pthread", os.path.join(ROOT, "scripts", "snappy_emu.cpp"), "-o", exe],
+                   check=True)
+    return exe
+
+
+def run(emu, tmp_path, raw):
+    i, o = tmp_path / "in.bin", tmp_path / "out.bin"
+    i.write_bytes(raw)
+    r = subprocess.run([emu, str(i), str(o)], capture_output=True, text=True, timeout=300)
+    return o.read_bytes() if r.returncode == 0 else None
+
+
+def test_emulated_snappy_decoder_matches_oracle(emu, tmp_path):
+    import json
+    import pyarrow as pa
+    golden = os.path.join(ROOT, "tests", "golden")
+    phys = json.load(open(os.path.join(golden, "physical.json")))
+    blob = open(os.path.join(golden, "physical_blocks.bin"), "rb").read()
+    for b in phys["hamlet_snappy"]["blocks"][:6]:
+        raw = blob[b["blob_off"]: b["blob_off"] + b["length"]]
+        assert run(emu, tmp_path, raw) == oracle.snappy_decode(raw)
+    from pebble_amd.rowblk import gen_row_blocks
+    buf, off, lens, _ = gen_row_blocks(7, 2, 32768, 16, 16, 100, n_threads=1)
+    rng = random.Random(3)
+    words = [rng.randbytes(rng.randrange(1, 10)) for _ in range(300)]
+    text = b" ".join(rng.choice(words) for _ in range(6000))[:30000]
+    for data in [bytes(buf[int(off[0]):int(off[0]) + int(lens[0])]), text, b"ab" * 9000, rng.randbytes(20000)]:
+        raw = pa.Codec("snappy").compress(data, asbytes=True)
+        assert run(emu, tmp_path, raw) == data
