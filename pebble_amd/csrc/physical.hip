@@ -13,13 +13,19 @@
 //                         ChecksumTypeXXHash64 of block.go:155-160): one lane
 //                         per block (XXH64's stripes are sequential)
 //   snappy_len_kernel     the decoded length (uvarint header, snappy.DecodedLen)
-//   snappy3_kernel        snappy.Decode (golang/snappy block format): one wave
-//                         per block, 2 per CU: lane 0 queues element
-//                         descriptors from the LDS-staged input, literals are
-//                         copied lane per element into an LDS output window,
-//                         copies by the wave in order, the window written out
-//                         once (snappy2_kernel: the same with the output in
-//                         HBM, copies in groups of independent ones)
+//   snappy_walk_kernel    snappy.Decode (golang/snappy block format), step 1:
+//                         each block's element chain walked and validated on
+//                         one lane (64 blocks a wave), a tag bitmap left in
+//                         the block's output region (snappy_dec.hip.h)
+//   snappy4_kernel        step 2, a wave per walked block, nothing staged:
+//                         elements decoded a lane each, copy chains resolved
+//                         by pointer jumping (to the input where they lead to
+//                         a literal), literals and resolved copies written in
+//                         parallel, the rest in groups of independent copies
+//   snappy2_kernel        the other blocks (uncompressed copies, snappy blocks
+//                         the walk does not cover): one wave per block, the
+//                         input staged in LDS, the elements walked by the wave
+//                         with scalar arithmetic, then snappy4's phases
 //   snappy_kernel         (PBL_SNAPPY_VER 1 A/B) the first form: input and output
 //                         staged in LDS, the wave copies one element at a time
 //   zstd_kernel           (zstd.hip) the blocks whose indicator is zstd
@@ -501,7 +507,7 @@ __global__ void __launch_bounds__(kWave) snappy_kernel(const pbl_phys_batch B, u
 // Blocks past the LDS stage (or decoding past 64 KiB) take snappy_wave on one
 // lane from global memory.
 #ifndef PBL_SNAPPY_VER
-#define PBL_SNAPPY_VER 2  // 1: snappy_kernel, 2: snappy2_kernel, 3: snappy3_kernel (67.7 vs 88.9 GB/s: rejected)
+#define PBL_SNAPPY_VER 2  // 1: snappy_kernel (A/B), 2: snappy_walk_kernel + snappy4_kernel + snappy2_kernel
 #endif
 constexpr uint32_t kSnIn = 32768;
 constexpr uint32_t kSnQ = 592;  // (4 blocks per CU: 40 KB of LDS each)
@@ -515,6 +521,38 @@ __device__ uint32_t g_sn_dummy;
 #define SN_ACC(i, v)
 #endif
 #include "snappy_dec.hip.h"
+
+// The element walk of the blocks snappy4_kernel decodes, a lane per block.
+__global__ void __launch_bounds__(kTPB) snappy_walk_kernel(const pbl_phys_batch B, uint8_t* out,
+                                                           const uint64_t* out_off, const uint32_t* out_cap) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B.n_blocks) return;
+  const uint32_t n = to_glb(B.block_len)[b];
+  const gptr<const uint8_t> src = to_glb(B.bytes + to_glb(B.block_off)[b]);
+  if (src[n] != PBL_COMPRESSION_SNAPPY) return;
+  uint32_t dl = 0, used = 0;
+  if (!uvarint32(src, n, &dl, &used) || dl > to_glb(out_cap)[b] || !sn4_walkable(n, dl)) return;
+  sn4_walk(src, n, used, dl, to_glb(out + to_glb(out_off)[b]));
+}
+
+// A wave per walked block (sn4_decode); snappy2_kernel takes the others.
+__global__ void __launch_bounds__(kWave) snappy4_kernel(const pbl_phys_batch B, uint8_t* out, const uint64_t* out_off,
+                                                        const uint32_t* out_cap, uint32_t* out_len, uint32_t* status) {
+  __shared__ Snap4Lds S;
+  for (uint32_t b = blockIdx.x; b < B.n_blocks; b += gridDim.x) {
+    const uint32_t n = to_glb(B.block_len)[b];
+    const gptr<const uint8_t> src = to_glb(B.bytes + to_glb(B.block_off)[b]);
+    if (src[n] != PBL_COMPRESSION_SNAPPY) continue;
+    uint32_t dl = 0, used = 0;
+    if (!uvarint32(src, n, &dl, &used) || dl > to_glb(out_cap)[b] || !sn4_walkable(n, dl)) continue;
+    const bool ok = sn4_decode(S, src, n, dl, to_glb(out + to_glb(out_off)[b]), b);
+    if (lane_id() == 0) {
+      to_glb(out_len)[b] = ok ? dl : 0u;
+      to_glb(status)[b] = ok ? uint32_t(PBL_OK) : uint32_t(PBL_CORRUPT_COMPRESSION);
+    }
+    wave_sync();
+  }
+}
 
 __global__ void __launch_bounds__(kWave) snappy2_kernel(const pbl_phys_batch B, uint8_t* out, const uint64_t* out_off,
                                                         const uint32_t* out_cap, uint32_t* out_len, uint32_t* status) {
@@ -544,6 +582,7 @@ __global__ void __launch_bounds__(kWave) snappy2_kernel(const pbl_phys_batch B, 
       uint32_t dl = 0, used = 0;
       if (!uvarint32(src, n, &dl, &used)) st = PBL_CORRUPT_COMPRESSION;
       else if (dl > cap) st = PBL_OVERFLOW;
+      else if (sn4_walkable(n, dl)) continue;  // snappy4_kernel's
       else if (n <= kSnIn && dl <= 0xffffu) {
         const uint64_t sa = reinterpret_cast<uint64_t>(B.bytes + boff);
         const uint32_t ssh = uint32_t(sa & 15), ng = (ssh + n + 15) / 16;
@@ -557,159 +596,6 @@ __global__ void __launch_bounds__(kWave) snappy2_kernel(const pbl_phys_batch B, 
         }
         len = dl;
         if (!sn_decode(S, ssh, n, used, dl, dst, b)) st = PBL_CORRUPT_COMPRESSION;
-      } else {
-        len = ~0u;
-        if (lane == 0) len = snappy_wave(GlbBytes{src}, n, GlbBytesW{dst}, dl, 0, 1);
-        len = __shfl(len, 0, kWave);
-        if (len == ~0u) st = PBL_CORRUPT_COMPRESSION;
-      }
-    } else {
-      st = PBL_UNSUPPORTED;
-    }
-    if (lane == 0) {
-      to_glb(out_len)[b] = st == PBL_OK ? len : 0u;
-      to_glb(status)[b] = st;
-    }
-    wave_sync();
-  }
-}
-
-// ---- snappy v3 (PBL_SNAPPY_VER 3): the output staged in LDS -------------------
-// As v2 (lane 0 queues the elements, literals lane per element), but the block
-// is decoded into an LDS window (D <= kS3Out) and written out once as aligned
-// 16-B granules, so a copy whose source another copy produced costs an LDS
-// round trip instead of an HBM one: the wave walks the queued copies in order
-// (descriptors read 64 at a time, one per lane, then taken by readlane), every
-// lane one byte of the copy (an overlapping copy repeats its period).  Two
-// blocks per CU (72 KB of LDS each).  Blocks decoding past the window take v2.
-constexpr uint32_t kS3Out = 32768;
-constexpr uint32_t kS3Pad = 16;  // front pad of the input stage (literal words may start 3 bytes early)
-struct Snap3Lds {
-  Snap2Lds s2;                      // (the input stage is shifted by kS3Pad here)
-  uint32_t out[(kS3Out + 32) / 4];  // decoded bytes, byte i at dsh + i
-};
-
-__device__ __forceinline__ uint32_t sn_lds4(lptr<const uint32_t> W, uint32_t a) {
-  const uint32_t q = a >> 2, r = a & 3;
-  return __builtin_amdgcn_alignbyte(W[q + 1], W[q], r);
-}
-
-__device__ bool sn3_decode(Snap3Lds& S, uint32_t ib, uint32_t n, uint32_t used, uint32_t D, uint32_t ob) {
-  const uint32_t lane = lane_id();
-  lptr<const uint32_t> W = to_lds_ptr(static_cast<const uint32_t*>(S.s2.in));
-  lptr<uint64_t> Q = to_lds_ptr(S.s2.q);
-  const lptr<const uint64_t> QR = to_lds_ptr(static_cast<const uint64_t*>(S.s2.q));
-  lptr<uint32_t> OW = to_lds_ptr(S.out);
-  lptr<uint8_t> OB = to_lds_ptr(reinterpret_cast<uint8_t*>(S.out));
-  uint32_t s = used, d = 0;
-  bool ok = true;
-  while (s < n) {
-    uint32_t qc = 0;
-    qc = sn_parse(W, ib, Q, n, D, &s, &d, &ok);
-    if (!ok) return false;
-    wave_sync();
-    // literals, lane per element: whole output words, the edge bytes one by one
-    for (uint32_t i0 = 0; i0 < qc; i0 += kWave) {
-      const uint32_t i = i0 + lane;
-      if (i < qc) {
-        const uint64_t e = QR[i];
-        if (!(e >> 63)) {
-          const uint32_t o = ob + (uint32_t(e) & 0xffffu), len = uint32_t(e >> 16) & 0xffffu;
-          const uint32_t src = ib + (uint32_t(e >> 32) & 0x7fffffffu);
-          const uint32_t o_end = o + len, w0 = (o + 3) >> 2, w1 = o_end >> 2;
-          if (w0 >= w1) {  // within one word: bytes
-            for (uint32_t x = o; x < o_end; x++) OB[x] = uint8_t(sn_lds4(W, src + (x - o)));
-          } else {
-            for (uint32_t x = o; x < 4 * w0; x++) OB[x] = uint8_t(sn_lds4(W, src + (x - o)));
-            for (uint32_t w = w0; w < w1; w++) OW[w] = sn_lds4(W, src + (4 * w - o));
-            for (uint32_t x = 4 * w1; x < o_end; x++) OB[x] = uint8_t(sn_lds4(W, src + (x - o)));
-          }
-        }
-      }
-    }
-    wave_sync();
-    // copies in order, the wave per copy (a lane per byte, len <= 64)
-    for (uint32_t i0 = 0; i0 < qc; i0 += kWave) {
-      const uint32_t i = i0 + lane;
-      const uint64_t e = i < qc ? QR[i] : 0ull;
-      uint64_t cm = __ballot(e >> 63);
-      const uint32_t ex = uint32_t(e), ey = uint32_t(e >> 32);
-      while (cm) {
-        const int k = __builtin_ctzll(cm);
-        cm &= cm - 1;
-        const uint32_t x = __builtin_amdgcn_readlane(ex, k), y = __builtin_amdgcn_readlane(ey, k);
-        const uint32_t o = ob + (x & 0xffffu), len = x >> 16, off = y & 0x7fffffffu;
-        if (lane < len) {
-          const uint32_t from = o - off + (off >= len ? lane : lane % off);
-          OB[o + lane] = OB[from];
-        }
-      }
-    }
-    wave_sync();
-  }
-  return d == D;
-}
-
-__global__ void __launch_bounds__(kWave) snappy3_kernel(const pbl_phys_batch B, uint8_t* out, const uint64_t* out_off,
-                                                        const uint32_t* out_cap, uint32_t* out_len, uint32_t* status) {
-  __shared__ Snap3Lds S;
-  const uint32_t lane = lane_id();
-  for (uint32_t b = blockIdx.x; b < B.n_blocks; b += gridDim.x) {
-    const uint32_t n = to_glb(B.block_len)[b];
-    const uint64_t boff = to_glb(B.block_off)[b];
-    const gptr<const uint8_t> src = to_glb(B.bytes + boff);
-    const uint32_t ind = src[n];
-    if (ind == PBL_COMPRESSION_ZSTD) continue;  // zstd_kernel's
-    uint8_t* dptr = out + to_glb(out_off)[b];
-    gptr<uint8_t> dst = to_glb(dptr);
-    const uint32_t cap = to_glb(out_cap)[b];
-    uint32_t st = PBL_OK, len = 0;
-    if (ind == PBL_COMPRESSION_NONE) {
-      if (n > cap) {
-        st = PBL_OVERFLOW;
-      } else {
-        const uint32_t nf = n & ~15u;
-        for (uint32_t c = 16 * lane; c < nf; c += 16 * kWave)
-          *(gptr<sn_u32x4_u>)(dst + c) = *(gptr<const sn_u32x4_u>)(src + c);
-        for (uint32_t c = nf + lane; c < n; c += kWave) dst[c] = src[c];
-      }
-      len = n;
-    } else if (ind == PBL_COMPRESSION_SNAPPY) {
-      uint32_t dl = 0, used = 0;
-      if (!uvarint32(src, n, &dl, &used)) st = PBL_CORRUPT_COMPRESSION;
-      else if (dl > cap) st = PBL_OVERFLOW;
-      else if (n <= kSnIn - kS3Pad && dl <= 0xffffu) {
-        const uint64_t sa = reinterpret_cast<uint64_t>(B.bytes + boff);
-        const uint32_t ssh = uint32_t(sa & 15), ng = (ssh + n + 15) / 16;
-        const gptr<const u32x4> sg = to_glb(reinterpret_cast<const u32x4*>(sa - ssh));
-        lds_stage16(to_lds_ptr(reinterpret_cast<u32x4*>(S.s2.in)) + kS3Pad / 16, sg, ng);
-        len = dl;
-        if (dl <= kS3Out) {
-          const uint64_t da = reinterpret_cast<uint64_t>(dptr);
-          const uint32_t dsh = uint32_t(da & 15);
-          if (!sn3_decode(S, kS3Pad + ssh, n, used, dl, dsh)) {
-            st = PBL_CORRUPT_COMPRESSION;
-          } else {
-            const uint32_t nd = (dsh + dl + 15) / 16;
-            const gptr<u32x4> dg = to_glb(reinterpret_cast<u32x4*>(da - dsh));
-            const lptr<const u32x4> dl4 = to_lds_ptr(reinterpret_cast<const u32x4*>(S.out));
-            for (uint32_t g = lane; g < nd; g += kWave) {
-              const u32x4 v = dl4[g];
-              const uint32_t lo = g == 0 ? dsh : 0u, hi = g + 1 == nd ? dsh + dl - 16 * g : 16u;
-              if (lo == 0 && hi == 16) {
-                dg[g] = v;
-              } else {
-                gptr<uint8_t> db = reinterpret_cast<gptr<uint8_t>>(dg + g);
-                for (uint32_t k = lo; k < hi; k++) {
-                  const uint32_t w = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
-                  db[k] = uint8_t(w >> (8 * (k & 3)));
-                }
-              }
-            }
-          }
-        } else if (!sn_decode(S.s2, kS3Pad + ssh, n, used, dl, dst)) {
-          st = PBL_CORRUPT_COMPRESSION;
-        }
       } else {
         len = ~0u;
         if (lane == 0) len = snappy_wave(GlbBytes{src}, n, GlbBytesW{dst}, dl, 0, 1);
@@ -783,12 +669,12 @@ int pbl_decompress_blocks(const pbl_phys_batch* batch, uint8_t* out, const uint6
   hipLaunchKernelGGL(pbl::phys::snappy_kernel, dim3(grid), dim3(pbl::kWave), 0, st, *batch, out, out_off, out_cap,
                      out_len, status);
 #elif PBL_SNAPPY_VER == 2
+  hipLaunchKernelGGL(pbl::phys::snappy_walk_kernel, dim3((batch->n_blocks + pbl::kTPB - 1) / pbl::kTPB),
+                     dim3(pbl::kTPB), 0, st, *batch, out, out_off, out_cap);
+  hipLaunchKernelGGL(pbl::phys::snappy4_kernel, dim3(std::min<uint32_t>(batch->n_blocks, 8192)), dim3(pbl::kWave), 0,
+                     st, *batch, out, out_off, out_cap, out_len, status);
   const uint32_t grid = std::min<uint32_t>(batch->n_blocks, 4096);
   hipLaunchKernelGGL(pbl::phys::snappy2_kernel, dim3(grid), dim3(pbl::kWave), 0, st, *batch, out, out_off, out_cap,
-                     out_len, status);
-#else
-  const uint32_t grid = std::min<uint32_t>(batch->n_blocks, 2048);
-  hipLaunchKernelGGL(pbl::phys::snappy3_kernel, dim3(grid), dim3(pbl::kWave), 0, st, *batch, out, out_off, out_cap,
                      out_len, status);
 #endif
   if (hipGetLastError() != hipSuccess) return PBL_DEVICE_ERROR;

@@ -6,10 +6,12 @@
 // kSnIn / kSnQ and the SN_T / SN_ACC stamp macros.
 #pragma once
 
+constexpr uint32_t kSnBkShift = 7, kSnBk = 65536u >> kSnBkShift;  // output buckets (sn_buckets)
 struct Snap2Lds {
   alignas(16) uint32_t in[(kSnIn + 64) / 4];  // compressed bytes at their 16-B phase (+ slack)
   uint64_t q[kSnQ];               // dst | len << 16 | (src or offset) << 32 | copy << 63
   uint32_t r[kSnQ];               // copies: where their bytes are (see sn_resolve)
+  uint16_t bk[kSnBk];             // output buckets -> element (sn_buckets)
 };
 
 // bytes [a, a + 16) of the staged LDS words, any alignment
@@ -49,12 +51,54 @@ __device__ __forceinline__ void sn_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// Lane 0: queue the elements starting at input offset *s (output offset *d)
-// until the queue or the input is full.  Returns the count; *ok clears on a
-// corrupt element (snappy.Decode's ErrCorrupt cases).
-// The whole wave runs it with uniform values (the LDS words are read by every
-// lane at one address and made scalar with readfirstlane), so the element
-// walk's arithmetic and branches are scalar; lane 0 writes the queue.
+// One element at the start of w (the 8 input bytes from its tag on, zero past
+// the input): header bytes h, output length len, copy offset off (copies).
+// Unvalidated; the callers check it against the input and output left.
+struct SnElem {
+  uint32_t h, len, off;
+  bool lit;
+};
+__device__ __forceinline__ SnElem sn_elem(uint64_t w) {
+  const uint32_t t = uint32_t(w) & 0xff, kind = t & 3, ext = uint32_t(w >> 8);
+  SnElem e;
+  e.lit = kind == 0;
+  if (kind == 0) {
+    uint32_t x = t >> 2;
+    e.h = 1;
+    if (x >= 60) {
+      const uint32_t nb = x - 59;
+      e.h = 1 + nb;
+      x = ext & (nb == 4 ? 0xffffffffu : (1u << (8 * nb)) - 1u);
+    }
+    e.len = x + 1;  // (x = 2^32 - 1 wraps to 0: rejected)
+    e.off = 0;
+  } else if (kind == 1) {
+    e.h = 2;
+    e.len = 4 + ((t >> 2) & 7);
+    e.off = ((t & 0xe0) << 3) | (ext & 0xff);
+  } else {
+    e.h = kind == 2 ? 3 : 5;
+    e.len = 1 + (t >> 2);
+    e.off = kind == 2 ? (ext & 0xffff) : ext;
+  }
+  return e;
+}
+// snappy.Decode's ErrCorrupt cases for the element at input offset s (n input
+// bytes) and output offset d (D output bytes)
+__device__ __forceinline__ bool sn_elem_ok(const SnElem& e, uint32_t s, uint32_t n, uint32_t d, uint32_t D) {
+  if (e.h > n - s || e.len > D - d) return false;
+  return e.lit ? (e.len != 0 && e.len <= n - s - e.h) : (e.off != 0 && e.off <= d);
+}
+__device__ __forceinline__ uint64_t sn_qent(const SnElem& e, uint32_t s, uint32_t d) {
+  return e.lit ? uint64_t(d) | uint64_t(e.len) << 16 | uint64_t(s + e.h) << 32
+               : uint64_t(d) | uint64_t(e.len) << 16 | uint64_t(e.off) << 32 | (1ull << 63);
+}
+
+// The whole wave: queue the elements starting at input offset *s (output
+// offset *d) until the queue or the input is full.  Returns the count; *ok
+// clears on a corrupt element.  The LDS words are read by every lane at one
+// address and made uniform with readfirstlane, so the walk's arithmetic and
+// branches are scalar; lane 0 writes the queue.
 __device__ __forceinline__ uint32_t sn_parse(lptr<const uint32_t> W, uint32_t ib, lptr<uint64_t> Q, uint32_t n,
                                              uint32_t D, uint32_t* s_io, uint32_t* d_io, bool* ok) {
   uint32_t s = *s_io, d = *d_io, c = 0;
@@ -66,72 +110,68 @@ __device__ __forceinline__ uint32_t sn_parse(lptr<const uint32_t> W, uint32_t ib
                          uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(W[q + 1]))) << 32;
     const uint32_t x2 = uint32_t(__builtin_amdgcn_readfirstlane(W[q + 2]));
     const uint64_t w = (x01 >> r) | (r ? uint64_t(x2) << (64 - r) : 0ull);  // bytes [a, a + 8)
-    const uint32_t t = uint32_t(w) & 0xff, kind = t & 3, ext = uint32_t(w >> 8);
-    uint32_t len, h;
-    uint64_t e;
-    if (kind == 0) {
-      uint32_t x = t >> 2;
-      h = 1;
-      if (x >= 60) {
-        const uint32_t nb = x - 59;
-        h = 1 + nb;
-        x = ext & (nb == 4 ? 0xffffffffu : (1u << (8 * nb)) - 1u);
-      }
-      len = x + 1;  // (x = 2^32 - 1 wraps to 0: rejected)
-      if (h > n - s || len == 0 || len > n - s - h || len > D - d) { *ok = false; break; }
-      e = uint64_t(d) | uint64_t(len) << 16 | uint64_t(s + h) << 32;
-      s += h + len;
-    } else {
-      uint32_t off;
-      if (kind == 1) {
-        h = 2;
-        len = 4 + ((t >> 2) & 7);
-        off = ((t & 0xe0) << 3) | (ext & 0xff);
-      } else {
-        h = kind == 2 ? 3 : 5;
-        len = 1 + (t >> 2);
-        off = kind == 2 ? (ext & 0xffff) : ext;
-      }
-      if (h > n - s || off == 0 || off > d || len > D - d) { *ok = false; break; }
-      e = uint64_t(d) | uint64_t(len) << 16 | uint64_t(off) << 32 | (1ull << 63);
-      s += h;
-    }
-    if (l0) Q[c] = e;
+    const SnElem e = sn_elem(w);
+    if (!sn_elem_ok(e, s, n, d, D)) { *ok = false; break; }
+    if (l0) Q[c] = sn_qent(e, s, d);
     c++;
-    d += len;
+    s += e.h + (e.lit ? e.len : 0u);
+    d += e.len;
   }
   *s_io = s;
   *d_io = d;
   return c;
 }
 
-// Copy sources resolved to the INPUT by pointer jumping.  r[j] of copy j holds
-// a position whose bytes equal the copy's source: first its output position
-// o - off, then, hop by hop, the source of the element whose output contains
-// that range (a literal: its input bytes -> resolved, kSnRes | input offset; a
-// copy without self-overlap: that copy's own r), so a chain of copies of
-// copies collapses in log rounds.  A range that straddles elements, reaches
-// before this round's queue or into a self-overlapping copy stays kSnStuck and
-// is copied from the output afterwards.  Races between lanes are benign: every
-// value r[k] takes is a valid source of copy k's bytes.
-constexpr uint32_t kSnRes = 1u << 31, kSnStuck = 1u << 30;
-__device__ __forceinline__ uint32_t sn_find(const lptr<const uint64_t> Q, uint32_t qc, uint32_t a) {
-  uint32_t lo = 0, hi = qc;  // the last element with dst <= a (qc when before the first)
-  if ((uint32_t(Q[0]) & 0xffffu) > a) return qc;
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if ((uint32_t(Q[mid]) & 0xffffu) <= a) lo = mid;
-    else hi = mid;
+constexpr uint32_t kSnWalkMin = 64;  // smaller blocks: sn_decode walks them itself
+
+// Copy sources by pointer jumping.  R[j] of copy j holds a position whose
+// final bytes equal the copy's: first its output position o - off; each round
+// finds the element whose output holds that range and replaces it by the same
+// range of that element's source -- a literal's input bytes (kSnRes | input
+// offset: resolved, copied with the literals), or a copy's own R (an output
+// position, strictly lower) -- so a chain of copies of copies collapses in log
+// rounds.  A range that straddles elements or lies before this round's queue
+// stops (kSnStop | output position).  Unresolved copies then run in output
+// order, a group at a time, each reading the final output at its position;
+// since chains collapse towards their roots, a group can take every copy whose
+// position range ends below the group's first output.  Races between lanes are
+// benign: every value R[k] takes is a valid source of copy k's bytes.
+// Overlapping copies (off < len) keep o - off and repeat their period.
+constexpr uint32_t kSnRes = 1u << 31, kSnStop = 1u << 30, kSnPos = 0xffffu;
+__device__ __forceinline__ uint32_t sn_dst(uint64_t e) { return uint32_t(e) & 0xffffu; }
+__device__ __forceinline__ uint32_t sn_len(uint64_t e) { return uint32_t(e >> 16) & 0xffffu; }
+__device__ __forceinline__ uint32_t sn_src(uint64_t e) { return uint32_t(e >> 32) & 0x7fffffffu; }
+// Buckets of the round's output: BK[c] = the element holding output offset
+// d0 + c * 2^kSnBkShift.
+__device__ __forceinline__ void sn_buckets(lptr<const uint64_t> QR, lptr<uint16_t> BK, uint32_t qc, uint32_t d0) {
+  const uint32_t lane = lane_id();
+  for (uint32_t i0 = 0; i0 < qc; i0 += kWave) {
+    const uint32_t j = i0 + lane;
+    uint32_t c0 = 0, c1 = 0;
+    if (j < qc) {
+      const uint64_t e = QR[j];
+      const uint32_t r = sn_dst(e) - d0, m = (1u << kSnBkShift) - 1;
+      c0 = (r + m) >> kSnBkShift;
+      c1 = (r + sn_len(e) + m) >> kSnBkShift;
+      if (c1 - c0 <= 4)
+        for (uint32_t c = c0; c < c1; c++) BK[c] = uint16_t(j);
+    }
+    for (uint64_t wm = __ballot(c1 - c0 > 4); wm; wm &= wm - 1) {
+      const int sl = __builtin_ctzll(wm);
+      const uint32_t a = __shfl(c0, sl, kWave), z = __shfl(c1, sl, kWave);
+      for (uint32_t c = a + lane; c < z; c += kWave) BK[c] = uint16_t(i0 + uint32_t(sl));
+    }
   }
-  return lo;
+  wave_sync();
 }
-__device__ __forceinline__ void sn_resolve(lptr<const uint64_t> QR, lptr<uint32_t> R, uint32_t qc) {
+__device__ __forceinline__ void sn_resolve(lptr<const uint64_t> QR, lptr<uint32_t> R, lptr<const uint16_t> BK,
+                                           uint32_t qc, uint32_t d0) {
   const uint32_t lane = lane_id();
   for (uint32_t j = lane; j < qc; j += kWave) {
     const uint64_t e = QR[j];
     if (e >> 63) {
-      const uint32_t o = uint32_t(e) & 0xffffu, len = uint32_t(e >> 16) & 0xffffu, off = uint32_t(e >> 32) & 0x7fffffffu;
-      R[j] = off < len ? kSnStuck : o - off;
+      const uint32_t o = sn_dst(e), len = sn_len(e), off = sn_src(e);
+      R[j] = (off < len ? kSnStop : 0u) | (o - off);
     }
   }
   wave_sync();
@@ -141,20 +181,25 @@ __device__ __forceinline__ void sn_resolve(lptr<const uint64_t> QR, lptr<uint32_
       const uint64_t e = QR[j];
       if (!(e >> 63)) continue;
       const uint32_t rj = R[j];
-      if (rj & (kSnRes | kSnStuck)) continue;
-      const uint32_t len = uint32_t(e >> 16) & 0xffffu;
-      const uint32_t k = sn_find(QR, qc, rj);
-      uint32_t nr = kSnStuck;
-      if (k < qc) {
+      if (rj & (kSnRes | kSnStop)) continue;
+      const uint32_t len = sn_len(e);
+      uint32_t nr = kSnStop | rj;
+      if (rj >= d0) {
+        uint32_t k = BK[(rj - d0) >> kSnBkShift];
+        while (k + 1 < qc && sn_dst(QR[k + 1]) <= rj) k++;
         const uint64_t ek = QR[k];
-        const uint32_t dk = uint32_t(ek) & 0xffffu, lk = uint32_t(ek >> 16) & 0xffffu;
-        if (rj + len <= dk + lk) {
+        const uint32_t dk = sn_dst(ek);
+        if (rj + len <= dk + sn_len(ek)) {
           if (!(ek >> 63)) {
-            nr = kSnRes | ((uint32_t(ek >> 32) & 0x7fffffffu) + (rj - dk));
+            nr = kSnRes | (sn_src(ek) + (rj - dk));
           } else {
             const uint32_t rk = R[k];
-            if (rk & kSnRes) nr = kSnRes | ((rk & ~kSnRes) + (rj - dk));
-            else if (!(rk & kSnStuck)) { nr = rk + (rj - dk); open = true; }
+            if (rk & kSnRes) {
+              nr = rk + (rj - dk);
+            } else {
+              nr = (rk & kSnPos) + (rj - dk);  // (< rj: another round)
+              open = true;
+            }
           }
         }
       }
@@ -166,7 +211,7 @@ __device__ __forceinline__ void sn_resolve(lptr<const uint64_t> QR, lptr<uint32_
   wave_sync();
 }
 
-// One snappy block: compressed bytes staged at byte ib of W (n bytes, the
+// One snappy block (those the walk does not cover): compressed bytes staged at byte ib of W (n bytes, the
 // uvarint header included), D decoded bytes to dst.  Uniform result: false = corrupt.
 __device__ bool sn_decode(Snap2Lds& S, uint32_t ib, uint32_t n, uint32_t used, uint32_t D, gptr<uint8_t> dst,
                           uint32_t g_sn_b = 0) {
@@ -176,17 +221,21 @@ __device__ bool sn_decode(Snap2Lds& S, uint32_t ib, uint32_t n, uint32_t used, u
   lptr<uint64_t> Q = to_lds_ptr(S.q);
   const lptr<const uint64_t> QR = to_lds_ptr(static_cast<const uint64_t*>(S.q));
   lptr<uint32_t> R = to_lds_ptr(S.r);
+  lptr<uint16_t> BK = to_lds_ptr(S.bk);
   uint32_t s = used, d = 0;
   bool ok = true;
   while (s < n) {
-    uint32_t qc = 0;
+    const uint32_t dr = d;  // the round's first output offset
     SN_T(t0);
-    qc = sn_parse(W, ib, Q, n, D, &s, &d, &ok);
+    const uint32_t qc = sn_parse(W, ib, Q, n, D, &s, &d, &ok);
     if (!ok) return false;
     wave_sync();
     SN_ACC(1, t0);
     SN_T(t1);
-    sn_resolve(QR, R, qc);
+    sn_buckets(QR, BK, qc, dr);
+    sn_resolve(QR, R, to_lds_ptr(static_cast<const uint16_t*>(S.bk)), qc, dr);
+    SN_ACC(6, t1);
+    SN_T(t1b);
     // literals and resolved copies: lane per element, from the staged input
     for (uint32_t i0 = 0; i0 < qc; i0 += kWave) {
       const uint32_t i = i0 + lane;
@@ -218,7 +267,7 @@ __device__ bool sn_decode(Snap2Lds& S, uint32_t ib, uint32_t n, uint32_t used, u
       }
     }
     sn_fence();
-    SN_ACC(2, t1);
+    SN_ACC(2, t1b);
     SN_T(t2);
     // copies: groups of independent ones, lane per copy
     uint32_t i = 0;
@@ -236,13 +285,15 @@ __device__ bool sn_decode(Snap2Lds& S, uint32_t ib, uint32_t n, uint32_t used, u
       const uint32_t o = uint32_t(e) & 0xffffu, len = uint32_t(e >> 16) & 0xffffu,
                      off = uint32_t(e >> 32) & 0x7fffffffu;
       const uint32_t d0 = __shfl(o, first, kWave);
-      // bytes read below its own output: [o - off, o - off + min(len, off))
-      const bool indep = isc && (o - off + (len < off ? len : off) <= d0);
+      // final bytes at [P, P + len) (an overlapping copy: its period [o - off, o))
+      const bool ovl = off < len;
+      const uint32_t P = ovl ? o - off : (isc ? R[j] & kSnPos : 0u);
+      const bool indep = isc && (ovl ? o <= d0 : P + len <= d0);
       const uint64_t stop = first == 63 ? 0ull : (__ballot(isc && !indep) & ~((2ull << first) - 1));
       const uint32_t end = stop ? uint32_t(__builtin_ctzll(stop)) : uint32_t(kWave);  // lanes [first, end) run
       if (isc && uint32_t(lane) >= uint32_t(first) && uint32_t(lane) < end) {
-        const gptr<const uint8_t> sp = dst + (o - off);
-        if (off >= 16) {
+        const gptr<const uint8_t> sp = dst + P;
+        if (!ovl || off >= 16) {  // (an overlapping copy: each chunk's source is written before it)
           for (uint32_t c = 0; c < len; c += 16) {
             const u32x4 v = *(gptr<const sn_u32x4_u>)(sp + c);
             sn_store_n(dst + o + c, make_uint4(v.x, v.y, v.z, v.w), len - c < 16 ? len - c : 16u);
@@ -268,3 +319,331 @@ __device__ bool sn_decode(Snap2Lds& S, uint32_t ib, uint32_t n, uint32_t used, u
   return d == D;
 }
 
+
+// ==== snappy4: the blocks the walk covers (sn4_walkable) ======================
+// snappy_walk_kernel walks each block's element chain on one lane (64 blocks
+// per wave: the chain's latency becomes throughput), validates every element
+// and leaves, in the block's own output region, which the decode overwrites
+// afterwards:
+//   out[0, 16)             {ok, elements, D, n}
+//   out[16, 16 + 4 nw)     the tag bitmap: bit i of word w = an element's tag
+//                          at input offset 32 w + i (nw = ceil(n / 32))
+// snappy4_kernel then decodes a block per wave with nothing staged: the tag
+// offsets come from the bitmap (a popcount scan), every element decodes on its
+// own lane from the input in HBM, output offsets by a scan of the lengths; an
+// output-start bitmap with per-word counts finds the element holding any
+// output offset with one LDS round trip, so the copy-chain pointer jumping
+// (sn_resolve's scheme) runs with each lane's copies in registers.  20 KB of
+// LDS: 8 blocks per CU.
+constexpr uint32_t kS4In = 32768, kS4Span = 32768, kS4Q = 768, kS4Slots = kS4Q / kWave;
+struct Snap4Lds {
+  uint64_t q[kS4Q];           // dst | len << 16 | (src or offset) << 32 | copy << 63
+  uint32_t r[kS4Q];           // copies: where their bytes are (kSnRes / kSnStop / output offset)
+  uint32_t tb[kS4In / 32];    // the walk's tag bitmap
+  uint32_t ob[kS4Span / 32];  // the round's element starts, by output offset - the round's first
+  uint16_t pf[kS4Span / 64];  // element starts before each 64-bit word of ob
+  uint16_t cl[kS4Q];          // the round's copies, in order
+};
+__device__ __forceinline__ bool sn4_walkable(uint32_t n, uint32_t D) {
+  return n >= 8 && n <= kS4In && D >= kSnWalkMin && D <= kS4Span && D >= 16 + 4 * ((n + 31) / 32);
+}
+// bytes [s, s + 8) (s < n) reading nothing past p[n] (the block's indicator)
+__device__ __forceinline__ uint64_t sn_load8c(gptr<const uint8_t> p, uint32_t s, uint32_t n) {
+  const uint32_t a = s < n - 7 ? s : n - 7;
+  return *(gptr<const sn_u64_u>)(p + a) >> (8 * (s - a));
+}
+// bytes [s, s + 16) (s < n; past p[n]: unspecified)
+__device__ __forceinline__ uint4 sn_load16c(gptr<const uint8_t> p, uint32_t s, uint32_t n) {
+  if (s + 16 <= n + 1) {
+    const u32x4 v = *(gptr<const sn_u32x4_u>)(p + s);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  }
+  const uint64_t lo = sn_load8c(p, s, n), hi = s + 8 < n ? sn_load8c(p, s + 8, n) : 0ull;
+  return make_uint4(uint32_t(lo), uint32_t(lo >> 32), uint32_t(hi), uint32_t(hi >> 32));
+}
+__device__ __forceinline__ uint32_t sn_scan(uint32_t v) {  // inclusive, over the wave
+  const uint32_t lane = lane_id();
+  for (uint32_t o = 1; o < uint32_t(kWave); o <<= 1) {
+    const uint32_t t = __shfl(v, lane >= o ? int(lane - o) : int(lane), kWave);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+#ifndef SN_LDS_OR
+#define SN_LDS_OR(p, v) __hip_atomic_fetch_or((p), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+#endif
+
+// One lane: the walk of a block (n input bytes from `used` on, D output bytes).
+__device__ __forceinline__ void sn4_walk(gptr<const uint8_t> p, uint32_t n, uint32_t used, uint32_t D,
+                                         gptr<uint8_t> out) {
+  const gptr<uint8_t> bm = out + 16;
+  const uint32_t nw = (n + 31) / 32;
+  uint32_t s = used, d = 0, cnt = 0, ok = 1, cw = 0, acc = 0;
+  uint64_t w = s < n ? sn_load8c(p, s, n) : 0ull;
+  while (s < n) {
+    const SnElem e = sn_elem(w);
+    if (!sn_elem_ok(e, s, n, d, D)) { ok = 0; break; }
+    const uint32_t s0 = s;
+    s += e.h + (e.lit ? e.len : 0u);
+    d += e.len;
+    // the next tag's load before this element's stores: loads and stores
+    // retire in order, so the next step waits for the load alone
+    if (s < n) w = sn_load8c(p, s, n);
+    for (; cw < (s0 >> 5); cw++, acc = 0) *(gptr<sn_u32_u>)(bm + 4 * cw) = acc;
+    acc |= 1u << (s0 & 31);
+    cnt++;
+  }
+  if (ok)
+    for (; cw < nw; cw++, acc = 0) *(gptr<sn_u32_u>)(bm + 4 * cw) = acc;
+  *(gptr<sn_u32x4_u>)out = u32x4{ok && d == D ? 1u : 0u, cnt, d, s};
+}
+
+// The element holding output offset a (d0 <= a < the round's end).
+__device__ __forceinline__ uint32_t sn4_find(lptr<const uint32_t> OB, lptr<const uint16_t> PF, uint32_t x) {
+  const uint32_t w = x >> 6;
+  const uint64_t b = uint64_t(OB[2 * w]) | uint64_t(OB[2 * w + 1]) << 32;
+  return uint32_t(PF[w]) + uint32_t(__builtin_popcountll(b & (~0ull >> (63 - (x & 63))))) - 1u;
+}
+
+// Pointer jumping (as sn_resolve) with each lane's copies in registers: copy
+// g of the round's list on lane g % 64, slot g / 64; every round reads the
+// state it needs first and writes all new states after (the wave in lockstep).
+__device__ __forceinline__ void sn4_resolve(lptr<const uint64_t> QR, lptr<uint32_t> R, lptr<const uint16_t> CL,
+                                            lptr<const uint32_t> OB, lptr<const uint16_t> PF, uint32_t cc,
+                                            uint32_t dr) {
+  const uint32_t lane = lane_id();
+  uint32_t sj[kS4Slots], sl[kS4Slots], sr[kS4Slots];
+#pragma unroll
+  for (uint32_t t = 0; t < kS4Slots; t++) {
+    const uint32_t g = lane + kWave * t;
+    sj[t] = 0;
+    sl[t] = 0;
+    sr[t] = kSnStop;
+    if (g < cc) {
+      sj[t] = CL[g];
+      const uint64_t e = QR[sj[t]];
+      const uint32_t o = sn_dst(e), len = sn_len(e), off = sn_src(e);
+      sl[t] = len;
+      sr[t] = (off < len ? kSnStop : 0u) | (o - off);
+      R[sj[t]] = sr[t];
+    }
+  }
+  wave_sync();
+  for (int round = 0; round < 16; round++) {
+    bool open = false;
+    uint32_t nr[kS4Slots];
+#pragma unroll
+    for (uint32_t t = 0; t < kS4Slots; t++) {
+      const uint32_t x = sr[t];
+      nr[t] = x;
+      if (!(x & (kSnRes | kSnStop))) {
+        nr[t] = kSnStop | x;
+        if (x >= dr) {
+          const uint32_t k = sn4_find(OB, PF, x - dr);
+          const uint64_t ek = QR[k];
+          const uint32_t dk = sn_dst(ek);
+          if (x + sl[t] <= dk + sn_len(ek)) {
+            if (!(ek >> 63)) {
+              nr[t] = kSnRes | (sn_src(ek) + (x - dk));
+            } else {
+              const uint32_t rk = R[k];
+              if (rk & kSnRes) {
+                nr[t] = rk + (x - dk);
+              } else {
+                nr[t] = (rk & kSnPos) + (x - dk);  // (< x: another round)
+                open = true;
+              }
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (uint32_t t = 0; t < kS4Slots; t++) {
+      if (lane + kWave * t < cc && nr[t] != sr[t]) R[sj[t]] = nr[t];
+      sr[t] = nr[t];
+    }
+    wave_sync();
+    if (!__ballot(open)) break;
+  }
+}
+
+// One block the walk covers: n input bytes at src (HBM), D output bytes to dst
+// (holding the walk's header and bitmap).  Uniform result: false = corrupt.
+__device__ bool sn4_decode(Snap4Lds& S, gptr<const uint8_t> src, uint32_t n, uint32_t D, gptr<uint8_t> dst,
+                           uint32_t g_sn_b = 0) {
+  const uint32_t lane = lane_id();
+  (void)g_sn_b;
+  lptr<uint64_t> Q = to_lds_ptr(S.q);
+  const lptr<const uint64_t> QR = to_lds_ptr(static_cast<const uint64_t*>(S.q));
+  lptr<uint32_t> R = to_lds_ptr(S.r);
+  lptr<uint32_t> TB = to_lds_ptr(S.tb);
+  lptr<uint32_t> OB = to_lds_ptr(S.ob);
+  lptr<uint16_t> PF = to_lds_ptr(S.pf);
+  lptr<uint16_t> CL = to_lds_ptr(S.cl);
+  SN_T(ts);
+  const u32x4 hd = *(gptr<const sn_u32x4_u>)dst;  // (read before any output is written)
+  if (!hd[0]) return false;
+  const uint32_t nw = (n + 31) / 32;
+  for (uint32_t w = lane; w < nw; w += kWave) TB[w] = *(gptr<const sn_u32_u>)(dst + 16 + 4 * w);
+  wave_sync();
+  SN_ACC(0, ts);
+  uint32_t wc = 0, d = 0;
+  while (wc < nw) {
+    const uint32_t dr = d;
+    SN_T(t0);
+    // 1. the round's tag offsets from the bitmap (whole words, <= kS4Q)
+    uint32_t qc = 0;
+    for (;;) {
+      const uint32_t w = wc + lane;
+      const uint32_t bits = w < nw ? TB[w] : 0u;
+      const uint32_t c = uint32_t(__builtin_popcount(bits));
+      const uint32_t incl = sn_scan(c);
+      const bool take = w < nw && qc + incl <= kS4Q;
+      const uint64_t tm = __ballot(take);
+      if (take) {
+        uint32_t k = qc + incl - c;
+        for (uint32_t b = bits; b; b &= b - 1) Q[k++] = 32 * w + uint32_t(__builtin_ctz(b));
+      }
+      const uint32_t na = uint32_t(__builtin_popcountll(tm));
+      if (na) qc += __shfl(incl, int(na - 1), kWave);
+      wc += na;
+      if (na < uint32_t(kWave)) break;
+    }
+    for (uint32_t i = lane; i < kS4Span / 32; i += kWave) OB[i] = 0;
+    wave_sync();
+    // 2. the elements, a lane each: decode, output offsets, output starts
+    uint64_t wv[kS4Slots];
+#pragma unroll
+    for (uint32_t t = 0; t < kS4Slots; t++) {
+      const uint32_t i = lane + kWave * t;
+      wv[t] = i < qc ? sn_load8c(src, uint32_t(QR[i]), n) : 0ull;
+    }
+#pragma unroll
+    for (uint32_t t = 0; t < kS4Slots; t++) {
+      if (kWave * t >= qc) break;
+      const uint32_t i = lane + kWave * t;
+      SnElem e{0, 0, 0, true};
+      uint32_t pos = 0;
+      if (i < qc) {
+        pos = uint32_t(QR[i]);
+        e = sn_elem(wv[t]);
+      }
+      const uint32_t incl = sn_scan(e.len), o = d + incl - e.len;
+      if (i < qc) {
+        Q[i] = sn_qent(e, pos, o);
+        SN_LDS_OR(OB + ((o - dr) >> 5), 1u << ((o - dr) & 31));
+      }
+      d += __shfl(incl, kWave - 1, kWave);
+    }
+    wave_sync();
+    // element starts before each 64-bit word of OB (8 words a lane)
+    {
+      uint32_t cnt[8], tot = 0;
+#pragma unroll
+      for (uint32_t t = 0; t < 8; t++) {
+        const uint32_t w = 8 * lane + t;
+        cnt[t] = uint32_t(__builtin_popcountll(uint64_t(OB[2 * w]) | uint64_t(OB[2 * w + 1]) << 32));
+        tot += cnt[t];
+      }
+      uint32_t run = sn_scan(tot) - tot;
+#pragma unroll
+      for (uint32_t t = 0; t < 8; t++) {
+        PF[8 * lane + t] = uint16_t(run);
+        run += cnt[t];
+      }
+    }
+    // the round's copies, in order
+    uint32_t cc = 0;
+    for (uint32_t i0 = 0; i0 < qc; i0 += kWave) {
+      const uint32_t i = i0 + lane;
+      const bool isc = i < qc && (QR[i] >> 63);
+      const uint64_t m = __ballot(isc);
+      if (isc) CL[cc + uint32_t(__builtin_popcountll(m & ((1ull << lane) - 1)))] = uint16_t(i);
+      cc += uint32_t(__builtin_popcountll(m));
+    }
+    wave_sync();
+    SN_ACC(1, t0);
+    SN_T(t1);
+    // 3. copy sources
+    sn4_resolve(QR, R, to_lds_ptr(static_cast<const uint16_t*>(S.cl)), to_lds_ptr(static_cast<const uint32_t*>(S.ob)),
+                to_lds_ptr(static_cast<const uint16_t*>(S.pf)), cc, dr);
+    SN_ACC(6, t1);
+    SN_T(t1b);
+    // 4. literals and resolved copies: lane per element, from the input
+    for (uint32_t i0 = 0; i0 < qc; i0 += kWave) {
+      const uint32_t i = i0 + lane;
+      uint32_t len = 0, x = 0, o = 0;
+      if (i < qc) {
+        const uint64_t e = QR[i];
+        o = sn_dst(e);
+        len = sn_len(e);
+        x = sn_src(e);
+        if (e >> 63) {
+          const uint32_t ri = R[i];
+          if (ri & kSnRes) x = ri & ~kSnRes;
+          else len = 0;
+        }
+      }
+      if (len && len <= 256)
+        for (uint32_t c = 0; c < len; c += 16) sn_store_n(dst + o + c, sn_load16c(src, x + c, n), len - c < 16 ? len - c : 16u);
+      for (uint64_t m = __ballot(len > 256); m; m &= m - 1) {
+        const int sl = __builtin_ctzll(m);
+        const uint32_t lo = __shfl(o, sl, kWave), ls = __shfl(x, sl, kWave), ll = __shfl(len, sl, kWave);
+        for (uint32_t c = 16 * lane; c < ll; c += 16 * kWave)
+          sn_store_n(dst + lo + c, sn_load16c(src, ls + c, n), ll - c < 16 ? ll - c : 16u);
+      }
+    }
+    sn_fence();
+    SN_ACC(2, t1b);
+    SN_T(t2);
+    // 5. the other copies in output order, groups of independent ones (sn_decode's)
+    uint32_t g = 0;
+    while (g < cc) {
+      const uint32_t gi = g + lane;
+      uint32_t j = 0, ri = kSnRes;
+      if (gi < cc) {
+        j = CL[gi];
+        ri = R[j];
+      }
+      const bool isc = gi < cc && !(ri & kSnRes);
+      const uint64_t cm = __ballot(isc);
+      if (!cm) {
+        g += kWave;
+        continue;
+      }
+      const int first = __builtin_ctzll(cm);
+      const uint64_t e = isc ? QR[j] : 0ull;
+      const uint32_t o = sn_dst(e), len = sn_len(e), off = sn_src(e);
+      const uint32_t d0 = __shfl(o, first, kWave);
+      const bool ovl = off < len;
+      const uint32_t P = ovl ? o - off : (ri & kSnPos);
+      const bool indep = isc && (ovl ? o <= d0 : P + len <= d0);
+      const uint64_t stop = first == 63 ? 0ull : (__ballot(isc && !indep) & ~((2ull << first) - 1));
+      const uint32_t end = stop ? uint32_t(__builtin_ctzll(stop)) : uint32_t(kWave);
+      if (isc && uint32_t(lane) >= uint32_t(first) && uint32_t(lane) < end) {
+        const gptr<const uint8_t> sp = dst + P;
+        if (!ovl || off >= 16) {
+          for (uint32_t c = 0; c < len; c += 16) {
+            const u32x4 v = *(gptr<const sn_u32x4_u>)(sp + c);
+            sn_store_n(dst + o + c, make_uint4(v[0], v[1], v[2], v[3]), len - c < 16 ? len - c : 16u);
+          }
+        } else {
+          uint8_t per[16];
+          for (uint32_t k = 0; k < off; k++) per[k] = sp[k];
+          for (uint32_t k = 0; k < len; k++) dst[o + k] = per[k % off];
+        }
+      }
+      sn_fence();
+      g += end;
+#ifdef PBL_SNAP_STAMPS
+      if (lane == 0 && g_sn_b < 65536) g_snap_stamps[8 * g_sn_b + 5] += 1;  // groups
+#endif
+    }
+    SN_ACC(3, t2);
+#ifdef PBL_SNAP_STAMPS
+    if (lane == 0 && g_sn_b < 65536) g_snap_stamps[8 * g_sn_b + 4] += 1;  // rounds
+#endif
+  }
+  return d == D;
+}

@@ -40,6 +40,6 @@ assert not st.any()
 h = np.zeros(65536 * 8, np.uint64)
 assert f(h.ctypes.data, 65536 * 8, 0) == 0
 h = h.reshape(65536, 8)[:nb].astype(np.float64)
-names = ["stage", "parse", "literals", "copies", "calls", "groups"]
+names = ["stage", "parse", "literals", "copies", "calls", "groups", "resolve"]
 for k, nm in enumerate(names):
     print(f"{nm:10s} median {np.median(h[:, k]):10.0f} mean {h[:, k].mean():10.0f} p90 {np.percentile(h[:, k], 90):10.0f}")

@@ -7,6 +7,7 @@
 #include <barrier>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -56,6 +57,7 @@ static uint32_t emu_alignbyte(uint32_t hi, uint32_t lo, uint32_t r) {
 #define __builtin_amdgcn_alignbyte(a, b, c) emu_alignbyte(a, b, c)
 #define __builtin_amdgcn_fence(a, b) ((void)0)
 #define __builtin_amdgcn_wave_barrier() g_bar->arrive_and_wait()
+#define SN_LDS_OR(p, v) __atomic_fetch_or((p), (v), __ATOMIC_RELAXED)
 #define SN_T(v)
 #define SN_ACC(i, v)
 using std::min;
@@ -70,7 +72,7 @@ constexpr uint32_t kSnQ = 592;
 int main(int argc, char** argv) {
   if (argc < 2) return 2;
   FILE* f = fopen(argv[1], "rb");
-  std::vector<uint8_t> in(1 << 20);
+  std::vector<uint8_t> in(1 << 20);  // (zero past the block: the indicator byte's place)
   const size_t n = fread(in.data(), 1, in.size(), f);
   fclose(f);
   uint64_t D = 0;
@@ -83,6 +85,10 @@ int main(int argc, char** argv) {
   if (n > pbl::phys::kSnIn || D > 0xffff) return 3;
   std::memcpy(S.in, in.data(), n);
   std::vector<uint8_t> out(D + 64);
+  // snappy_walk_kernel's lane for this block, then snappy4's decode (or snappy2's)
+  const bool walked = pbl::phys::sn4_walkable(uint32_t(n), uint32_t(D)) && !getenv("EMU_NO_WALK");
+  if (walked) pbl::phys::sn4_walk(in.data(), uint32_t(n), used, uint32_t(D), out.data());
+  static pbl::phys::Snap4Lds S4;
   std::barrier<> bar(64);
   g_bar = &bar;
   bool res[64];
@@ -90,7 +96,8 @@ int main(int argc, char** argv) {
   for (int l = 0; l < 64; l++)
     th.emplace_back([&, l] {
       g_lane = l;
-      res[l] = pbl::phys::sn_decode(S, 0, uint32_t(n), used, uint32_t(D), out.data());
+      res[l] = walked ? pbl::phys::sn4_decode(S4, in.data(), uint32_t(n), uint32_t(D), out.data())
+                      : pbl::phys::sn_decode(S, 0, uint32_t(n), used, uint32_t(D), out.data());
     });
   for (auto& t : th) t.join();
   printf("ok %d D %llu\n", int(res[0]), (unsigned long long)D);

@@ -50,3 +50,32 @@ def test_emulated_snappy_decoder_matches_oracle(emu, tmp_path):
     for data in [bytes(buf[int(off[0]):int(off[0]) + int(lens[0])]), text, b"ab" * 9000, rng.randbytes(20000)]:
         raw = pa.Codec("snappy").compress(data, asbytes=True)
         assert run(emu, tmp_path, raw) == data
+
+
+def _uvarint(n):
+    out = bytearray()
+    while n >= 0x80:
+        out.append(n & 0x7F | 0x80)
+        n >>= 7
+    out.append(n)
+    return bytes(out)
+
+
+def test_emulated_walk_capacity_and_overwrite_paths(emu, tmp_path, monkeypatch):
+    """Blocks of 1-byte literals (more elements than one snappy4 round holds,
+    every output byte its own element), the scalar-walk decode of snappy2
+    (EMU_NO_WALK) and a corrupt block the walk rejects."""
+    rng = random.Random(11)
+    for d_len in (200, 4000):
+        data = rng.randbytes(d_len)
+        raw = _uvarint(d_len) + b"".join(bytes([0, c]) for c in data)  # 1-byte literals
+        assert oracle.snappy_decode(raw) == data
+        assert run(emu, tmp_path, raw) == data
+    import pyarrow as pa
+    text = b" ".join(rng.choice([b"alpha", b"beta", b"gamma", b"delta"]) for _ in range(5000))
+    raw = pa.Codec("snappy").compress(text, asbytes=True)
+    monkeypatch.setenv("EMU_NO_WALK", "1")
+    assert run(emu, tmp_path, raw) == text
+    # corrupt: a copy reaching before the output start
+    bad = _uvarint(100) + bytes([0, 65]) + bytes([1 | (7 << 2), 9]) + bytes([0, 66]) * 10
+    assert run(emu, tmp_path, bad) is None
