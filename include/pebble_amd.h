@@ -93,6 +93,9 @@ enum {
 #define PBL_KERNEL_FLAT 0x800u    /* A/B measurement, no effect on results: row
                                      batches on the one-wave-per-block kernel
                                      (rowblk_flat.hip.h) even without VARLEN        */
+#define PBL_KERNEL_RUN 0x1000u    /* A/B measurement, no effect on results: row
+                                     batches on the run-major one-wave-per-block
+                                     kernel (rowblk_run.hip.h)                      */
 
 /* per-KV flag byte (kv_flags[]) */
 #define PBL_KV_RESTART 0x01u       /* entry offset is a restart point            */

@@ -800,6 +800,7 @@ __global__ void __launch_bounds__(kTPB, 3) rowblk_decode_kernel(Args A) {
 
 #include "rowblk_pipe.hip.h"
 #include "rowblk_flat.hip.h"
+#include "rowblk_run.hip.h"
 
 // Mixed row + colblk batch (config 4): per-block format from block_format[];
 // both paths share the ticket order and the look-back state.
@@ -1119,6 +1120,23 @@ int launch_row_flat(const pbl::Args& a, hipStream_t st, bool values) {
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }
 
+// Row batches on the run-major kernel (rowblk_run.hip.h), with the same
+// big-block passes around it.
+int launch_row_run(const pbl::Args& a, hipStream_t st, bool values) {
+  const uint32_t nb = a.in.n_blocks;
+  int cus = 0;
+  const uint64_t grid = pbl::persistent_grid(st, pbl::kKRowRun,
+                                             reinterpret_cast<const void*>(pbl::row::runk::rowblk_run_kernel),
+                                             (uint64_t(nb) + pbl::row::runk::kRW - 1) / pbl::row::runk::kRW, &cus,
+                                             pbl::row::runk::kRTPB);
+  if (!grid) return PBL_DEVICE_ERROR;
+  const uint32_t small = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4));
+  hipLaunchKernelGGL(pbl::row::pipe::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+  hipLaunchKernelGGL(pbl::row::runk::rowblk_run_kernel, dim3(uint32_t(grid)), dim3(pbl::row::runk::kRTPB), 0, st, a);
+  if (values) hipLaunchKernelGGL(pbl::row::pipe::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+  return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
+}
+
 // Mixed batches: PBL_KERNEL_SINGLE keeps the one-block-per-workgroup kernel
 // (A/B); the default splits the ids by format and runs the mixed pipeline,
 // with the big row blocks' size / value passes around it.
@@ -1201,6 +1219,7 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
     // blocks).  PBL_KERNEL_SINGLE selects the one-block-per-workgroup
     // persistent kernel (kept for A/B measurement); the default is the pipeline.
     const bool single = (batch->flags & PBL_KERNEL_SINGLE) != 0;
+    if (!single && (batch->flags & PBL_KERNEL_RUN)) return launch_row_run(a, st, true);
     if (!single && use_flat(batch->flags)) return launch_row_flat(a, st, true);
     const void* fn = single ? reinterpret_cast<const void*>(pbl::row::rowblk_decode_kernel)
                             : reinterpret_cast<const void*>(pbl::row::pipe::rowblk_pipe_kernel);
@@ -1263,6 +1282,9 @@ int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stre
     // pointers), minus the big-block value pass
     if (batch->block_format) {
       rc = launch_mixed(batch, a, st, batch->flags & PBL_KERNEL_SINGLE, false);
+      if (rc != PBL_OK) return rc;
+    } else if (batch->flags & PBL_KERNEL_RUN) {
+      rc = launch_row_run(a, st, false);
       if (rc != PBL_OK) return rc;
     } else if (use_flat(batch->flags)) {
       rc = launch_row_flat(a, st, false);

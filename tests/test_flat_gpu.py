@@ -1,5 +1,5 @@
-"""The one-wave-per-block row kernel (rowblk_flat.hip.h, batch flag
-PBL_KERNEL_FLAT) against the oracle: bit-exact on every output array, over the
+"""The one-wave-per-block row kernels (rowblk_flat.hip.h, batch flag
+PBL_KERNEL_FLAT; rowblk_run.hip.h, PBL_KERNEL_RUN) against the oracle: bit-exact on every output array, over the
 same inputs as the pipeline's parity tests (reference blocks, synthetic
 configs, random and fuzzed blocks, value prefixes, blocks past the LDS limits,
 the general-path fallbacks)."""
@@ -15,47 +15,53 @@ from pebble_amd.rowblk import Writer, gen_row_blocks
 from test_rowblk_gpu import GOLDEN, assert_same, pack, random_block
 
 pytestmark = pytest.mark.gpu
+KERNELS = {"flat": N.PBL_KERNEL_FLAT, "run": N.PBL_KERNEL_RUN}
 FLAT = N.PBL_KERNEL_FLAT
 
 
-def check(buf, off, lens, flags=0, ctx=""):
+@pytest.fixture(params=sorted(KERNELS))
+def kern(request):
+    return KERNELS[request.param]
+
+
+def check(buf, off, lens, flags=0, ctx="", kern=FLAT):
     from pebble_amd.batch import BlockBatch, decode
     o = oracle.rowblk_decode_batch(buf, off, lens, flags)
-    g = decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, flags | FLAT)).to_host()
-    assert_same(g, o, ctx)
+    g = decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, flags | kern)).to_host()
+    assert_same(g, o, f"{ctx} kernel={kern:#x}")
     return g
 
 
-def test_flat_hamlet_and_golden(golden):
+def test_flat_hamlet_and_golden(golden, kern):
     g = golden["h_no_compression"]
     blob = np.fromfile(os.path.join(GOLDEN, "h_no_compression_blocks.bin"), np.uint8)
     blob = np.concatenate([blob, np.zeros(16, np.uint8)])
-    check(blob, np.array(g["block_off"], np.uint64), np.array(g["block_len"], np.uint32), 0, "hamlet")
+    check(blob, np.array(g["block_off"], np.uint64), np.array(g["block_len"], np.uint32), 0, "hamlet", kern)
     wp = bytes.fromhex(golden["writer_with_prefix"]["block_hex"])
     wb = bytes.fromhex(golden["writer_basic"]["block_hex"])
     for flags in (0, N.PBL_ROW_VALUE_PREFIX, N.PBL_ROW_RAW_KEYS):
-        check(*pack([wp, wb, wp]), flags, f"golden flags={flags}")
+        check(*pack([wp, wb, wp]), flags, f"golden flags={flags}", kern)
 
 
 @pytest.mark.parametrize("ri", [1, 2, 16, 17, 32, 64])
 @pytest.mark.parametrize("kl,vl", [(16, 100), (8, 0), (64, 7), (24, 1000)])
 @pytest.mark.parametrize("vp", [False, True])
-def test_flat_synthetic_batches(ri, kl, vl, vp):
+def test_flat_synthetic_batches(ri, kl, vl, vp, kern):
     for bs in (4096, 32768):
         buf, off, lens, n = gen_row_blocks(1000 + ri + kl + vl, 48, bs, ri, kl, vl, vp)
-        g = check(buf, off, lens, N.PBL_ROW_VALUE_PREFIX if vp else 0, f"ri={ri} kl={kl} vl={vl} vp={vp} bs={bs}")
+        g = check(buf, off, lens, N.PBL_ROW_VALUE_PREFIX if vp else 0, f"ri={ri} kl={kl} vl={vl} vp={vp} bs={bs}", kern)
         assert g["n_kv"] == n
 
 
-def test_flat_random_blocks():
+def test_flat_random_blocks(kern):
     rng = random.Random(4321)
     for flags in (0, N.PBL_ROW_VALUE_PREFIX, N.PBL_ROW_VALUE_PREFIX | N.PBL_ROW_NO_VALUER, N.PBL_ROW_RAW_KEYS):
         blocks = [random_block(rng)[0] for _ in range(300)]
         for align in (8, 1):
-            check(*pack(blocks, align), flags, f"random flags={flags} align={align}")
+            check(*pack(blocks, align), flags, f"random flags={flags} align={align}", kern)
 
 
-def test_flat_fuzzed_blocks():
+def test_flat_fuzzed_blocks(kern):
     rng = random.Random(98)
     blocks = []
     for _ in range(400):
@@ -71,26 +77,26 @@ def test_flat_fuzzed_blocks():
         blocks.append(bytes(b))
     blocks += [b"", b"\x00", b"\x00\x00\x00\x00", Writer(16).finish()]
     for flags in (0, N.PBL_ROW_VALUE_PREFIX):
-        g = check(*pack(blocks, 8), flags, f"fuzz flags={flags}")
+        g = check(*pack(blocks, 8), flags, f"fuzz flags={flags}", kern)
         assert g["n_bad_blocks"] > 0
 
 
 @pytest.mark.parametrize("bs", [65536, 200000])
-def test_flat_blocks_past_the_limit(bs):
+def test_flat_blocks_past_the_limit(bs, kern):
     buf, off, lens, n = gen_row_blocks(5, 6, bs, 16, 16, 100)
     small = gen_row_blocks(6, 10, 32768, 16, 16, 100)
     blocks = [bytes(buf[o:o + l]) for o, l in zip(off, lens)] + [bytes(small[0][o:o + l]) for o, l in zip(small[1], small[2])]
     rng = random.Random(bs)
     rng.shuffle(blocks)
-    check(*pack(blocks), 0, f"bs={bs}")
+    check(*pack(blocks), 0, f"bs={bs}", kern)
 
 
-def test_flat_config2_full_size_sha():
+def test_flat_config2_full_size_sha(kern):
     import hashlib
     from pebble_amd.batch import BlockBatch, decode
     buf, off, lens, n = gen_row_blocks(42, 65536, 32768, 16, 16, 100, n_threads=16)
     gp = decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, N.PBL_KERNEL_PIPE)).to_host()
-    gf = decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, FLAT)).to_host()
+    gf = decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, kern)).to_host()
     for k in ("trailer", "kv_flags", "entry_off", "key_off", "val_off", "key_bytes", "val_bytes", "restarts",
               "blk_kv_base", "blk_key_base", "blk_val_base", "blk_rst_base", "blk_status"):
         assert hashlib.sha256(gp[k].tobytes()).digest() == hashlib.sha256(gf[k].tobytes()).digest(), k
