@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define PBL_ABI_VERSION 6
+#define PBL_ABI_VERSION 7
 
 /* ---- status codes (per block, and OR-ed as bit masks into totals) ---------- */
 enum {
@@ -210,8 +210,9 @@ int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stre
  *   sizeof(pbl_block_batch), the offsets of its 9 fields in declaration order,
  *   sizeof(pbl_totals), the offsets of its 8 fields,
  *   sizeof(pbl_decode_out), the offsets of its 20 fields,
- *   then likewise pbl_transforms, pbl_footer, pbl_index_out, pbl_kv_out and
- *   pbl_value_out (sizeof, then every field's offset in declaration order).
+ *   then likewise pbl_transforms, pbl_footer, pbl_index_out, pbl_kv_out,
+ *   pbl_value_out and pbl_kv (sizeof, then every field's offset in declaration
+ *   order).
  */
 size_t pbl_struct_layout(uint64_t* out, size_t cap);
 
@@ -557,6 +558,56 @@ typedef struct pbl_zipf_config {
 uint64_t pbl_gen_zipf_blocks(const pbl_zipf_config* cfg, uint32_t format, uint32_t n_blocks,
                              uint8_t* dst, uint64_t dst_cap, uint64_t* block_off, uint32_t* block_len,
                              uint64_t* bytes_used, int n_threads);
+
+/* ---- blockiter.Data over one decoded block (host side) ----
+ * The adapter a Go shim exposes behind sstable/blockiter
+ * (sstable/blockiter/block_iter.go:19-108): rowblk.Iter / colblk.DataBlockIter
+ * positioning over the arrays of a decoded batch COPIED TO HOST MEMORY (every
+ * pointer of `host` is a host pointer; nothing here touches the device).  A
+ * positioning call returns the KV it lands on or NULL (exhausted); the pbl_kv
+ * it points to lives in the iterator and is valid until the next call. */
+#define PBL_CMP_DEFAULT 0u  /* base.DefaultComparer: bytes.Compare, Split = len   */
+#define PBL_CMP_TESTKEYS 1u /* testkeys.Comparer (internal/testkeys/testkeys.go)  */
+#define PBL_CMP_CRDB 2u     /* cockroachkvs.Comparer (cockroachkvs/cockroachkvs.go) */
+
+typedef struct pbl_kv {   /* base.InternalKV over the decoded arrays (block/kv.go) */
+  const uint8_t* user_key;
+  uint64_t user_key_len;
+  uint64_t trailer;       /* InternalKeyTrailer, as decoded (transforms applied) */
+  const uint8_t* value;   /* in-place value bytes, or the handle bytes          */
+  uint64_t value_len;
+  uint32_t kv_flags;      /* PBL_KV_*                                          */
+  uint32_t reserved;
+} pbl_kv;
+
+typedef struct pbl_data_iter pbl_data_iter;
+pbl_data_iter* pbl_data_iter_new(void);
+void pbl_data_iter_free(pbl_data_iter* it);
+/* InitHandle (block_iter.go:84-90) for block `block` of a decoded batch of
+ * n_blocks: PBL_OK, or the block's decode status (the iterator is then
+ * invalidated), or PBL_INVALID_ARG.  hide_obsolete_points: the
+ * HideObsoletePoints transform (KVs with PBL_KV_OBSOLETE are skipped). */
+int pbl_data_iter_init(pbl_data_iter* it, const pbl_decode_out* host, uint32_t n_blocks, uint32_t block,
+                       uint32_t comparer, uint32_t hide_obsolete_points);
+const pbl_kv* pbl_data_iter_first(pbl_data_iter* it);
+const pbl_kv* pbl_data_iter_last(pbl_data_iter* it);
+const pbl_kv* pbl_data_iter_next(pbl_data_iter* it);
+const pbl_kv* pbl_data_iter_prev(pbl_data_iter* it);
+const pbl_kv* pbl_data_iter_seek_ge(pbl_data_iter* it, const uint8_t* key, uint64_t key_len, uint32_t flags);
+const pbl_kv* pbl_data_iter_seek_lt(pbl_data_iter* it, const uint8_t* key, uint64_t key_len, uint32_t flags);
+/* (kv, 0) same prefix; (NULL, 1) positioned at a KV of another prefix; (NULL, 0) none */
+const pbl_kv* pbl_data_iter_seek_prefix_ge(pbl_data_iter* it, const uint8_t* key, uint64_t key_len, uint32_t flags,
+                                           int* prefix_did_not_match);
+const pbl_kv* pbl_data_iter_next_with_same_prefix(pbl_data_iter* it, int* prefix_exhausted);
+const pbl_kv* pbl_data_iter_next_prefix(pbl_data_iter* it, const uint8_t* succ_key, uint64_t succ_len);
+int pbl_data_iter_is_lower_bound(const pbl_data_iter* it, const uint8_t* key, uint64_t key_len);
+int pbl_data_iter_valid(const pbl_data_iter* it);
+const pbl_kv* pbl_data_iter_kv(pbl_data_iter* it);
+void pbl_data_iter_invalidate(pbl_data_iter* it);
+int pbl_data_iter_is_data_invalidated(const pbl_data_iter* it);
+/* the comparers themselves (Compare < 0 / 0 / > 0, Split) */
+int pbl_key_compare(uint32_t comparer, const uint8_t* a, uint64_t a_len, const uint8_t* b, uint64_t b_len);
+uint64_t pbl_key_split(uint32_t comparer, const uint8_t* key, uint64_t key_len);
 
 #ifdef __cplusplus
 }

@@ -42,7 +42,7 @@ PBL_TABLE_PEBBLEV5, PBL_TABLE_PEBBLEV6, PBL_TABLE_PEBBLEV7 = 7, 8, 9
 PBL_CHECKSUM_NONE, PBL_CHECKSUM_CRC32C, PBL_CHECKSUM_XXHASH, PBL_CHECKSUM_XXHASH64 = 0, 1, 2, 3
 PBL_COMPRESSION_NONE, PBL_COMPRESSION_SNAPPY, PBL_COMPRESSION_ZSTD, PBL_COMPRESSION_MINLZ = 0, 1, 7, 8
 
-ABI_VERSION = 6  # include/pebble_amd.h PBL_ABI_VERSION
+ABI_VERSION = 7  # include/pebble_amd.h PBL_ABI_VERSION
 
 PBL_FMT_ROW = 0
 PBL_FMT_COL_DEFAULT = 1
@@ -159,8 +159,39 @@ class TransformsC(ctypes.Structure):
     ]
 
 
+class KvC(ctypes.Structure):  # pbl_kv (base.InternalKV over the decoded arrays)
+    _fields_ = [("user_key", _vp), ("user_key_len", ctypes.c_uint64), ("trailer", ctypes.c_uint64),
+                ("value", _vp), ("value_len", ctypes.c_uint64), ("kv_flags", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
+PBL_CMP_DEFAULT, PBL_CMP_TESTKEYS, PBL_CMP_CRDB = 0, 1, 2
+_kvp = ctypes.POINTER(KvC)
+_u8p = ctypes.c_char_p
+
 # Every symbol include/pebble_amd.h declares, with its ctypes signature.
 SIGNATURES = {
+    "pbl_data_iter_new": (_vp, []),
+    "pbl_data_iter_free": (None, [_vp]),
+    "pbl_data_iter_init": (ctypes.c_int, [_vp, ctypes.POINTER(DecodeOutC), ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.c_uint32, ctypes.c_uint32]),
+    "pbl_data_iter_first": (_kvp, [_vp]),
+    "pbl_data_iter_last": (_kvp, [_vp]),
+    "pbl_data_iter_next": (_kvp, [_vp]),
+    "pbl_data_iter_prev": (_kvp, [_vp]),
+    "pbl_data_iter_seek_ge": (_kvp, [_vp, _u8p, ctypes.c_uint64, ctypes.c_uint32]),
+    "pbl_data_iter_seek_lt": (_kvp, [_vp, _u8p, ctypes.c_uint64, ctypes.c_uint32]),
+    "pbl_data_iter_seek_prefix_ge": (_kvp, [_vp, _u8p, ctypes.c_uint64, ctypes.c_uint32,
+                                            ctypes.POINTER(ctypes.c_int)]),
+    "pbl_data_iter_next_with_same_prefix": (_kvp, [_vp, ctypes.POINTER(ctypes.c_int)]),
+    "pbl_data_iter_next_prefix": (_kvp, [_vp, _u8p, ctypes.c_uint64]),
+    "pbl_data_iter_is_lower_bound": (ctypes.c_int, [_vp, _u8p, ctypes.c_uint64]),
+    "pbl_data_iter_valid": (ctypes.c_int, [_vp]),
+    "pbl_data_iter_kv": (_kvp, [_vp]),
+    "pbl_data_iter_invalidate": (None, [_vp]),
+    "pbl_data_iter_is_data_invalidated": (ctypes.c_int, [_vp]),
+    "pbl_key_compare": (ctypes.c_int, [ctypes.c_uint32, _u8p, ctypes.c_uint64, _u8p, ctypes.c_uint64]),
+    "pbl_key_split": (ctypes.c_uint64, [ctypes.c_uint32, _u8p, ctypes.c_uint64]),
     "pbl_abi_version": (ctypes.c_int, []),
     "pbl_workspace_bytes": (ctypes.c_uint64, [ctypes.c_uint32]),
     "pbl_decode_batch": (ctypes.c_int, [ctypes.POINTER(BlockBatchC), ctypes.POINTER(DecodeOutC), _vp]),

@@ -1341,7 +1341,9 @@ size_t pbl_struct_layout(uint64_t* out, size_t cap) {
       PBL_OFF(pbl_kv_out, val_len), PBL_OFF(pbl_kv_out, blk_base), PBL_OFF(pbl_kv_out, blk_status),
       PBL_OFF(pbl_kv_out, cap),
       sizeof(pbl_value_out), PBL_OFF(pbl_value_out, val_off), PBL_OFF(pbl_value_out, val_bytes),
-      PBL_OFF(pbl_value_out, blk_val_base), PBL_OFF(pbl_value_out, blk_status), PBL_OFF(pbl_value_out, val_cap)};
+      PBL_OFF(pbl_value_out, blk_val_base), PBL_OFF(pbl_value_out, blk_status), PBL_OFF(pbl_value_out, val_cap),
+      sizeof(pbl_kv), PBL_OFF(pbl_kv, user_key), PBL_OFF(pbl_kv, user_key_len), PBL_OFF(pbl_kv, trailer),
+      PBL_OFF(pbl_kv, value), PBL_OFF(pbl_kv, value_len), PBL_OFF(pbl_kv, kv_flags), PBL_OFF(pbl_kv, reserved)};
 #undef PBL_OFF
   const size_t n = sizeof(v) / sizeof(v[0]);
   for (size_t i = 0; i < n && i < cap && out; i++) out[i] = v[i];

@@ -335,7 +335,7 @@ __device__ bool sn_decode(Snap2Lds& S, uint32_t ib, uint32_t n, uint32_t used, u
 // output offset with one LDS round trip, so the copy-chain pointer jumping
 // (sn_resolve's scheme) runs with each lane's copies in registers.  20 KB of
 // LDS: 8 blocks per CU.
-constexpr uint32_t kS4In = 32768, kS4Span = 32768, kS4Q = 768, kS4Slots = kS4Q / kWave;
+constexpr uint32_t kS4In = 36864, kS4Span = 32768, kS4Q = 768, kS4Slots = kS4Q / kWave;
 struct Snap4Lds {
   uint64_t q[kS4Q];           // dst | len << 16 | (src or offset) << 32 | copy << 63
   uint32_t r[kS4Q];           // copies: where their bytes are (kSnRes / kSnStop / output offset)
@@ -344,6 +344,10 @@ struct Snap4Lds {
   uint16_t pf[kS4Span / 64];  // element starts before each 64-bit word of ob
   uint16_t cl[kS4Q];          // the round's copies, in order
 };
+// (kS4In past 32 KiB: an incompressible 32 KiB block's snappy form is a few
+// bytes longer than the block; at 32 KiB such blocks fell to the one-lane
+// global-memory decoder, 1/256 of a text batch's blocks taking 80 % of its time)
+static_assert(8 * sizeof(Snap4Lds) <= 163840, "8 blocks per CU");
 __device__ __forceinline__ bool sn4_walkable(uint32_t n, uint32_t D) {
   return n >= 8 && n <= kS4In && D >= kSnWalkMin && D <= kS4Span && D >= 16 + 4 * ((n + 31) / 32);
 }

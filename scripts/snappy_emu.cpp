@@ -82,11 +82,11 @@ int main(int argc, char** argv) {
     if (in[i] < 0x80) { used = i + 1; break; }
   }
   static pbl::phys::Snap2Lds S;
-  if (n > pbl::phys::kSnIn || D > 0xffff) return 3;
-  std::memcpy(S.in, in.data(), n);
-  std::vector<uint8_t> out(D + 64);
   // snappy_walk_kernel's lane for this block, then snappy4's decode (or snappy2's)
   const bool walked = pbl::phys::sn4_walkable(uint32_t(n), uint32_t(D)) && !getenv("EMU_NO_WALK");
+  if ((!walked && n > pbl::phys::kSnIn) || D > 0xffff) return 3;
+  if (!walked) std::memcpy(S.in, in.data(), n);
+  std::vector<uint8_t> out(D + 64);
   if (walked) pbl::phys::sn4_walk(in.data(), uint32_t(n), used, uint32_t(D), out.data());
   static pbl::phys::Snap4Lds S4;
   std::barrier<> bar(64);

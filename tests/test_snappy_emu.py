@@ -47,7 +47,8 @@ def test_emulated_snappy_decoder_matches_oracle(emu, tmp_path):
     rng = random.Random(3)
     words = [rng.randbytes(rng.randrange(1, 10)) for _ in range(300)]
     text = b" ".join(rng.choice(words) for _ in range(6000))[:30000]
-    for data in [bytes(buf[int(off[0]):int(off[0]) + int(lens[0])]), text, b"ab" * 9000, rng.randbytes(20000)]:
+    for data in [bytes(buf[int(off[0]):int(off[0]) + int(lens[0])]), text, b"ab" * 9000, rng.randbytes(20000),
+                 rng.randbytes(32768)]:  # (the last one compresses to more than 32 KiB)
         raw = pa.Codec("snappy").compress(data, asbytes=True)
         assert run(emu, tmp_path, raw) == data
 
