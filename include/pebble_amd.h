@@ -96,6 +96,9 @@ enum {
 #define PBL_KERNEL_RUN 0x1000u    /* A/B measurement, no effect on results: row
                                      batches on the run-major one-wave-per-block
                                      kernel (rowblk_run.hip.h)                      */
+#define PBL_KERNEL_GLOBAL 0x2000u /* A/B measurement, no effect on results: row
+                                     batches walked from HBM by a wave per block in
+                                     three launches (rowblk_global.hip.h)           */
 
 /* per-KV flag byte (kv_flags[]) */
 #define PBL_KV_RESTART 0x01u       /* entry offset is a restart point            */

@@ -801,6 +801,7 @@ __global__ void __launch_bounds__(kTPB, 3) rowblk_decode_kernel(Args A) {
 #include "rowblk_pipe.hip.h"
 #include "rowblk_flat.hip.h"
 #include "rowblk_run.hip.h"
+#include "rowblk_global.hip.h"
 
 // Mixed row + colblk batch (config 4): per-block format from block_format[];
 // both paths share the ticket order and the look-back state.
@@ -1137,6 +1138,29 @@ int launch_row_run(const pbl::Args& a, hipStream_t st, bool values) {
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }
 
+// Row batches walked from HBM (rowblk_global.hip.h): sizes, the 32 KiB-key
+// sizes, the tile scan, then (values) the outputs.
+int launch_row_global(const pbl::Args& a, hipStream_t st, bool values) {
+  const uint32_t nb = a.in.n_blocks;
+  int dev = 0, cus = 0;
+  if (hipStreamGetDevice(st, &dev) != hipSuccess && hipGetDevice(&dev) != hipSuccess) return PBL_DEVICE_ERROR;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    return PBL_DEVICE_ERROR;
+  // (the size walk takes 35 VGPRs: 8 waves per SIMD; the values walk 117: 4)
+  const uint32_t walk = uint32_t(std::min<uint64_t>(nb, uint64_t(cus) * 32));
+  const uint32_t vwalk = uint32_t(std::min<uint64_t>(nb, uint64_t(cus) * 4 * PBL_GLB_WAVES));
+  const uint32_t small = uint32_t(std::min<uint64_t>((uint64_t(nb) + pbl::kWave - 1) / pbl::kWave, uint64_t(cus) * 4));
+  const uint32_t tiles = uint32_t(std::min<uint64_t>(pbl::row::glb::glb_tiles(nb), uint64_t(cus)));
+  hipLaunchKernelGGL(pbl::row::glb::glb_sizes_kernel, dim3(walk), dim3(pbl::kWave), 0, st, a);
+  hipLaunchKernelGGL(pbl::row::glb::glb_sizes_big_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+  hipLaunchKernelGGL(pbl::row::glb::glb_scan_kernel, dim3(tiles), dim3(pbl::kTPB), 0, st, a);
+  if (values) {
+    hipLaunchKernelGGL(pbl::row::glb::glb_values_kernel, dim3(vwalk), dim3(pbl::kWave), 0, st, a);
+    hipLaunchKernelGGL(pbl::row::glb::glb_values_big_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+  }
+  return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
+}
+
 // Mixed batches: PBL_KERNEL_SINGLE keeps the one-block-per-workgroup kernel
 // (A/B); the default splits the ids by format and runs the mixed pipeline,
 // with the big row blocks' size / value passes around it.
@@ -1219,6 +1243,7 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
     // blocks).  PBL_KERNEL_SINGLE selects the one-block-per-workgroup
     // persistent kernel (kept for A/B measurement); the default is the pipeline.
     const bool single = (batch->flags & PBL_KERNEL_SINGLE) != 0;
+    if (!single && (batch->flags & PBL_KERNEL_GLOBAL)) return launch_row_global(a, st, true);
     if (!single && (batch->flags & PBL_KERNEL_RUN)) return launch_row_run(a, st, true);
     if (!single && use_flat(batch->flags)) return launch_row_flat(a, st, true);
     const void* fn = single ? reinterpret_cast<const void*>(pbl::row::rowblk_decode_kernel)
@@ -1282,6 +1307,9 @@ int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stre
     // pointers), minus the big-block value pass
     if (batch->block_format) {
       rc = launch_mixed(batch, a, st, batch->flags & PBL_KERNEL_SINGLE, false);
+      if (rc != PBL_OK) return rc;
+    } else if (batch->flags & PBL_KERNEL_GLOBAL) {
+      rc = launch_row_global(a, st, false);
       if (rc != PBL_OK) return rc;
     } else if (batch->flags & PBL_KERNEL_RUN) {
       rc = launch_row_run(a, st, false);

@@ -115,9 +115,14 @@ __device__ __forceinline__ void slow_walk_t(const Src S, uint64_t len, uint32_t 
   int64_t offset = 0;
   uint32_t ri = 0;
   uint32_t status = PBL_OK;
+  // the next entry's header window is loaded before this entry's stores: a
+  // load's data waits for every older vector-memory op, so a header read
+  // behind the value stores would wait for all of them (config 5's values walk:
+  // see rowblk_global.hip.h)
+  uint4 hw_next = restarts > 0 ? S.ld16(0) : make_uint4(0, 0, 0, 0);
   while (offset >= 0 && offset < restarts) {
     // the header's bytes in one window, the three varints from registers
-    const uint4 hw = S.ld16(offset);
+    const uint4 hw = hw_next;
     const uint32_t hn = uint32_t(min<int64_t>(15, int64_t(len) - offset));
     uint32_t shared, unshared, vlen;
     const uint32_t a = w_varint(hw, 0, hn, &shared);
@@ -131,6 +136,7 @@ __device__ __forceinline__ void slow_walk_t(const Src S, uint64_t len, uint32_t 
     if (shared > full_len) { status = PBL_CORRUPT_BOUNDS; break; }
     const uint64_t klen = uint64_t(shared) + unshared;
     if (klen > keycap) { status = PBL_UNSUPPORTED; break; }
+    if (int64_t(vp + vlen) < restarts) hw_next = S.ld16(int64_t(vp + vlen));
     wave_sync();
     // unshared key bytes -> keybuf[shared, klen): one 16-B window per lane step
     for (uint32_t i0 = 16u * l; i0 < unshared; i0 += 16u * kWave) {
