@@ -64,15 +64,6 @@ using flat::dpp_incl_scan;
 using flat::last_lane;
 using flat::store_n;
 
-// Bytes [0, n) of the 32-B register key k to p (n <= 32).
-__device__ __forceinline__ void store_key(gptr<uint8_t> p, const uint64_t k[4], uint32_t n) {
-  if (n == 0) return;
-  const uint32_t n0 = n < 16 ? n : 16u;
-  store_n(p, make_uint4(uint32_t(k[0]), uint32_t(k[0] >> 32), uint32_t(k[1]), uint32_t(k[1] >> 32)), n0);
-  if (n > 16)
-    store_n(p + 16, make_uint4(uint32_t(k[2]), uint32_t(k[2] >> 32), uint32_t(k[3]), uint32_t(k[3] >> 32)), n - 16);
-}
-
 // LE64 of register-key bytes [o, o + 8), o <= 24.
 __device__ __forceinline__ uint64_t key_u64(const uint64_t k[4], uint32_t o) {
   const uint32_t w = o >> 3, s = (o & 7u) * 8u;
@@ -236,7 +227,6 @@ __device__ __forceinline__ void long_values(const View& V, uint32_t r0, uint32_t
   const uint32_t l = lane_id();
   const bool rawk = (flags & PBL_ROW_RAW_KEYS) != 0;
   uint32_t pos = V.le32(roff + 4 * r0) & kRestartMask, rend = run_end(V, r0, nres, roff), r = r0;
-  uint64_t k[4] = {0, 0, 0, 0};
   for (;;) {
     if (pos == rend) {
       if (++r >= r1) break;
@@ -254,7 +244,6 @@ __device__ __forceinline__ void long_values(const View& V, uint32_t r0, uint32_t
         if ((pre & 0xC0) == 0 || (flags & PBL_ROW_NO_VALUER)) { vs++; vlen--; }
       }
     }
-    (void)k;
     if (vlen > kRLongVal)
       for (uint32_t c = 16u * l; c < vlen; c += 16u * kWave) {
         const uint32_t n = vlen - c < 16 ? vlen - c : 16u;
