@@ -271,12 +271,13 @@ def main():
         buf, off, lens, n_kv = gen_zipf_blocks(seed, nb, fmt, a.restart_interval, a.block_size, n_threads=16)
         from pebble_amd.batch import varlen_hint
         # (a Zipf colblk batch carries PBL_BATCH_VARLEN: one-block-per-workgroup kernel)
-        # (a VARLEN row batch takes the flat kernel, a VARLEN colblk batch the
-        # one-block-per-workgroup kernel, unless --kernel pipe)
+        # (a VARLEN row batch is walked from HBM, a VARLEN colblk batch takes the
+        # one-block-per-workgroup kernel, unless --kernel names another)
         vl = varlen_hint(lens) and a.kernel not in ("pipe", "single")
-        kernel = (("glb_sizes_kernel+glb_scan_kernel+glb_values_kernel" if a.kernel == "global" else
+        kernel = (("glb_sizes_kernel+glb_scan_kernel+glb_values_kernel" if a.kernel == "global" or
+                   (vl and a.kernel == "auto") else
                    "rowblk_run_kernel" if a.kernel == "run" else
-                   "rowblk_flat_kernel" if vl or a.kernel == "flat" else
+                   "rowblk_flat_kernel" if a.kernel == "flat" else
                    "rowblk_decode_kernel" if a.kernel == "single" else "rowblk_pipe_kernel") if fmt == N.PBL_FMT_ROW
                   else "colblk_decode_kernel" if vl or a.kernel == "single" else "colblk_pipe_kernel")
         wl = (f"config5: {nb} variable-length blocks per GPU targeting {a.block_size // 1024} KiB, "

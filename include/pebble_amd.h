@@ -81,8 +81,8 @@ enum {
                                      lengths vary widely (e.g. Zipf value sizes), so a
                                      colblk batch takes the one-block-per-workgroup
                                      kernel, whose look-back does not convoy behind
-                                     long blocks, and a row batch the one-wave-per-
-                                     block kernel (config 5: 1.1-1.5x the pipeline).
+                                     long blocks, and a row batch is walked from HBM
+                                     by a wave per block (rowblk_global.hip.h).
                                      The caller knows the lengths on the host
                                      (block handles carry them).                   */
 #define PBL_KERNEL_SINGLE 0x200u  /* A/B measurement, no effect on results: the

@@ -1099,8 +1099,14 @@ namespace {
 // block lengths vary widely (PBL_BATCH_VARLEN, unless PBL_KERNEL_PIPE): on
 // config 5 it measured 542 / 499 / 619 GiB/s against the pipeline's 495 / 340 /
 // 598 at restart intervals 16 / 32 / 1 (profiles/r03/zipf_ab_*.json).
-bool use_flat(uint32_t flags) {
-  return (flags & PBL_KERNEL_FLAT) || ((flags & PBL_BATCH_VARLEN) && !(flags & PBL_KERNEL_PIPE));
+bool use_flat(uint32_t flags) { return (flags & PBL_KERNEL_FLAT) != 0; }
+// VARLEN row batches (unless an A/B flag names a kernel) are walked from HBM
+// (rowblk_global.hip.h): config 5 574 / 584 / 551 GiB/s at restart intervals
+// 16 / 32 / 1 against the flat kernel's 541 / 499 / 614
+// (profiles/r03_final/ab_zipf_global_*.json, bench_zipf_ri*.json).
+bool use_global(uint32_t flags) {
+  return (flags & PBL_KERNEL_GLOBAL) ||
+         ((flags & PBL_BATCH_VARLEN) && !(flags & (PBL_KERNEL_PIPE | PBL_KERNEL_FLAT | PBL_KERNEL_RUN)));
 }
 
 // Row batches on the flat kernel (rowblk_flat.hip.h): blocks past its length
@@ -1243,7 +1249,7 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
     // blocks).  PBL_KERNEL_SINGLE selects the one-block-per-workgroup
     // persistent kernel (kept for A/B measurement); the default is the pipeline.
     const bool single = (batch->flags & PBL_KERNEL_SINGLE) != 0;
-    if (!single && (batch->flags & PBL_KERNEL_GLOBAL)) return launch_row_global(a, st, true);
+    if (!single && use_global(batch->flags)) return launch_row_global(a, st, true);
     if (!single && (batch->flags & PBL_KERNEL_RUN)) return launch_row_run(a, st, true);
     if (!single && use_flat(batch->flags)) return launch_row_flat(a, st, true);
     const void* fn = single ? reinterpret_cast<const void*>(pbl::row::rowblk_decode_kernel)
@@ -1308,7 +1314,7 @@ int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stre
     if (batch->block_format) {
       rc = launch_mixed(batch, a, st, batch->flags & PBL_KERNEL_SINGLE, false);
       if (rc != PBL_OK) return rc;
-    } else if (batch->flags & PBL_KERNEL_GLOBAL) {
+    } else if (use_global(batch->flags)) {
       rc = launch_row_global(a, st, false);
       if (rc != PBL_OK) return rc;
     } else if (batch->flags & PBL_KERNEL_RUN) {

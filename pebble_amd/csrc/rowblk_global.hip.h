@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(kTPB) glb_scan_kernel(Args A) {
           to_glb(O.key_off)[e[0] + b] = 0;
           to_glb(O.val_off)[e[0] + b] = 0;
         }
-        write_block_meta(O, b, nb, st, e, c[k], false);
+        write_block_meta(O, b, nb, st, e, c[k], true);  // (every block takes the general walk: n_slow_blocks)
 #pragma unroll
         for (int q = 0; q < kNumComp; q++) e[q] += c[k][q];
       }
