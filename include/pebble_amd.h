@@ -99,6 +99,9 @@ enum {
 #define PBL_KERNEL_GLOBAL 0x2000u /* A/B measurement, no effect on results: row
                                      batches walked from HBM by a wave per block in
                                      three launches (rowblk_global.hip.h)           */
+#define PBL_KERNEL_POOL 0x4000u   /* A/B measurement, no effect on results: row
+                                     batches on the staging-pool kernel
+                                     (rowblk_pool.hip.h)                            */
 
 /* per-KV flag byte (kv_flags[]) */
 #define PBL_KV_RESTART 0x01u       /* entry offset is a restart point            */
@@ -270,9 +273,11 @@ int pbl_verify_checksums(const pbl_phys_batch* batch, uint32_t checksum_type, ui
                          void* stream);
 /*
  * Decompressor.DecompressedLen (block.go:549-556) of every block: out_len[b];
- * status[b] = PBL_OK, PBL_CORRUPT_COMPRESSION or PBL_UNSUPPORTED (minlz and the
- * legacy codecs are not decoded on the device).  Snappy: its uvarint header;
- * zstd: the uvarint Pebble prefixes (zstd_cgo.go:111-119).
+ * status[b] = PBL_OK, PBL_CORRUPT_COMPRESSION or PBL_UNSUPPORTED (the legacy
+ * codecs are not decoded on the device).  Snappy: its uvarint header; zstd: the
+ * uvarint Pebble prefixes (zstd_cgo.go:111-119); MinLZ: minlz.DecodedLen
+ * (internal/compression/minlz.go:70-73; a block in the Snappy form, first byte
+ * not 0, by its Snappy header).
  */
 int pbl_decompressed_lengths(const pbl_phys_batch* batch, uint32_t* out_len, uint32_t* status, void* stream);
 /*

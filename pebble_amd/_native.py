@@ -57,6 +57,7 @@ PBL_KERNEL_PIPE = 0x400
 PBL_KERNEL_FLAT = 0x800
 PBL_KERNEL_RUN = 0x1000
 PBL_KERNEL_GLOBAL = 0x2000
+PBL_KERNEL_POOL = 0x4000
 
 PBL_KV_RESTART = 0x01
 PBL_KV_RESTART_SAMEPFX = 0x02

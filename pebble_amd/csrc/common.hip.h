@@ -485,7 +485,7 @@ __device__ inline bool overflows(const pbl_decode_out& O, const uint64_t excl[kN
 // immutable once written; racing first calls store the same values).
 enum PersistentKernel {
   kKRowPipe = 0, kKRowSingle = 1, kKColPipe = 2, kKMixedPipe = 3, kKMixedColSize = 4, kKMixedRow = 5, kKMixedCol = 6,
-  kKRowFlat = 7, kKRowRun = 8, kKNum = 9
+  kKRowFlat = 7, kKRowRun = 8, kKRowPool = 9, kKNum = 10
 };
 
 // Resident grid for `fn` on the stream's device (never more than n_units, at

@@ -29,7 +29,10 @@
 //   snappy_kernel         (PBL_SNAPPY_VER 1 A/B) the first form: input and output
 //                         staged in LDS, the wave copies one element at a time
 //   zstd_kernel           (zstd.hip) the blocks whose indicator is zstd
-// MinLZ (indicator 8) and unknown indicators report PBL_UNSUPPORTED.
+//   minlz_kernel          (minlz_dec.hip.h) MinLZ blocks in the MinLZ form; a
+//                         MinLZ-indicated block in the Snappy form (first byte
+//                         not 0: minlz_test.go:31-36) takes the snappy kernels
+// Unknown indicators report PBL_UNSUPPORTED.
 #include <algorithm>
 
 #include "common.hip.h"
@@ -262,15 +265,51 @@ __device__ inline bool uvarint32(gptr<const uint8_t> p, uint64_t n, uint32_t* v,
   return false;
 }
 
+// ---- MinLZ (minlz_dec.hip.h decodes the MinLZ form) ------------------------------
+constexpr uint32_t kMinlzMaxBlock = 8u << 20;  // minlz.MaxBlockSize
+
+// The MinLZ form's header (src[0] == 0): decoded length, header bytes, stored.
+// False on a corrupt header (minlz.DecodedLen's errors).
+__device__ inline bool minlz_header(gptr<const uint8_t> p, uint32_t n, uint32_t* dlen, uint32_t* hdr, bool* stored) {
+  *stored = false;
+  if (n == 1) {  // the empty block
+    *dlen = 0;
+    *hdr = 1;
+    return true;
+  }
+  uint32_t v = 0, u = 0;
+  if (!uvarint32(p + 1, n - 1, &v, &u) || v > kMinlzMaxBlock) return false;
+  const uint32_t rest = n - 1 - u;
+  if (rest == 0) return false;
+  *hdr = 1 + u;
+  if (v == 0) {
+    *stored = true;
+    *dlen = rest;
+    return true;
+  }
+  if (v < rest) return false;  // a compressed block is never longer than its output
+  *dlen = v;
+  return true;
+}
+
+// Whether a block with indicator `ind` is decoded by the snappy kernels:
+// snappy blocks, and MinLZ-indicated blocks in the Snappy form.
+__device__ __forceinline__ bool snappy_form(uint32_t ind, gptr<const uint8_t> p, uint32_t n) {
+  return ind == PBL_COMPRESSION_SNAPPY || (ind == PBL_COMPRESSION_MINLZ && n > 0 && p[0] != 0);
+}
+
 __global__ void __launch_bounds__(kTPB) snappy_len_kernel(const pbl_phys_batch B, uint32_t* out_len, uint32_t* status) {
   for (uint32_t b = blockIdx.x * kTPB + threadIdx.x; b < B.n_blocks; b += gridDim.x * kTPB) {
     const uint32_t n = B.block_len[b];
     const gptr<const uint8_t> p = to_glb(B.bytes + B.block_off[b]);
     const uint32_t ind = p[n];
     uint32_t st = PBL_OK, len = 0, used = 0;
+    bool stored = false;
     if (ind == PBL_COMPRESSION_NONE) len = n;
-    else if (ind == PBL_COMPRESSION_SNAPPY || ind == PBL_COMPRESSION_ZSTD)  // (zstd_cgo.go:111-119)
+    else if (snappy_form(ind, p, n) || ind == PBL_COMPRESSION_ZSTD)  // (zstd_cgo.go:111-119)
       st = uvarint32(p, n, &len, &used) ? PBL_OK : PBL_CORRUPT_COMPRESSION;
+    else if (ind == PBL_COMPRESSION_MINLZ)  // minlz.DecodedLen
+      st = n > 0 && minlz_header(p, n, &len, &used, &stored) ? PBL_OK : PBL_CORRUPT_COMPRESSION;
     else st = PBL_UNSUPPORTED;
     out_len[b] = st == PBL_OK ? len : 0u;
     status[b] = st;
@@ -317,6 +356,8 @@ struct GlbBytesW {
   __device__ uint8_t get(uint32_t i) const { return p[i]; }
   __device__ void set(uint32_t i, uint8_t v) const { p[i] = v; }
 };
+
+#include "minlz_dec.hip.h"
 
 // Decode one snappy block.  Lane 0 reads element headers; the wave copies.
 // Returns the decoded length, or ~0u when the input is corrupt.
@@ -529,7 +570,7 @@ __global__ void __launch_bounds__(kTPB) snappy_walk_kernel(const pbl_phys_batch 
   if (b >= B.n_blocks) return;
   const uint32_t n = to_glb(B.block_len)[b];
   const gptr<const uint8_t> src = to_glb(B.bytes + to_glb(B.block_off)[b]);
-  if (src[n] != PBL_COMPRESSION_SNAPPY) return;
+  if (!snappy_form(src[n], src, n)) return;
   uint32_t dl = 0, used = 0;
   if (!uvarint32(src, n, &dl, &used) || dl > to_glb(out_cap)[b] || !sn4_walkable(n, dl)) return;
   sn4_walk(src, n, used, dl, to_glb(out + to_glb(out_off)[b]));
@@ -542,7 +583,7 @@ __global__ void __launch_bounds__(kWave) snappy4_kernel(const pbl_phys_batch B, 
   for (uint32_t b = blockIdx.x; b < B.n_blocks; b += gridDim.x) {
     const uint32_t n = to_glb(B.block_len)[b];
     const gptr<const uint8_t> src = to_glb(B.bytes + to_glb(B.block_off)[b]);
-    if (src[n] != PBL_COMPRESSION_SNAPPY) continue;
+    if (!snappy_form(src[n], src, n)) continue;
     uint32_t dl = 0, used = 0;
     if (!uvarint32(src, n, &dl, &used) || dl > to_glb(out_cap)[b] || !sn4_walkable(n, dl)) continue;
     const bool ok = sn4_decode(S, src, n, dl, to_glb(out + to_glb(out_off)[b]), b);
@@ -564,6 +605,7 @@ __global__ void __launch_bounds__(kWave) snappy2_kernel(const pbl_phys_batch B, 
     const gptr<const uint8_t> src = to_glb(B.bytes + boff);
     const uint32_t ind = src[n];
     if (ind == PBL_COMPRESSION_ZSTD) continue;  // zstd_kernel's
+    if (ind == PBL_COMPRESSION_MINLZ && !snappy_form(ind, src, n)) continue;  // minlz_kernel's
     gptr<uint8_t> dst = to_glb(out + to_glb(out_off)[b]);
     const uint32_t cap = to_glb(out_cap)[b];
     uint32_t st = PBL_OK, len = 0;
@@ -578,7 +620,7 @@ __global__ void __launch_bounds__(kWave) snappy2_kernel(const pbl_phys_batch B, 
         for (uint32_t c = nf + lane; c < n; c += kWave) dst[c] = src[c];
       }
       len = n;
-    } else if (ind == PBL_COMPRESSION_SNAPPY) {
+    } else if (snappy_form(ind, src, n)) {
       uint32_t dl = 0, used = 0;
       if (!uvarint32(src, n, &dl, &used)) st = PBL_CORRUPT_COMPRESSION;
       else if (dl > cap) st = PBL_OVERFLOW;
@@ -677,6 +719,8 @@ int pbl_decompress_blocks(const pbl_phys_batch* batch, uint8_t* out, const uint6
   hipLaunchKernelGGL(pbl::phys::snappy2_kernel, dim3(grid), dim3(pbl::kWave), 0, st, *batch, out, out_off, out_cap,
                      out_len, status);
 #endif
+  hipLaunchKernelGGL(pbl::phys::minlz_kernel, dim3(std::min<uint32_t>(batch->n_blocks, 2048)), dim3(pbl::kWave), 0, st,
+                     *batch, out, out_off, out_cap, out_len, status);
   if (hipGetLastError() != hipSuccess) return PBL_DEVICE_ERROR;
   return pbl::launch_zstd(*batch, out, out_off, out_cap, out_len, status, st) == hipSuccess ? PBL_OK
                                                                                               : PBL_DEVICE_ERROR;

@@ -800,6 +800,7 @@ __global__ void __launch_bounds__(kTPB, 3) rowblk_decode_kernel(Args A) {
 
 #include "rowblk_pipe.hip.h"
 #include "rowblk_flat.hip.h"
+#include "rowblk_pool.hip.h"
 #include "rowblk_run.hip.h"
 #include "rowblk_global.hip.h"
 
@@ -1106,7 +1107,7 @@ bool use_flat(uint32_t flags) { return (flags & PBL_KERNEL_FLAT) != 0; }
 // (profiles/r03_final/ab_zipf_global_*.json, bench_zipf_ri*.json).
 bool use_global(uint32_t flags) {
   return (flags & PBL_KERNEL_GLOBAL) ||
-         ((flags & PBL_BATCH_VARLEN) && !(flags & (PBL_KERNEL_PIPE | PBL_KERNEL_FLAT | PBL_KERNEL_RUN)));
+         ((flags & PBL_BATCH_VARLEN) && !(flags & (PBL_KERNEL_PIPE | PBL_KERNEL_FLAT | PBL_KERNEL_RUN | PBL_KERNEL_POOL)));
 }
 
 // Row batches on the flat kernel (rowblk_flat.hip.h): blocks past its length
@@ -1123,6 +1124,23 @@ int launch_row_flat(const pbl::Args& a, hipStream_t st, bool values) {
   hipLaunchKernelGGL(pbl::row::pipe::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
   hipLaunchKernelGGL(pbl::row::flat::rowblk_flat_kernel, dim3(uint32_t(grid)), dim3(pbl::row::flat::kFTPB), 0, st,
                      a);
+  if (values) hipLaunchKernelGGL(pbl::row::pipe::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+  return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
+}
+
+// Row batches on the staging-pool kernel (rowblk_pool.hip.h), with the same
+// big-block passes around it.
+int launch_row_pool(const pbl::Args& a, hipStream_t st, bool values) {
+  const uint32_t nb = a.in.n_blocks;
+  int cus = 0;
+  const uint64_t grid = pbl::persistent_grid(st, pbl::kKRowPool,
+                                             reinterpret_cast<const void*>(pbl::row::pool::rowblk_pool_kernel),
+                                             (uint64_t(nb) + pbl::row::pool::kNW - 1) / pbl::row::pool::kNW, &cus,
+                                             pbl::row::pool::kTPBP);
+  if (!grid) return PBL_DEVICE_ERROR;
+  const uint32_t small = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4));
+  hipLaunchKernelGGL(pbl::row::pipe::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+  hipLaunchKernelGGL(pbl::row::pool::rowblk_pool_kernel, dim3(uint32_t(grid)), dim3(pbl::row::pool::kTPBP), 0, st, a);
   if (values) hipLaunchKernelGGL(pbl::row::pipe::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }
@@ -1251,6 +1269,7 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
     const bool single = (batch->flags & PBL_KERNEL_SINGLE) != 0;
     if (!single && use_global(batch->flags)) return launch_row_global(a, st, true);
     if (!single && (batch->flags & PBL_KERNEL_RUN)) return launch_row_run(a, st, true);
+    if (!single && (batch->flags & PBL_KERNEL_POOL)) return launch_row_pool(a, st, true);
     if (!single && use_flat(batch->flags)) return launch_row_flat(a, st, true);
     const void* fn = single ? reinterpret_cast<const void*>(pbl::row::rowblk_decode_kernel)
                             : reinterpret_cast<const void*>(pbl::row::pipe::rowblk_pipe_kernel);
@@ -1319,6 +1338,9 @@ int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stre
       if (rc != PBL_OK) return rc;
     } else if (batch->flags & PBL_KERNEL_RUN) {
       rc = launch_row_run(a, st, false);
+      if (rc != PBL_OK) return rc;
+    } else if (batch->flags & PBL_KERNEL_POOL) {
+      rc = launch_row_pool(a, st, false);
       if (rc != PBL_OK) return rc;
     } else if (use_flat(batch->flags)) {
       rc = launch_row_flat(a, st, false);

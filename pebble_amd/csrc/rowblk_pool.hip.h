@@ -1,0 +1,677 @@
+// rowblk_pool.hip.h — the row-format decode with one wave per block, sixteen
+// waves per CU, and a shared pool of LDS staging buffers.
+//
+// Every earlier single-pass form tied one 32 KiB LDS stage to every block in
+// flight, so at most 4-5 blocks per CU were ever in flight, each a long chain
+// of dependent LDS and HBM round trips.  Only the parse needs
+// the staged bytes; the value bytes (80 % of the output) can be copied
+// global->global from the block that was just read (L2 / MALL-hot).  So here:
+//
+//   acquire   a wave takes a free stage from the workgroup's pool (LDS mask),
+//             THEN a ticket (the only order that keeps the look-back
+//             deadlock-free: every ticket holder either holds a stage or is
+//             past needing one)
+//   stage     the block HBM -> LDS by LDS-DMA, one round trip
+//   walk      lane per restart run (rowblk_writer.go:147-155 cuts the prefix
+//             chain there): headers parked in registers, a DPP scan places the
+//             runs, the block's aggregate is published and its look-back
+//             windows requested at once
+//   meta      per-KV metadata written from the registers (key source, shared
+//             and key length, prefix parent, key output offset, entry offset,
+//             flags: in the stage; value output / source offsets and the
+//             value bucket table: in the wave's own small slot)
+//   resolve   the exclusive prefix (normally one round trip, already in flight)
+//   keys      lane per KV from the stage: offsets, trailer, flags, entry offset,
+//             the user key merged from its prefix chain; restart words
+//   release   the stage goes back to the pool
+//   values    16-B output granules per lane, each gathered from the block in
+//             GLOBAL memory (unaligned 16-B loads) through the slot's tables
+//
+// LDS per CU: 3 stages x 38 KB + 16 slots x 2.1 KB.  16 waves hold 16 blocks
+// in flight; a stage is held only from the DMA to the end of the key emit.
+//
+// Blocks outside the fast-path limits take the wave-serial general walk
+// (rowblk_general.hip.h) on the staged bytes; blocks past kMaxFastLen are sized
+// and written by big_block_{sizes,values}_kernel around this launch.  Results
+// are identical on every path.
+//
+// Semantics: cockroachdb/pebble sstable/rowblk/rowblk_iter.go — Init :241-276,
+// readFirstKey :418-485, readEntry :333-416, decodeInternalKey :487-504, value
+// prefix :1192-1199 (sstable/block/kv.go:14-41), decodeRestart :1092-1096.
+#pragma once
+
+namespace pool {
+
+#ifndef PBL_POOL_WAVES
+#define PBL_POOL_WAVES 16
+#endif
+#ifndef PBL_POOL_STAGES
+#define PBL_POOL_STAGES 3
+#endif
+#ifndef PBL_POOL_VU
+#define PBL_POOL_VU 2
+#endif
+constexpr int kNW = PBL_POOL_WAVES;      // waves per workgroup (one workgroup per CU)
+constexpr int kNS = PBL_POOL_STAGES;     // staging buffers per workgroup
+constexpr int kTPBP = kNW * kWave;
+constexpr int kPKv = 400;                // KVs per block on the fast path
+constexpr uint32_t kPKeyCap = 65535;     // user-key bytes per block on the fast path (u16 offsets)
+constexpr int kVB = 7;                   // value output bucket = 128 B
+constexpr int kVBkt = kMaxFastLen >> kVB;
+constexpr int kVU = PBL_POOL_VU;         // value granules per lane per step
+
+// A stage: the block bytes and the per-KV metadata the key emit reads.
+// m0[j] = key source offset | shared << 16 | internal key length << 32 |
+// prefix parent << 48.
+struct Stage {
+  uint4 x[kLdsBlkBytes / 16];  // the block, byte i at kPad + (boff & 15) + i
+  uint64_t m0[kPKv];
+  uint16_t kout[kPKv + 1];     // user-key output offsets (block relative)
+  uint16_t eoff[kPKv];         // entry offsets (KVEncoding.Offset)
+  uint8_t kvf[kPKv];           // PBL_KV_* (OBSOLETE is added at emit time)
+};
+// A wave's slot: what the value copy needs after the stage is released.
+struct Slot {
+  uint32_t vp[kPKv + 5];       // value output offset | value source offset << 16;
+                               // entries nkv..nkv+4 hold the value total (window reads)
+  uint16_t vbkt[kVBkt];        // KV holding value output byte q * 128
+};
+struct PoolLds {
+  Stage st[kNS];
+  Slot sl[kNW];
+  uint32_t free_mask;          // bit s: stage s is free
+};
+static_assert(sizeof(PoolLds) <= 163840, "one pool workgroup per CU");
+
+__device__ __forceinline__ uint32_t m_ksrc(uint64_t m) { return uint32_t(m) & 0xffffu; }
+__device__ __forceinline__ uint32_t m_sh(uint64_t m) { return uint32_t(m >> 16) & 0xffffu; }
+__device__ __forceinline__ uint32_t m_klen(uint64_t m) { return uint32_t(m >> 32) & 0xffffu; }
+__device__ __forceinline__ uint32_t m_par(uint64_t m) { return uint32_t(m >> 48); }
+
+typedef u32x4 u32x4_ug __attribute__((aligned(1)));
+typedef uint32_t u32_ug __attribute__((aligned(1)));
+typedef uint64_t u64_ug __attribute__((aligned(1)));
+typedef uint16_t u16_ug __attribute__((aligned(1)));
+
+// Inclusive wave scan by DPP row shifts and row broadcasts (no ds_bpermute).
+__device__ __forceinline__ uint32_t dpp_incl_scan(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+__device__ __forceinline__ uint32_t last_lane(uint32_t v) { return __builtin_amdgcn_readlane(v, kWave - 1); }
+
+// Bytes [0, n) of w (n <= 16) to p, any alignment: one 16-B store when whole,
+// else the fewest 8/4/2/1-B stores (nothing past n: the next key belongs to
+// another lane).
+__device__ __forceinline__ void store_n(gptr<uint8_t> p, const uint4& w, uint32_t n) {
+  if (n == 16) {
+    *(gptr<u32x4_ug>)p = u32x4{w.x, w.y, w.z, w.w};
+    return;
+  }
+  uint64_t lo = uint64_t(w.x) | uint64_t(w.y) << 32, hi = uint64_t(w.z) | uint64_t(w.w) << 32;
+  uint32_t o = 0;
+  if (n & 8) {
+    *(gptr<u64_ug>)p = lo;
+    lo = hi;
+    o = 8;
+  }
+  if (n & 4) {
+    *(gptr<u32_ug>)(p + o) = uint32_t(lo);
+    lo >>= 32;
+    o += 4;
+  }
+  if (n & 2) {
+    *(gptr<u16_ug>)(p + o) = uint16_t(lo);
+    lo >>= 16;
+    o += 2;
+  }
+  if (n & 1) *(p + o) = uint8_t(lo);
+}
+
+// 16 bytes of the block in global memory at block offset i (any alignment,
+// i may be up to 15 below 0 or end past the block: those bytes are
+// don't-cares).  One unaligned load inside the block's 16-B granules; at the
+// two edges the general path's aligned pair (never a byte outside them).
+__device__ __forceinline__ uint4 gld16(gptr<const uint8_t> g, int32_t i, uint32_t blen, uint32_t end16) {
+  if (i >= 0 && uint32_t(i) + 16u <= end16) {
+    const u32x4 v = *(gptr<const u32x4_ug>)(g + i);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+  return SlowGlb{g, blen}.ld16(i);
+}
+
+// Per-KV metadata of the parked entries of one run at final indices (acc = the
+// run's bases): the prefix parent is the nearest earlier entry of the run with
+// a smaller shared length (all-nearest-smaller-values, amortised O(1); the
+// previous entry and its parent kept in registers).
+__device__ __forceinline__ void park_meta(Stage& S, Slot& W, const View& V, const pipe::RunBuf& B, uint32_t flags,
+                                          bool vprefix, pipe::RunAcc& acc, pipe::ParState& P) {
+  uint32_t j = acc.cnt, kb = acc.kb, vb = acc.vb;
+  uint32_t prev_sh = 0, pp = 0, ppsh = 0;
+#pragma unroll
+  for (int k = 0; k < pipe::kRunBuf; k++) {
+    if (uint32_t(k) < B.cnt) {
+      const uint32_t pos = B.ea[k] & 0xffffu, sh = B.ea[k] >> 16;
+      const uint32_t un = B.eb[k] & 0x3fffu, h = (B.eb[k] >> 14) & 7u, vl = B.eb[k] >> 17;
+      const uint32_t kl = sh + un;
+      uint32_t vs = pos + h + un, vlen = vl;
+      uint8_t fl = 0;
+      if (k == 0) fl = uint8_t(PBL_KV_RESTART | ((B.rw >> 31) ? PBL_KV_RESTART_SAMEPFX : 0));
+      if (!(flags & PBL_ROW_RAW_KEYS) && kl < 8) fl |= PBL_KV_INVALID_KEY;
+      if (vprefix && kl >= 8 && (V.byte(pos + h + (kl - 8 - sh)) & 0xBF) == 1) {
+        const uint32_t pre = V.byte(vs);
+        if ((pre & 0xC0) == 0 || (flags & PBL_ROW_NO_VALUER)) { vs++; vlen--; }
+        else if ((pre & 0xC0) == 0x80) fl |= PBL_KV_VALBLK_HANDLE;
+        else fl |= PBL_KV_BLOB_HANDLE;
+      }
+      uint32_t par = j, parsh = 0;
+      if (sh != 0) {
+        uint32_t c = j - 1, csh = prev_sh;
+        if (csh >= sh) { c = pp; csh = ppsh; }
+        while (csh >= sh) {
+          c = m_par(S.m0[c]);
+          csh = m_sh(S.m0[c]);
+        }
+        par = c;
+        parsh = csh;
+      }
+      S.m0[j] = uint64_t(pos + h) | uint64_t(sh) << 16 | uint64_t(kl) << 32 | uint64_t(par) << 48;
+      S.kout[j] = uint16_t(kb);
+      S.eoff[j] = uint16_t(pos);
+      S.kvf[j] = fl;
+      W.vp[j] = vb | (vs << 16);
+      prev_sh = sh;
+      pp = par;
+      ppsh = parsh;
+      kb += (flags & PBL_ROW_RAW_KEYS) ? kl : (kl >= 8 ? kl - 8 : 0);
+      vb += vlen;
+      j++;
+    }
+  }
+  acc = pipe::RunAcc{j, kb, vb};
+  P = pipe::ParState{prev_sh, pp, ppsh};
+}
+
+// Per-KV metadata of entries [pos, e0) of a run, re-read from the stage
+// (`first` = pos is the restart point; P = the chain state before pos).
+__device__ __forceinline__ void span_meta(Stage& S, Slot& W, const View& V, uint32_t pos, uint32_t e0, uint32_t rw,
+                                          bool first, pipe::ParState P, uint32_t flags, bool vprefix,
+                                          pipe::RunAcc& acc) {
+  uint32_t j = acc.cnt, kb = acc.kb, vb = acc.vb;
+  uint32_t prev_sh = P.prev_sh, pp = P.pp, ppsh = P.ppsh;
+  while (pos < e0) {
+    uint32_t sh, un, vl, h;
+    pipe::hdr2(V.ld8(pos), &sh, &un, &vl, &h);
+    const uint32_t kl = sh + un;
+    uint32_t vs = pos + h + un, vlen = vl;
+    uint8_t fl = 0;
+    if (first) fl = uint8_t(PBL_KV_RESTART | ((rw >> 31) ? PBL_KV_RESTART_SAMEPFX : 0));
+    if (!(flags & PBL_ROW_RAW_KEYS) && kl < 8) fl |= PBL_KV_INVALID_KEY;
+    if (vprefix && kl >= 8 && (V.byte(pos + h + (kl - 8 - sh)) & 0xBF) == 1) {
+      const uint32_t pre = V.byte(vs);
+      if ((pre & 0xC0) == 0 || (flags & PBL_ROW_NO_VALUER)) { vs++; vlen--; }
+      else if ((pre & 0xC0) == 0x80) fl |= PBL_KV_VALBLK_HANDLE;
+      else fl |= PBL_KV_BLOB_HANDLE;
+    }
+    uint32_t par = j, parsh = 0;
+    if (sh != 0) {
+      uint32_t c = j - 1, csh = prev_sh;
+      if (csh >= sh) { c = pp; csh = ppsh; }
+      while (csh >= sh) {
+        c = m_par(S.m0[c]);
+        csh = m_sh(S.m0[c]);
+      }
+      par = c;
+      parsh = csh;
+    }
+    S.m0[j] = uint64_t(pos + h) | uint64_t(sh) << 16 | uint64_t(kl) << 32 | uint64_t(par) << 48;
+    S.kout[j] = uint16_t(kb);
+    S.eoff[j] = uint16_t(pos);
+    S.kvf[j] = fl;
+    W.vp[j] = vb | (vs << 16);
+    prev_sh = sh;
+    pp = par;
+    ppsh = parsh;
+    kb += (flags & PBL_ROW_RAW_KEYS) ? kl : (kl >= 8 ? kl - 8 : 0);
+    vb += vlen;
+    j++;
+    first = false;
+    pos = pos + h + un + vl;
+  }
+  acc = pipe::RunAcc{j, kb, vb};
+}
+
+// byte p of the internal key of KV j (source = max{i <= j : shared_i <= p})
+__device__ __forceinline__ uint32_t key_byte(const Stage& S, const View& V, int j, uint32_t p) {
+  uint64_t m = S.m0[j];
+  while (p < m_sh(m)) m = S.m0[--j];
+  return V.byte(m_ksrc(m) + p - m_sh(m));
+}
+
+__device__ __forceinline__ uint64_t trailer_of(const Stage& S, const View& V, int j, uint64_t m, uint8_t* fl,
+                                               uint32_t flags) {
+  if (flags & PBL_ROW_RAW_KEYS) return 0;
+  const uint32_t kl = m_klen(m);
+  if (kl < 8) return kKindInvalid;
+  const uint32_t sh = m_sh(m);
+  uint64_t raw;
+  if (kl - 8 >= sh) {
+    raw = V.ld8(m_ksrc(m) + (kl - 8 - sh));
+  } else {
+    raw = 0;
+    for (int i = 0; i < 8; i++) raw |= uint64_t(key_byte(S, V, j, kl - 8 + i)) << (8 * i);
+  }
+  if (raw & 64u) *fl |= PBL_KV_OBSOLETE;
+  return raw & kTrailerObsoleteMask;
+}
+
+// Key bytes [c, c + n) of KV m (n <= 16) merged from the segments of its prefix
+// chain: each an LDS read that starts where the chunk's first byte would sit in
+// that entry (at most 15 bytes before the block: the stage's front pad).
+__device__ __forceinline__ uint4 key_chunk(const Stage& S, const View& V, uint64_t m, uint32_t c, uint32_t n) {
+  const uint32_t ce = c + n;
+  uint32_t cur = ce;
+  uint4 w = make_uint4(0, 0, 0, 0);
+  for (;;) {
+    const uint32_t shi = m_sh(m);
+    const uint32_t lo_i = shi < cur ? shi : cur;
+    const uint32_t a = lo_i > c ? lo_i : c;
+    if (a < cur) {
+      const uint4 v = V.ld16(int32_t(m_ksrc(m)) - int32_t(shi) + int32_t(c));
+      if (a == c && cur - a == 16) return v;
+      merge16(w, v, a - c, cur - c);
+    }
+    if (lo_i <= c) break;
+    cur = lo_i;
+    m = S.m0[m_par(m)];
+  }
+  return w;
+}
+
+__device__ __forceinline__ void put16(gptr<uint8_t> base, uint64_t a, const uint4& w, uint32_t lo, uint32_t hi) {
+  if (lo == 0 && hi == 16) *(gptr<u32x4>)(base + a) = u32x4{w.x, w.y, w.z, w.w};
+  else store_partial16(base + a, w, lo, hi);
+}
+
+// Value bytes of a block at output [vbb, vbb + tvb): one 16-B aligned output
+// granule per lane, kVU granules per step with their loads in flight
+// together.  (1) bucket -> first KV; (2) a 5-word window of packed
+// (vout | vsrc) words -> the KV holding the granule's first byte and the next
+// one; (3) both source segments loaded from the block in global memory at
+// once, merged when the granule straddles two values.  Granules touching 3+
+// values (values < 16 B) or more than 3 bucket steps take the general loop.
+__device__ __forceinline__ void copy_values(const Slot& W, gptr<const uint8_t> g, uint32_t blen, uint64_t vbb,
+                                            uint32_t tvb, gptr<uint8_t> vbytes) {
+  const int l = lane_id();
+  const uint32_t end16 = uint32_t(((uint64_t(g) + blen + 15) & ~uint64_t(15)) - uint64_t(g));
+  const uint64_t d0 = vbb, d1 = vbb + tvb;
+  for (uint64_t a = (d0 & ~uint64_t(15)) + 16 * uint64_t(l); a < d1; a += 16 * kVU * kWave) {
+    uint4 w[kVU];
+    uint32_t lo[kVU], hi[kVU], o[kVU], oe[kVU], j0[kVU];
+    bool live[kVU];
+#pragma unroll
+    for (int u = 0; u < kVU; u++) {
+      const uint64_t gq = a + uint64_t(u) * 16 * kWave;
+      live[u] = gq < d1;
+      lo[u] = gq < d0 ? uint32_t(d0 - gq) : 0u;
+      hi[u] = !live[u] ? 0u : (gq + 16 <= d1 ? 16u : uint32_t(d1 - gq));
+      o[u] = live[u] ? uint32_t(gq + lo[u] - d0) : 0u;
+      oe[u] = live[u] ? uint32_t(gq + hi[u] - d0) : 0u;
+      j0[u] = W.vbkt[o[u] >> kVB];
+    }
+    uint32_t vw[kVU][5];
+#pragma unroll
+    for (int u = 0; u < kVU; u++)
+#pragma unroll
+      for (int k = 0; k < 5; k++) vw[u][k] = W.vp[j0[u] + k];
+    uint4 ga[kVU], gb[kVU];
+    uint32_t sa[kVU], ea[kVU], sb[kVU], eb[kVU];
+    bool gen[kVU];
+#pragma unroll
+    for (int u = 0; u < kVU; u++) {
+      const uint32_t q = o[u];
+      const bool s1 = (vw[u][1] & 0xffff) <= q;
+      const bool s2 = s1 && (vw[u][2] & 0xffff) <= q;
+      const bool s3 = s2 && (vw[u][3] & 0xffff) <= q;
+      const uint32_t k = uint32_t(s1) + uint32_t(s2) + uint32_t(s3);
+      const uint32_t A0 = k == 0 ? vw[u][0] : k == 1 ? vw[u][1] : k == 2 ? vw[u][2] : vw[u][3];
+      const uint32_t A1 = k == 0 ? vw[u][1] : k == 1 ? vw[u][2] : k == 2 ? vw[u][3] : vw[u][4];
+      const uint32_t A2 = k == 0 ? vw[u][2] : k == 1 ? vw[u][3] : k == 2 ? vw[u][4] : vw[u][4];
+      const uint32_t v0 = A0 & 0xffff, v1 = A1 & 0xffff, v2 = A2 & 0xffff;
+      gen[u] = live[u] && ((s3 && (vw[u][4] & 0xffff) <= q) || (oe[u] > v1 && oe[u] > v2) || k == 3);
+      sa[u] = q;
+      ea[u] = oe[u] < v1 ? oe[u] : v1;
+      sb[u] = v1;
+      eb[u] = oe[u] < v2 ? oe[u] : v2;
+      const uint32_t gqa = uint32_t(d0 + sa[u] - (a + uint64_t(u) * 16 * kWave));
+      ga[u] = live[u] && !gen[u] ? gld16(g, int32_t(A0 >> 16) + int32_t(sa[u] - v0) - int32_t(gqa), blen, end16)
+                                 : make_uint4(0, 0, 0, 0);
+      const uint32_t gqb = gqa + (sb[u] - sa[u]);
+      gb[u] = live[u] && !gen[u] && oe[u] > v1 ? gld16(g, int32_t(A1 >> 16) - int32_t(gqb), blen, end16)
+                                               : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kVU; u++) {
+      if (!live[u]) continue;
+      const uint64_t gq = a + uint64_t(u) * 16 * kWave;
+      if (!gen[u]) {
+        const uint32_t gqa = uint32_t(d0 + sa[u] - gq);
+        if (gqa == 0 && ea[u] - sa[u] == 16) {
+          w[u] = ga[u];
+        } else {
+          w[u] = make_uint4(0, 0, 0, 0);
+          merge16(w[u], ga[u], gqa, gqa + (ea[u] - sa[u]));
+          if (oe[u] > sb[u]) {
+            const uint32_t gqb = gqa + (sb[u] - sa[u]);
+            merge16(w[u], gb[u], gqb, gqb + (eb[u] - sb[u]));
+          }
+        }
+      } else {
+        uint32_t j = j0[u];
+        while ((W.vp[j + 1] & 0xffffu) <= o[u]) j++;
+        w[u] = make_uint4(0, 0, 0, 0);
+        for (;;) {
+          const uint32_t v0 = W.vp[j] & 0xffffu, v1 = W.vp[j + 1] & 0xffffu;
+          const uint32_t s_ = o[u] > v0 ? o[u] : v0, e_ = oe[u] < v1 ? oe[u] : v1;
+          const uint32_t q = uint32_t(d0 + s_ - gq);
+          merge16(w[u], gld16(g, int32_t(W.vp[j] >> 16) + int32_t(s_ - v0) - int32_t(q), blen, end16), q,
+                  q + (e_ - s_));
+          if (v1 >= oe[u]) break;
+          j++;
+        }
+      }
+      put16(vbytes, gq, w[u], lo[u], hi[u]);
+    }
+  }
+}
+
+// Take a free stage (lane 0 spins on the workgroup's mask); returns its index.
+__device__ __forceinline__ uint32_t acquire(PoolLds& L) {
+  uint32_t s = 0;
+  if (lane_id() == 0) {
+    for (;;) {
+      const uint32_t m = __hip_atomic_load(&L.free_mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (m) {
+        const uint32_t c = uint32_t(__builtin_ctz(m));
+        const uint32_t old =
+            __hip_atomic_fetch_and(&L.free_mask, ~(1u << c), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (old & (1u << c)) {
+          s = c;
+          break;
+        }
+      } else {
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+  }
+  return __builtin_amdgcn_readfirstlane(__shfl(s, 0, kWave));
+}
+
+// Return stage s to the pool once every LDS read of it has completed.
+__device__ __forceinline__ void release(PoolLds& L, uint32_t s) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  wave_sync();
+  if (lane_id() == 0) __hip_atomic_fetch_or(&L.free_mask, 1u << s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// General path for one block (wave-serial Iter.Next) on the staged block, the
+// stage's metadata area as its key buffer; a key that outgrows it re-runs from
+// global memory with the whole stage as the key buffer.  Resolves its own
+// look-back and writes every output.  Out of line: rare and large.
+__device__ __noinline__ void block_slow(Stage& S, const Args A, uint32_t b, uint64_t boff, uint32_t blen) {
+  const int l = lane_id();
+  const uint32_t nb = A.in.n_blocks, flags = A.in.flags;
+  const pbl_decode_out& O = A.out;
+  uint64_t* lb_state = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(O.workspace) + kWsHeader);
+  SlowState ss;
+  uint64_t dummy[kNumComp] = {0, 0, 0, 0}, excl[kNumComp];
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(S.x) + kPad + (boff & 15);
+  bool from_lds = true;
+  uint8_t* keybuf = reinterpret_cast<uint8_t*>(S.m0);
+  uint32_t keycap = uint32_t(sizeof(Stage) - offsetof(Stage, m0)) & ~15u;
+  slow_walk(src, true, blen, flags, A.in.synthetic_seq_num, keybuf, keycap, kPassCount, O, b, dummy, &ss);
+  if (ss.status == PBL_UNSUPPORTED) {
+    from_lds = false;
+    src = A.in.blocks + boff;
+    keybuf = reinterpret_cast<uint8_t*>(S.x);
+    keycap = uint32_t(kLdsBlkBytes);
+    slow_walk(src, false, blen, flags, A.in.synthetic_seq_num, keybuf, keycap, kPassCount, O, b, dummy, &ss);
+  }
+  const bool okk = ss.status == PBL_OK;
+  const uint64_t agg[kNumComp] = {okk ? ss.nkv : 0, okk ? ss.kb : 0, okk ? ss.vb : 0, okk ? ss.nr : 0};
+  lookback(lb_state, nb, b, agg, excl, &O.totals->status_mask);
+  uint32_t st2 = ss.status;
+  if (okk && overflows(O, excl, agg)) st2 = PBL_OVERFLOW;
+  if (st2 == PBL_OK) slow_walk(src, from_lds, blen, flags, A.in.synthetic_seq_num, keybuf, keycap, kPassAll, O, b, excl, &ss);
+  else if (l == 0 && O.key_off && excl[0] + b < O.kv_cap + nb) {
+    to_glb(O.key_off)[excl[0] + b] = 0;
+    to_glb(O.val_off)[excl[0] + b] = 0;
+  }
+  if (l == 0) write_block_meta(O, b, nb, st2, excl, agg, true);
+}
+
+// A block past the stage: big_block_sizes_kernel walked it, published its
+// aggregate and left {status, counts} in its block-metadata slots;
+// big_block_values_kernel writes its outputs after this launch.  Out of line.
+__device__ __noinline__ void block_big(const Args A, uint32_t b, uint64_t boff, uint32_t blen) {
+  const int l = lane_id();
+  const uint32_t nb = A.in.n_blocks;
+  const pbl_decode_out& O = A.out;
+  uint64_t* lb_state = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(O.workspace) + kWsHeader);
+  const uint32_t st0 = to_glb(O.blk_status)[b];
+  const bool okk = st0 == PBL_OK;
+  const uint64_t agg[kNumComp] = {okk ? to_glb(O.blk_kv_base)[b] : 0, okk ? to_glb(O.blk_key_base)[b] : 0,
+                                  okk ? to_glb(O.blk_val_base)[b] : 0,
+                                  okk ? uint64_t(SlowGlb{to_glb(A.in.blocks + boff), blen}.le32(blen - 4)) : 0};
+  uint64_t excl[kNumComp];
+  lb_resolve(lb_state, nb, b, agg, excl, &O.totals->status_mask);
+  uint32_t st2 = st0;
+  if (okk && overflows(O, excl, agg)) st2 = PBL_OVERFLOW;
+  if (l == 0) {
+    if (st2 != PBL_OK && O.key_off && excl[0] + b < O.kv_cap + nb) {
+      to_glb(O.key_off)[excl[0] + b] = 0;
+      to_glb(O.val_off)[excl[0] + b] = 0;
+    }
+    write_block_meta(O, b, nb, st2, excl, agg, true);
+  }
+}
+
+// One block on one wave, stage s held on entry and released before return.
+__device__ __forceinline__ void pool_block(PoolLds& L, uint32_t s, Slot& W, const Args& A, uint32_t b) {
+  Stage& S = L.st[s];
+  const int l = lane_id();
+  const uint32_t nb = A.in.n_blocks, flags = A.in.flags;
+  const uint64_t boff = to_glb(A.in.block_off)[b];
+  const uint32_t blen = to_glb(A.in.block_len)[b];
+  const bool vprefix = (flags & PBL_ROW_VALUE_PREFIX) && !(flags & PBL_ROW_RAW_KEYS);
+  uint8_t* ws = reinterpret_cast<uint8_t*>(A.out.workspace);
+  uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
+  const uint8_t* gblk = A.in.blocks + boff;
+  const pbl_decode_out& O = A.out;
+
+  if (blen > kMaxFastLen) {
+    release(L, s);
+    block_big(A, b, boff, blen);
+    return;
+  }
+
+  PSTAMP(A, b, 1, l == 0);
+  {  // stage: the block by LDS-DMA (granule g of the 16-B aligned range at x[1 + g])
+    const uint64_t a0 = boff & ~uint64_t(15), a1 = (boff + blen + 15) & ~uint64_t(15);
+    const uint32_t n16 = uint32_t((a1 - a0) >> 4);
+    const gptr<const uint8_t> base = to_glb(A.in.blocks + a0);
+    for (uint32_t g0 = 0; g0 < n16; g0 += kWave) {
+      if (g0 + l < n16)
+        __builtin_amdgcn_global_load_lds((gptr<const void>)(base + 16ull * (g0 + l)),
+                                         (lptr<void>)to_lds_ptr(reinterpret_cast<void*>(&S.x[1 + g0])), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+  }
+  PSTAMP(A, b, 2, l == 0);
+  const View V = lds_view(S.x, uint32_t(kPad + (boff & 15)));
+  uint32_t roff, nres;
+  uint32_t status = pipe::init_checks(LdsRd{V}, blen, flags, &roff, &nres);
+  bool slow = status == PBL_OK && nres > uint32_t(kPKv);
+  uint32_t nkv = 0, tkb = 0, tvb = 0;
+  bool published = false;
+  LbWindows<kLbWin> G;
+  if (status == PBL_OK && !slow && roff > 0) {
+    // lane l owns runs [r0, r1): contiguous, so a lane scan orders them
+    const uint32_t R = (nres + kWave - 1) / kWave;
+    const uint32_t r0 = min(uint32_t(l) * R, nres), r1 = min(r0 + R, nres);
+    pipe::RunAcc acc{0, 0, 0};
+    bool ok = true, bad = false, vbad = false, over = false;
+    pipe::RunBuf RB;
+    RB.cnt = 0;
+    RB.pos = RB.e0 = 0;
+    const bool single = R == 1;
+    if (single) {
+      if (r0 < nres) pipe::run_walk(V, r0, nres, roff, flags, vprefix, RB, acc, ok, bad, vbad, over);
+      // a run longer than kRunBuf keeps its parked head and counts only its tail
+      if (over && ok) pipe::run_count_span(V, RB.pos, RB.e0, RB.cnt, RB.prev_kl, flags, vprefix, acc, ok, bad, vbad);
+    } else {
+      for (uint32_t r = r0; r < r1 && ok; r++) pipe::run_count(V, r, nres, roff, flags, vprefix, acc, ok, bad, vbad);
+    }
+    const uint32_t ic = dpp_incl_scan(acc.cnt), ik = dpp_incl_scan(acc.kb), iv = dpp_incl_scan(acc.vb);
+    nkv = last_lane(ic);
+    tkb = last_lane(ik);
+    tvb = last_lane(iv);
+    if (__ballot(bad)) status = PBL_CORRUPT_BOUNDS;
+    else if (__ballot(!ok) || nkv > uint32_t(kPKv) || tkb > kPKeyCap) slow = true;
+    else if (__ballot(vbad)) status = PBL_CORRUPT_BOUNDS;  // Go: i.val[0] on an empty SET value
+    if (status == PBL_OK && !slow) {
+      // the sizes are final: publish, request the look-back windows, and write
+      // the metadata while they are in flight
+      const uint64_t agg[kNumComp] = {nkv, tkb, tvb, nres};
+      lb_publish(lb_state, nb, b, agg);
+      published = true;
+      if (b > 0) G.issue(LbPtrs(lb_state, nb), int64_t(b) - 1);
+      PSTAMP(A, b, 3, l == 0);
+      pipe::RunAcc w{ic - acc.cnt, ik - acc.kb, iv - acc.vb};
+      if (single) {
+        if (r0 < nres) {
+          pipe::ParState P;
+          park_meta(S, W, V, RB, flags, vprefix, w, P);
+          if (over) span_meta(S, W, V, RB.pos, RB.e0, RB.rw, false, P, flags, vprefix, w);
+        }
+      } else {
+        for (uint32_t r = r0; r < r1; r++) {
+          const uint32_t st = roff + 4 * r;
+          const uint32_t rw = V.le32(st);
+          const uint32_t e0 = (r + 1 < nres) ? (V.le32(st + 4) & kRestartMask) : roff;
+          span_meta(S, W, V, rw & kRestartMask, e0, rw, true, pipe::ParState{0, 0, 0}, flags, vprefix, w);
+        }
+      }
+      if (l < 5) W.vp[nkv + l] = tvb;
+      if (l == 0) S.kout[nkv] = uint16_t(tkb);
+      wave_sync();
+      // value buckets: the KV holding byte q * 128 of the block's values
+      for (uint32_t j = l; j < nkv; j += kWave) {
+        const uint32_t v0 = W.vp[j] & 0xffffu, v1 = W.vp[j + 1] & 0xffffu;
+        for (uint32_t q = (v0 + 127) >> kVB; (q << kVB) < v1; q++) W.vbkt[q] = uint16_t(j);
+      }
+      wave_sync();
+      PSTAMP(A, b, 4, l == 0);
+    }
+  }
+
+  if (status == PBL_OK && slow) {
+    block_slow(S, A, b, boff, blen);
+    release(L, s);
+    return;
+  }
+
+  const bool okb = status == PBL_OK;
+  const uint64_t agg[kNumComp] = {okb ? nkv : 0, okb ? tkb : 0, okb ? tvb : 0, okb ? nres : 0};
+  uint64_t excl[kNumComp];
+  if (!published) {
+    lb_publish(lb_state, nb, b, agg);
+    if (b > 0) G.issue(LbPtrs(lb_state, nb), int64_t(b) - 1);
+  }
+  lb_finish(lb_state, nb, b, agg, excl, &O.totals->status_mask, G);
+  PSTAMP(A, b, 5, l == 0);
+  if (okb && overflows(O, excl, agg)) status = PBL_OVERFLOW;
+  if (l == 0) {
+    if (status != PBL_OK && O.key_off && excl[0] + b < O.kv_cap + nb) {
+      to_glb(O.key_off)[excl[0] + b] = 0;
+      to_glb(O.val_off)[excl[0] + b] = 0;
+    }
+    write_block_meta(O, b, nb, status, excl, agg, false);
+  }
+  if (status != PBL_OK) {
+    release(L, s);
+    return;
+  }
+  if (nkv == 0) {  // a block with no entries: its lone N+1 offsets
+    if (l == 0) {
+      S.kout[0] = 0;
+      W.vp[0] = 0;
+    }
+    wave_sync();
+  }
+
+  // ---- keys and per-KV arrays from the stage: lane per KV --------------------
+  const uint64_t kvb = excl[0], kbb = excl[1], vbb = excl[2], rbb = excl[3];
+  const gptr<uint8_t> kbytes = to_glb(O.key_bytes) + kbb;
+  const bool raw = (flags & PBL_ROW_RAW_KEYS) != 0;
+  for (uint32_t j = l; j <= nkv; j += kWave) {
+    to_glb(O.key_off)[kvb + b + j] = S.kout[j];
+    to_glb(O.val_off)[kvb + b + j] = W.vp[j] & 0xffffu;
+    if (j < nkv) {
+      const uint64_t m = S.m0[j];
+      uint8_t fl = S.kvf[j];
+      to_glb(O.trailer)[kvb + j] = with_seq(trailer_of(S, V, int(j), m, &fl, flags), A.in.synthetic_seq_num, flags);
+      if (O.kv_flags) to_glb(O.kv_flags)[kvb + j] = fl;
+      if (O.entry_off) to_glb(O.entry_off)[kvb + j] = S.eoff[j];
+      const uint32_t ukl = raw ? m_klen(m) : (m_klen(m) >= 8 ? m_klen(m) - 8 : 0u);
+      const uint32_t ko = S.kout[j];
+      for (uint32_t c = 0; c < ukl; c += 16) {
+        const uint32_t n = ukl - c < 16 ? ukl - c : 16u;
+        store_n(kbytes + ko + c, key_chunk(S, V, m, c, n), n);
+      }
+    }
+  }
+  if (O.restarts)
+    for (uint32_t r = l; r < nres; r += kWave) to_glb(O.restarts)[rbb + r] = V.le32(roff + 4 * r);
+  release(L, s);
+  PSTAMP(A, b, 6, l == 0);
+
+  // ---- values, global -> global --------------------------------------------
+  if (tvb) copy_values(W, to_glb(gblk), blen, vbb, tvb, to_glb(O.val_bytes));
+  PSTAMP(A, b, 7, l == 0);
+  wave_sync();  // (the slot is the next block's)
+}
+
+// The persistent kernel: one workgroup of kNW waves per CU, each wave an
+// independent loop of (acquire a stage, take a ticket, decode the block).
+// Deadlock-free for any residency: a wave takes a ticket only while holding a
+// stage, and waits (in the look-back) only on smaller tickets, all of them
+// taken by waves that hold a stage or no longer need one.
+__global__ void __launch_bounds__(kTPBP, 1) rowblk_pool_kernel(Args A) {
+  __shared__ PoolLds L;
+  if (threadIdx.x == 0) L.free_mask = (1u << kNS) - 1u;
+  __syncthreads();
+  Slot& W = L.sl[wave_id()];
+  const uint32_t nb = A.in.n_blocks;
+  uint32_t* tick = reinterpret_cast<uint32_t*>(A.out.workspace);
+  for (;;) {
+    const uint32_t s = acquire(L);
+    uint32_t t0 = 0;
+    if (lane_id() == 0) t0 = g_atomic_add(tick, 1u);
+    t0 = __builtin_amdgcn_readfirstlane(__shfl(t0, 0, kWave));
+    if (t0 >= nb) {
+      release(L, s);
+      break;
+    }
+    PSTAMP(A, t0, 0, lane_id() == 0);
+    pool_block(L, s, W, A, t0);
+  }
+}
+
+}  // namespace pool

@@ -15,7 +15,7 @@ from pebble_amd.rowblk import Writer, gen_row_blocks
 from test_rowblk_gpu import GOLDEN, assert_same, pack, random_block
 
 pytestmark = pytest.mark.gpu
-KERNELS = {"flat": N.PBL_KERNEL_FLAT, "run": N.PBL_KERNEL_RUN, "global": N.PBL_KERNEL_GLOBAL}
+KERNELS = {"flat": N.PBL_KERNEL_FLAT, "run": N.PBL_KERNEL_RUN, "global": N.PBL_KERNEL_GLOBAL, "pool": N.PBL_KERNEL_POOL}
 FLAT = N.PBL_KERNEL_FLAT
 
 

@@ -270,3 +270,89 @@ def test_snappy_corrupt_matches_oracle():
             assert st[i] in (N.PBL_CORRUPT_COMPRESSION,), (i, st[i])
         else:
             assert st[i] == 0 and bytes(out[bo[i]: bo[i] + bl[i]]) == want, i
+
+
+# ---- MinLZ (indicator 8) ---------------------------------------------------------
+def test_minlz_snappy_form_decodes_to_hamlet(golden):
+    """minlz_test.go:31-36: a MinLZ decompressor decodes the Snappy fallback's
+    output — the reference's snappy hamlet blocks relabelled indicator 8."""
+    blob = BLOB.copy()
+    for b in PHYS["hamlet_snappy"]["blocks"]:
+        blob[b["blob_off"] + b["length"]] = N.PBL_COMPRESSION_MINLZ
+    bb, st = decompress(file_batch("hamlet_snappy", blob))
+    assert list(st) == [0] * bb.n_blocks
+    assert list(bb.block_len.cpu().numpy()) == [b["decompressed_len"] for b in PHYS["hamlet_snappy"]["blocks"]]
+    assert hamlet_kvs(bb) == [tuple(x) for x in golden["hamlet_kvs"]]
+
+
+def test_minlz_random_blocks_lds_and_global_paths():
+    """The MinLZ form (parity unpinned: the oracle's restatement of the format,
+    oracle/minlz_oracle.c) on the device, every op form and the stored form,
+    blocks past the 32 KiB stage on the global path."""
+    rng = random.Random(31)
+    sizes = [0, 1, 2, 5, 64, 65, 1000, 32767, 32768, 32769, 40_000, 131_072, 300_000]
+    sizes += [rng.randrange(0, 33_000) for _ in range(150)]
+    raw = []
+    for i, n in enumerate(sizes):
+        k = i % 5
+        raw.append(rng.randbytes(n) if k == 0 else bytes([rng.randrange(3)]) * n if k == 1 else compressible(rng, n))
+    far = rng.randbytes(70_000)
+    raw += [far + rng.randbytes(50) + far[:5000], bytes(rng.randrange(3) for _ in range(40_000))]
+    comp = [oracle.minlz_encode(r, i % 16) for i, r in enumerate(raw)]
+    comp += [snappy(r) for r in raw[:30]]  # the Snappy form under indicator 8
+    want = raw + raw[:30]
+    buf, off, lens = pack_phys(comp, lambda b: 0, rng, indicator=N.PBL_COMPRESSION_MINLZ)
+    bb, st = decompress(PhysBatch.from_host(buf, off, lens))
+    assert list(st) == [0] * len(comp)
+    out, bo, bl = bb.blocks.cpu().numpy(), bb.block_off.cpu().numpy(), bb.block_len.cpu().numpy()
+    for i, w in enumerate(want):
+        assert bl[i] == len(w), i
+        assert bytes(out[bo[i]: bo[i] + bl[i]]) == w, i
+        assert oracle.minlz_decode(comp[i]) == w
+
+
+def test_minlz_corrupt_matches_oracle():
+    rng = random.Random(32)
+    blocks = []
+    for i in range(120):
+        r = compressible(rng, rng.randrange(1, 40_000))
+        b = bytearray(oracle.minlz_encode(r, rng.randrange(8)))
+        m = i % 6
+        if m == 0:
+            b = b[: rng.randrange(1, len(b))]                      # truncated
+        elif m == 1:
+            b[rng.randrange(3, len(b))] ^= 1 << rng.randrange(8)  # one bit flipped past the header
+        elif m == 2:
+            b = bytearray(b"\x00" + b"\xff" * 11)                 # unterminated length varint
+        elif m == 3:
+            b[1] = (b[1] + 1) & 0x7F if b[1] < 0x80 else b[1]     # wrong decoded length
+        elif m == 4:
+            b = bytearray(b"\x00\x05\x05\x00")                    # copy before any output
+        blocks.append(bytes(b))
+    blocks += [b"", b"\x00", b"\x00\x00", b"\x00\x00abc", b"\x00\x01\x08ab"]
+    buf, off, lens = pack_phys(blocks, lambda b: 0, rng, indicator=N.PBL_COMPRESSION_MINLZ)
+    bb, st = decompress(PhysBatch.from_host(buf, off, lens))
+    out, bo, bl = bb.blocks.cpu().numpy(), bb.block_off.cpu().numpy(), bb.block_len.cpu().numpy()
+    for i, b in enumerate(blocks):
+        want = oracle.minlz_decode(b)
+        if want is None:
+            assert st[i] == N.PBL_CORRUPT_COMPRESSION, (i, st[i])
+        else:
+            assert st[i] == 0 and bytes(out[bo[i]: bo[i] + bl[i]]) == want, i
+
+
+def test_minlz_mixed_with_other_codecs():
+    rng = random.Random(33)
+    raw = [compressible(rng, rng.randrange(1, 30_000)) for _ in range(80)]
+    blocks, inds = [], []
+    for i, r in enumerate(raw):
+        k = i % 4
+        blocks.append(zstd_block(r, 3) if k == 0 else snappy(r) if k == 1 else oracle.minlz_encode(r, 3) if k == 2 else r)
+        inds.append(7 if k == 0 else 1 if k == 1 else 8 if k == 2 else 0)
+    it = iter(inds)
+    buf, off, lens = pack_phys(blocks, lambda b: 0, rng, indicator=lambda b: next(it))
+    bb, st = decompress(PhysBatch.from_host(buf, off, lens))
+    assert list(st) == [0] * len(blocks)
+    out, bo, bl = bb.blocks.cpu().numpy(), bb.block_off.cpu().numpy(), bb.block_len.cpu().numpy()
+    for i, want in enumerate(raw):
+        assert bytes(out[bo[i]: bo[i] + bl[i]]) == want, i
