@@ -62,7 +62,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the host->device->host (PCIe-inclusive) pass")
     p.add_argument("--e2e-chunk", type=int, default=2048, help="blocks per PCIe pipeline chunk")
-    p.add_argument("--kernel", choices=["auto", "single", "pipe", "flat", "run", "global", "pool"], default="auto",
+    p.add_argument("--kernel", choices=["auto", "single", "pipe", "flat", "global", "pool"], default="auto",
                    help="A/B: PBL_KERNEL_SINGLE / PBL_KERNEL_PIPE / PBL_KERNEL_FLAT batch flags")
     p.add_argument("--launch-check", action="store_true",
                    help="launcher self-test without a GPU: N gloo ranks report in, rank 0 prints one JSON line")
@@ -244,7 +244,7 @@ def main():
 
     nb = a.blocks or (131072 if a.workload == "mixed" else 65536)
     flags = N.PBL_ROW_VALUE_PREFIX if a.value_prefix else 0
-    flags |= {"auto": 0, "single": N.PBL_KERNEL_SINGLE, "pipe": N.PBL_KERNEL_PIPE, "flat": N.PBL_KERNEL_FLAT, "run": N.PBL_KERNEL_RUN, "global": N.PBL_KERNEL_GLOBAL, "pool": N.PBL_KERNEL_POOL}[a.kernel]
+    flags |= {"auto": 0, "single": N.PBL_KERNEL_SINGLE, "pipe": N.PBL_KERNEL_PIPE, "flat": N.PBL_KERNEL_FLAT, "global": N.PBL_KERNEL_GLOBAL, "pool": N.PBL_KERNEL_POOL}[a.kernel]
     seed = a.seed + 7919 * rank
     t0 = time.time()
     block_fmt = None
@@ -252,7 +252,7 @@ def main():
         fmt = N.PBL_FMT_ROW
         buf, off, lens, n_kv = gen_row_blocks(seed, nb, a.block_size, a.restart_interval, a.key_len, a.val_len,
                                               a.value_prefix, n_threads=16)
-        kernel = {"single": "rowblk_decode_kernel", "flat": "rowblk_flat_kernel", "run": "rowblk_run_kernel", "pool": "rowblk_pool_kernel",
+        kernel = {"single": "rowblk_decode_kernel", "flat": "rowblk_flat_kernel", "pool": "rowblk_pool_kernel",
                   "global": "glb_sizes_kernel+glb_scan_kernel+glb_values_kernel"}.get(a.kernel, "rowblk_pipe_kernel")
         if a.workload == "transform":
             kernel = "tf_count_kernel+tf_scan_kernel+tf_scatter_kernel"
@@ -276,7 +276,6 @@ def main():
         vl = varlen_hint(lens) and a.kernel not in ("pipe", "single")
         kernel = (("glb_sizes_kernel+glb_scan_kernel+glb_values_kernel" if a.kernel == "global" or
                    (vl and a.kernel == "auto") else
-                   "rowblk_run_kernel" if a.kernel == "run" else
                    "rowblk_pool_kernel" if a.kernel == "pool" else
                    "rowblk_flat_kernel" if a.kernel == "flat" else
                    "rowblk_decode_kernel" if a.kernel == "single" else "rowblk_pipe_kernel") if fmt == N.PBL_FMT_ROW

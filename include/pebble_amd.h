@@ -93,9 +93,7 @@ enum {
 #define PBL_KERNEL_FLAT 0x800u    /* A/B measurement, no effect on results: row
                                      batches on the one-wave-per-block kernel
                                      (rowblk_flat.hip.h) even without VARLEN        */
-#define PBL_KERNEL_RUN 0x1000u    /* A/B measurement, no effect on results: row
-                                     batches on the run-major one-wave-per-block
-                                     kernel (rowblk_run.hip.h)                      */
+/* 0x1000u: retired (the run-major row kernel, removed; the bit is ignored)       */
 #define PBL_KERNEL_GLOBAL 0x2000u /* A/B measurement, no effect on results: row
                                      batches walked from HBM by a wave per block in
                                      three launches (rowblk_global.hip.h)           */

@@ -55,7 +55,6 @@ PBL_BATCH_VARLEN = 0x100
 PBL_KERNEL_SINGLE = 0x200
 PBL_KERNEL_PIPE = 0x400
 PBL_KERNEL_FLAT = 0x800
-PBL_KERNEL_RUN = 0x1000
 PBL_KERNEL_GLOBAL = 0x2000
 PBL_KERNEL_POOL = 0x4000
 

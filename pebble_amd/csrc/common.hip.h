@@ -484,8 +484,8 @@ __device__ inline bool overflows(const pbl_decode_out& O, const uint64_t excl[kN
 // they are queried once and cached (the library's only process-wide state, and
 // immutable once written; racing first calls store the same values).
 enum PersistentKernel {
-  kKRowPipe = 0, kKRowSingle = 1, kKColPipe = 2, kKMixedPipe = 3, kKMixedColSize = 4, kKMixedRow = 5, kKMixedCol = 6,
-  kKRowFlat = 7, kKRowRun = 8, kKRowPool = 9, kKNum = 10
+  kKRowPipe = 0, kKRowSingle = 1, kKColPipe = 2, kKMixedColSize = 3, kKMixedRow = 4, kKMixedCol = 5,
+  kKRowFlat = 6, kKRowPool = 7, kKNum = 8
 };
 
 // Resident grid for `fn` on the stream's device (never more than n_units, at

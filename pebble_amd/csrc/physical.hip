@@ -26,8 +26,6 @@
 //                         the walk does not cover): one wave per block, the
 //                         input staged in LDS, the elements walked by the wave
 //                         with scalar arithmetic, then snappy4's phases
-//   snappy_kernel         (PBL_SNAPPY_VER 1 A/B) the first form: input and output
-//                         staged in LDS, the wave copies one element at a time
 //   zstd_kernel           (zstd.hip) the blocks whose indicator is zstd
 //   minlz_kernel          (minlz_dec.hip.h) MinLZ blocks in the MinLZ form; a
 //                         MinLZ-indicated block in the Snappy form (first byte
@@ -320,12 +318,8 @@ __global__ void __launch_bounds__(kTPB) snappy_len_kernel(const pbl_phys_batch B
 // src[(block address & 15) + j]) so the staging loads and the output stores
 // are aligned 16-B accesses; 32 bytes of slack cover the phase and the 16-B
 // literal copies that run past an element's end.
-// PBL_SNAPPY_VEC: 16-B staging, literal / long-offset copies and output
-// stores (GPU parity green; 72.7 -> 77.1 GB/s on config-2 blocks: the bound is
-// elsewhere). 0 keeps the byte-wise form.
-#ifndef PBL_SNAPPY_VEC
-#define PBL_SNAPPY_VEC 1
-#endif
+// LDS staging of one block for the one-wave decoders (minlz_kernel): the
+// compressed bytes and the decoded bytes, each at its global 16-B phase.
 struct SnapLds {
   uint4 src4[(kSnapCap + 32) / 16];
   uint4 dst4[(kSnapCap + 32) / 16];
@@ -416,7 +410,7 @@ __device__ inline uint32_t snappy_wave(Src src, uint32_t n, Dst dst, uint32_t ca
       s += 5;
     }
     if (kind != 0 && (off == 0 || off > d || len > dlen - d)) { ok = false; break; }
-    if constexpr (Src::kVec && PBL_SNAPPY_VEC) {
+    if constexpr (Src::kVec) {
       // LDS -> LDS (the wave): 16 bytes per lane per step.  A chunk may write
       // up to 15 bytes past the element's end: later elements rewrite them, and
       // copies read only below d.  A copy whose offset is at least one step's
@@ -441,98 +435,7 @@ __device__ inline uint32_t snappy_wave(Src src, uint32_t n, Dst dst, uint32_t ca
   return ok && d == dlen ? d : ~0u;
 }
 
-__global__ void __launch_bounds__(kWave) snappy_kernel(const pbl_phys_batch B, uint8_t* out, const uint64_t* out_off,
-                                                       const uint32_t* out_cap, uint32_t* out_len, uint32_t* status) {
-  __shared__ SnapLds S;
-  const uint32_t lane = lane_id();
-  for (uint32_t b = blockIdx.x; b < B.n_blocks; b += gridDim.x) {
-    const uint32_t n = B.block_len[b];
-    const gptr<const uint8_t> src = to_glb(B.bytes + B.block_off[b]);
-    const uint32_t ind = src[n];
-    if (ind == PBL_COMPRESSION_ZSTD) continue;  // zstd_kernel's
-    gptr<uint8_t> dst = to_glb(out + out_off[b]);
-    const uint32_t cap = out_cap[b];
-    uint32_t st = PBL_OK, len = 0;
-    if (ind == PBL_COMPRESSION_NONE) {
-      if (n > cap) st = PBL_OVERFLOW;
-      else
-        for (uint32_t i = lane; i < n; i += kWave) dst[i] = src[i];
-      len = n;
-    } else if (ind == PBL_COMPRESSION_SNAPPY) {
-      uint32_t dl = 0, used = 0;
-      if (!uvarint32(src, n, &dl, &used)) st = PBL_CORRUPT_COMPRESSION;
-      else if (dl > cap) st = PBL_OVERFLOW;
-      else if (n <= kSnapCap && dl <= kSnapCap) {
-#if !PBL_SNAPPY_VEC
-        // stage the compressed bytes, decode LDS -> LDS, write the output out
-        lptr<uint8_t> s_src = to_lds_ptr(reinterpret_cast<uint8_t*>(S.src4));
-        lptr<uint8_t> s_dst = to_lds_ptr(reinterpret_cast<uint8_t*>(S.dst4));
-        for (uint32_t i = lane; i < n; i += kWave) s_src[i] = src[i];
-        wave_sync();
-        len = snappy_wave(LdsBytes{s_src}, n, LdsBytesW{s_dst}, dl, lane, kWave);
-        wave_sync();
-        if (len == ~0u) st = PBL_CORRUPT_COMPRESSION;
-        else
-          for (uint32_t i = lane; i < len; i += kWave) dst[i] = s_dst[i];
-#else
-        // stage the compressed bytes (aligned 16-B granules: the last one
-        // stays inside the 16-B granule of the block's last byte), decode
-        // LDS -> LDS, write the output as aligned 16-B granules
-        const uint64_t sa = reinterpret_cast<uint64_t>(B.bytes + B.block_off[b]);
-        const uint32_t ssh = uint32_t(sa & 15), ng = (ssh + n + 15) / 16;
-        const gptr<const u32x4> sg = to_glb(reinterpret_cast<const u32x4*>(sa - ssh));
-        lptr<u32x4> sl = to_lds_ptr(reinterpret_cast<u32x4*>(S.src4));
-        for (uint32_t g = lane; g < ng; g += kWave) sl[g] = sg[g];
-        const uint64_t da = reinterpret_cast<uint64_t>(out + out_off[b]);
-        const uint32_t dsh = uint32_t(da & 15);
-        lptr<uint8_t> sdst = to_lds_ptr(reinterpret_cast<uint8_t*>(S.dst4)) + dsh;
-        wave_sync();
-        len = snappy_wave(LdsBytes{to_lds_ptr(reinterpret_cast<uint8_t*>(S.src4)) + ssh}, n, LdsBytesW{sdst}, dl, lane,
-                          kWave);
-        wave_sync();
-        if (len == ~0u) st = PBL_CORRUPT_COMPRESSION;
-        else {
-          const uint32_t nd = (dsh + len + 15) / 16;
-          const gptr<u32x4> dg = to_glb(reinterpret_cast<u32x4*>(da - dsh));
-          const lptr<const u32x4> dl4 = to_lds_ptr(reinterpret_cast<const u32x4*>(S.dst4));
-          for (uint32_t g = lane; g < nd; g += kWave) {
-            const u32x4 v = dl4[g];
-            const uint32_t lo = g == 0 ? dsh : 0u, hi = g + 1 == nd ? dsh + len - 16 * g : 16u;
-            if (lo == 0 && hi == 16) {
-              dg[g] = v;
-            } else {
-              gptr<uint8_t> db = reinterpret_cast<gptr<uint8_t>>(dg + g);
-              for (uint32_t k = lo; k < hi; k++) {
-                const uint32_t w = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
-                db[k] = uint8_t(w >> (8 * (k & 3)));
-              }
-            }
-          }
-        }
-#endif
-      } else {
-        // large blocks: global -> global, each element's bytes fenced before the next reads them
-        len = ~0u;
-        if (lane == 0) {
-          // one lane: program order makes every earlier output byte visible to its own loads
-          len = snappy_wave(GlbBytes{src}, n, GlbBytesW{dst}, dl, 0, 1);
-        }
-        len = __shfl(len, 0, kWave);
-        if (len == ~0u) st = PBL_CORRUPT_COMPRESSION;
-      }
-    } else {
-      st = PBL_UNSUPPORTED;
-    }
-    if (lane == 0) {
-      out_len[b] = st == PBL_OK ? len : 0u;
-      status[b] = st;
-    }
-    wave_sync();
-  }
-}
-
-
-// ---- snappy v2 (PBL_SNAPPY_VER 2; also v3's path for blocks past its window) ----
+// ---- snappy: snappy2_kernel (also the path for blocks the walk does not cover) ----
 // One wave per block, four blocks per CU (38 KB of LDS each: the compressed
 // bytes and a queue of element descriptors; the output goes straight to HBM):
 //   parse     lane 0 walks the element tags from LDS (8 bytes per element in
@@ -547,9 +450,6 @@ __global__ void __launch_bounds__(kWave) snappy_kernel(const pbl_phys_batch B, u
 //             once), others 16-B chunks.  A workgroup fence between groups.
 // Blocks past the LDS stage (or decoding past 64 KiB) take snappy_wave on one
 // lane from global memory.
-#ifndef PBL_SNAPPY_VER
-#define PBL_SNAPPY_VER 2  // 1: snappy_kernel (A/B), 2: snappy_walk_kernel + snappy4_kernel + snappy2_kernel
-#endif
 constexpr uint32_t kSnIn = 32768;
 constexpr uint32_t kSnQ = 592;  // (4 blocks per CU: 40 KB of LDS each)
 #ifdef PBL_SNAP_STAMPS  // diagnostic builds: per-block phase cycles (scripts/snap_stamps.py)
@@ -706,11 +606,6 @@ int pbl_decompress_blocks(const pbl_phys_batch* batch, uint8_t* out, const uint6
   if (batch->n_blocks == 0) return PBL_OK;
   if (!batch->bytes || !batch->block_off || !batch->block_len) return PBL_INVALID_ARG;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-#if PBL_SNAPPY_VER == 1
-  const uint32_t grid = std::min<uint32_t>(batch->n_blocks, 2048);
-  hipLaunchKernelGGL(pbl::phys::snappy_kernel, dim3(grid), dim3(pbl::kWave), 0, st, *batch, out, out_off, out_cap,
-                     out_len, status);
-#elif PBL_SNAPPY_VER == 2
   hipLaunchKernelGGL(pbl::phys::snappy_walk_kernel, dim3((batch->n_blocks + pbl::kTPB - 1) / pbl::kTPB),
                      dim3(pbl::kTPB), 0, st, *batch, out, out_off, out_cap);
   hipLaunchKernelGGL(pbl::phys::snappy4_kernel, dim3(std::min<uint32_t>(batch->n_blocks, 8192)), dim3(pbl::kWave), 0,
@@ -718,7 +613,6 @@ int pbl_decompress_blocks(const pbl_phys_batch* batch, uint8_t* out, const uint6
   const uint32_t grid = std::min<uint32_t>(batch->n_blocks, 4096);
   hipLaunchKernelGGL(pbl::phys::snappy2_kernel, dim3(grid), dim3(pbl::kWave), 0, st, *batch, out, out_off, out_cap,
                      out_len, status);
-#endif
   hipLaunchKernelGGL(pbl::phys::minlz_kernel, dim3(std::min<uint32_t>(batch->n_blocks, 2048)), dim3(pbl::kWave), 0, st,
                      *batch, out, out_off, out_cap, out_len, status);
   if (hipGetLastError() != hipSuccess) return PBL_DEVICE_ERROR;

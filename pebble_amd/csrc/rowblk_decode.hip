@@ -801,7 +801,6 @@ __global__ void __launch_bounds__(kTPB, 3) rowblk_decode_kernel(Args A) {
 #include "rowblk_pipe.hip.h"
 #include "rowblk_flat.hip.h"
 #include "rowblk_pool.hip.h"
-#include "rowblk_run.hip.h"
 #include "rowblk_global.hip.h"
 
 // Mixed row + colblk batch (config 4): per-block format from block_format[];
@@ -848,12 +847,6 @@ namespace row {
 #endif
 #ifndef PBL_MIX_ROW_LB_WIN
 #define PBL_MIX_ROW_LB_WIN 2  // measured 2 / 4 / 8 windows: 965 / 954 / 946 GiB/s on config 4
-#endif
-#ifndef PBL_MIXED_SEQ
-#define PBL_MIXED_SEQ 1  // 0: one mixed_pipe_kernel launch (A/B)
-#endif
-#ifndef PBL_MIX_ROW_PRIO
-#define PBL_MIX_ROW_PRIO 0  // 1: the row parse wave at s_setprio 2 as in rowblk_pipe_kernel (measured 858 vs 870 GiB/s without)
 #endif
 
 __global__ void __launch_bounds__(kTPB) mixed_split_count_kernel(Args A, uint32_t* counts) {
@@ -920,31 +913,9 @@ __global__ void __launch_bounds__(kTPB) mixed_split_scatter_kernel(Args A, const
   }
 }
 
-union MixedPipeLds {
-  pipe::PLds row;
-  col::cpipe::CLds col;
-};
-
-__global__ void __launch_bounds__(pipe::kPTPB) __attribute__((amdgpu_waves_per_eu(PBL_PIPE_WAVES / 2, PBL_PIPE_WAVES / 2)))
-mixed_pipe_kernel(Args A, const uint32_t* ids) {
-  __shared__ MixedPipeLds L;
-  const uint32_t nb = A.in.n_blocks;
-  uint32_t* hdr = reinterpret_cast<uint32_t*>(A.out.workspace);
-  const uint32_t n_row = __hip_atomic_load(to_glb(hdr) + kWsRowCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t n_col = nb - n_row;
-  const uint64_t G = gridDim.x;
-  uint64_t g_row = n_col == 0 ? G : n_row == 0 ? 0
-                 : (G * 1000ull * n_row + (1000ull * n_row + uint64_t(PBL_MIX_COL_COST) * n_col) / 2) /
-                       (1000ull * n_row + uint64_t(PBL_MIX_COL_COST) * n_col);
-  if (n_row && n_col) g_row = g_row < 1 ? 1 : g_row > G - 1 ? G - 1 : g_row;
-  if (blockIdx.x < g_row)
-    pipe::row_pipe_body<PBL_MIX_ROW_PRIO != 0>(L.row, A, ListQueue{hdr, ids, n_row, nb});
-  else
-    col::cpipe::col_pipe_body(L.col, A, ListQueue{hdr + kWsColTick, ids + n_row, n_col, nb});
-}
-
-// Sequential mixed batches (the default): three persistent launches over the
-// split id lists instead of one.  (1) mixed_col_size_kernel parses every
+// Mixed batches: three persistent launches over the split id lists.  (A single
+// launch running both pipeline bodies, the first form, measured 892 against
+// 976 GiB/s on config 4.)  (1) mixed_col_size_kernel parses every
 // colblk block and publishes its aggregate; (2) mixed_row_kernel runs the row
 // pipeline over the row list, its look-back walking through the colblk
 // aggregates; (3) mixed_col_kernel runs the colblk pipeline over the colblk
@@ -1107,7 +1078,7 @@ bool use_flat(uint32_t flags) { return (flags & PBL_KERNEL_FLAT) != 0; }
 // (profiles/r03_final/ab_zipf_global_*.json, bench_zipf_ri*.json).
 bool use_global(uint32_t flags) {
   return (flags & PBL_KERNEL_GLOBAL) ||
-         ((flags & PBL_BATCH_VARLEN) && !(flags & (PBL_KERNEL_PIPE | PBL_KERNEL_FLAT | PBL_KERNEL_RUN | PBL_KERNEL_POOL)));
+         ((flags & PBL_BATCH_VARLEN) && !(flags & (PBL_KERNEL_PIPE | PBL_KERNEL_FLAT | PBL_KERNEL_POOL)));
 }
 
 // Row batches on the flat kernel (rowblk_flat.hip.h): blocks past its length
@@ -1141,23 +1112,6 @@ int launch_row_pool(const pbl::Args& a, hipStream_t st, bool values) {
   const uint32_t small = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4));
   hipLaunchKernelGGL(pbl::row::pipe::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
   hipLaunchKernelGGL(pbl::row::pool::rowblk_pool_kernel, dim3(uint32_t(grid)), dim3(pbl::row::pool::kTPBP), 0, st, a);
-  if (values) hipLaunchKernelGGL(pbl::row::pipe::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
-  return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
-}
-
-// Row batches on the run-major kernel (rowblk_run.hip.h), with the same
-// big-block passes around it.
-int launch_row_run(const pbl::Args& a, hipStream_t st, bool values) {
-  const uint32_t nb = a.in.n_blocks;
-  int cus = 0;
-  const uint64_t grid = pbl::persistent_grid(st, pbl::kKRowRun,
-                                             reinterpret_cast<const void*>(pbl::row::runk::rowblk_run_kernel),
-                                             (uint64_t(nb) + pbl::row::runk::kRW - 1) / pbl::row::runk::kRW, &cus,
-                                             pbl::row::runk::kRTPB);
-  if (!grid) return PBL_DEVICE_ERROR;
-  const uint32_t small = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4));
-  hipLaunchKernelGGL(pbl::row::pipe::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
-  hipLaunchKernelGGL(pbl::row::runk::rowblk_run_kernel, dim3(uint32_t(grid)), dim3(pbl::row::runk::kRTPB), 0, st, a);
   if (values) hipLaunchKernelGGL(pbl::row::pipe::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }
@@ -1202,7 +1156,6 @@ int launch_mixed(const pbl_block_batch* batch, const pbl::Args& a, hipStream_t s
   hipLaunchKernelGGL(pbl::row::mixed_split_scatter_kernel, dim3(nch), dim3(pbl::kTPB), 0, st, a,
                      static_cast<const uint32_t*>(counts), nch, ids);
   int cus = 0;
-#if PBL_MIXED_SEQ
   const uint64_t g_r = pbl::persistent_grid(st, pbl::kKMixedRow, reinterpret_cast<const void*>(pbl::row::mixed_row_kernel),
                                             nb, &cus, pbl::row::pipe::kPTPB);
   const uint64_t g_c = pbl::persistent_grid(st, pbl::kKMixedCol, reinterpret_cast<const void*>(pbl::row::mixed_col_kernel),
@@ -1218,19 +1171,6 @@ int launch_mixed(const pbl_block_batch* batch, const pbl::Args& a, hipStream_t s
   if (values)
     hipLaunchKernelGGL(pbl::row::pipe::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
-#else
-  const uint64_t grid = pbl::persistent_grid(st, pbl::kKMixedPipe,
-                                             reinterpret_cast<const void*>(pbl::row::mixed_pipe_kernel), nb, &cus,
-                                             pbl::row::pipe::kPTPB);
-  if (!grid) return PBL_DEVICE_ERROR;
-  const uint32_t small = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4));
-  hipLaunchKernelGGL(pbl::row::pipe::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
-  hipLaunchKernelGGL(pbl::row::mixed_pipe_kernel, dim3(uint32_t(grid)), dim3(pbl::row::pipe::kPTPB), 0, st, a,
-                     static_cast<const uint32_t*>(ids));
-  if (values)
-    hipLaunchKernelGGL(pbl::row::pipe::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
-  return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
-#endif
 }
 }  // namespace
 
@@ -1268,7 +1208,6 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
     // persistent kernel (kept for A/B measurement); the default is the pipeline.
     const bool single = (batch->flags & PBL_KERNEL_SINGLE) != 0;
     if (!single && use_global(batch->flags)) return launch_row_global(a, st, true);
-    if (!single && (batch->flags & PBL_KERNEL_RUN)) return launch_row_run(a, st, true);
     if (!single && (batch->flags & PBL_KERNEL_POOL)) return launch_row_pool(a, st, true);
     if (!single && use_flat(batch->flags)) return launch_row_flat(a, st, true);
     const void* fn = single ? reinterpret_cast<const void*>(pbl::row::rowblk_decode_kernel)
@@ -1335,9 +1274,6 @@ int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stre
       if (rc != PBL_OK) return rc;
     } else if (use_global(batch->flags)) {
       rc = launch_row_global(a, st, false);
-      if (rc != PBL_OK) return rc;
-    } else if (batch->flags & PBL_KERNEL_RUN) {
-      rc = launch_row_run(a, st, false);
       if (rc != PBL_OK) return rc;
     } else if (batch->flags & PBL_KERNEL_POOL) {
       rc = launch_row_pool(a, st, false);

@@ -75,13 +75,7 @@ constexpr int kVU = PBL_VU;  // value granules per emit-loop step (their LDS rou
 constexpr int kPTPB = PBL_PIPE_WAVES * kWave;  // threads per pipelined workgroup
 constexpr int kEmit = kPTPB - kWave;           // emitter threads (waves 1..)
 
-enum { kModeNone = 0, kModeFast = 1, kModeErr = 2, kModeDone = 3, kModeResolve = 4 };
-#ifndef PBL_PIPE_LANE
-// 1: the emit waves resolve the look-back and write lane per KV (no output
-// bucket tables, no resolve on the parse wave); 0: the parse wave resolves and
-// the emit writes 16-B output granules
-#define PBL_PIPE_LANE 0
-#endif
+enum { kModeNone = 0, kModeFast = 1, kModeErr = 2, kModeDone = 3 };
 
 // One parsed block.  Offsets are block-relative (u16: the block is <= 32 KiB,
 // user-key bytes <= kKeyCap).
@@ -647,7 +641,6 @@ __device__ __forceinline__ void parse_block(Meta& M, uint4* X, const Args& A) {
       if (l < 5) M.vp[nkv + l] = tvb;
       if (l == 0) M.kout[nkv] = uint16_t(tkb);
       wave_sync();
-#if !PBL_PIPE_LANE
       // output buckets: the KV holding byte q*128 of the block's keys / values
       for (uint32_t j = l; j < nkv; j += kWave) {
         const uint32_t k0 = M.kout[j], k1 = M.kout[j + 1];
@@ -655,7 +648,6 @@ __device__ __forceinline__ void parse_block(Meta& M, uint4* X, const Args& A) {
         const uint32_t v0 = vout_of(M, j), v1 = vout_of(M, j + 1);
         for (uint32_t q = (v0 + 127) >> kBs; (q << kBs) < v1; q++) M.vbkt[q] = uint16_t(j);
       }
-#endif
     }
   }
 
@@ -667,22 +659,6 @@ __device__ __forceinline__ void parse_block(Meta& M, uint4* X, const Args& A) {
   const uint64_t agg[kNumComp] = {okb ? nkv : 0, okb ? tkb : 0, okb ? tvb : 0, okb ? nres : 0};
   if (!published) lb_publish(lb_state, nb, b, agg);
   PSTAMP(A, b, 3, l == 0);
-#if PBL_PIPE_LANE
-  // the emit waves resolve this block's prefix next iteration (its
-  // predecessors published at least an iteration earlier by then)
-  if (l == 0) {
-    M.kout[nkv] = uint16_t(tkb);  // (also the lone N+1 offset of a block with no entries)
-    M.vp[nkv] = tvb;
-    M.status = status;
-    M.mode = kModeResolve;
-    M.nkv = nkv;
-    M.nres = okb ? nres : 0;
-    M.roff = roff;
-    M.tot_kb = tkb;
-    M.tot_vb = tvb;
-  }
-  return;
-#endif
   // resolve this block's exclusive prefix now: the parse wave has slack, the
   // emit waves then start on their stores at once next iteration
   uint64_t excl[kNumComp];
@@ -949,137 +925,6 @@ __device__ __forceinline__ void emit_write(const Meta& M, const uint4* X, const 
 #endif
 }
 
-// Lane-per-KV emit (PBL_PIPE_LANE): every emit wave resolves the block's
-// exclusive prefix itself (its predecessors published at least an iteration
-// ago: normally one round trip, no waiting; the same prefix is stored by each,
-// harmlessly), wave 1 writes the block metadata, then the 192 emit lanes take
-// a KV each: trailer, flags, offsets, the user key as 16-B chunks merged from
-// its prefix chain, the value as 16-B chunks straight from the stage, plain
-// (unaligned) global stores exact at every tail.  Values longer than
-// kLaneLong are copied by their emit wave, 16 B per lane per step.
-#ifndef PBL_LANE_LONG
-#define PBL_LANE_LONG 256
-#endif
-typedef u32x4 u32x4_ug __attribute__((aligned(1)));
-typedef uint32_t u32_ug __attribute__((aligned(1)));
-typedef uint64_t u64_ug __attribute__((aligned(1)));
-typedef uint16_t u16_ug __attribute__((aligned(1)));
-
-// Bytes [0, n) of w (n <= 16) to p, any alignment (nothing past n).
-__device__ __forceinline__ void store_n(gptr<uint8_t> p, const uint4& w, uint32_t n) {
-  if (n == 16) {
-    *(gptr<u32x4_ug>)p = u32x4{w.x, w.y, w.z, w.w};
-    return;
-  }
-  uint64_t lo = uint64_t(w.x) | uint64_t(w.y) << 32, hi = uint64_t(w.z) | uint64_t(w.w) << 32;
-  uint32_t o = 0;
-  if (n & 8) {
-    *(gptr<u64_ug>)p = lo;
-    lo = hi;
-    o = 8;
-  }
-  if (n & 4) {
-    *(gptr<u32_ug>)(p + o) = uint32_t(lo);
-    lo >>= 32;
-    o += 4;
-  }
-  if (n & 2) {
-    *(gptr<u16_ug>)(p + o) = uint16_t(lo);
-    lo >>= 16;
-    o += 2;
-  }
-  if (n & 1) *(p + o) = uint8_t(lo);
-}
-
-template <class F>
-__device__ __forceinline__ void emit_lane(const Meta& M, const uint4* X, const Args& A, const F& mid) {
-  const int tb = int(threadIdx.x) - kWave;
-  const int l = lane_id();
-  const uint32_t b = M.b, flags = A.in.flags, nb = A.in.n_blocks;
-  const pbl_decode_out& O = A.out;
-  const uint32_t nkv = M.nkv, nres = M.nres, roff = M.roff;
-  uint32_t status = M.status;
-  const bool okb = status == PBL_OK;
-  const uint64_t agg[kNumComp] = {okb ? nkv : 0, okb ? M.tot_kb : 0, okb ? M.tot_vb : 0, okb ? nres : 0};
-  uint8_t* ws = reinterpret_cast<uint8_t*>(A.out.workspace);
-  uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
-  uint64_t excl[kNumComp];
-  PSTAMP(A, b, 5, tb == 0);
-  lb_resolve<kLbWin>(lb_state, nb, b, agg, excl, &A.out.totals->status_mask);
-  PSTAMP(A, b, 6, tb == 0);
-  if (okb && overflows(O, excl, agg)) status = PBL_OVERFLOW;
-  if (tb == 0) {
-    if (status != PBL_OK && O.key_off && excl[0] + b < O.kv_cap + nb) {
-      to_glb(O.key_off)[excl[0] + b] = 0;
-      to_glb(O.val_off)[excl[0] + b] = 0;
-    }
-    write_block_meta(O, b, nb, status, excl, agg, false);
-  }
-  mid();  // the next block's loads go out first: the emit below waits on nothing global
-  if (status != PBL_OK) return;
-  const View V = lds_view(X, uint32_t(kPad + (M.boff & 15)));
-  const uint64_t kvb = excl[0], kbb = excl[1], vbb = excl[2], rbb = excl[3];
-  const gptr<uint8_t> kbytes = to_glb(O.key_bytes) + kbb, vbytes = to_glb(O.val_bytes) + vbb;
-  const bool raw = (flags & PBL_ROW_RAW_KEYS) != 0;
-  for (uint32_t j0 = 0; j0 <= nkv; j0 += kEmit) {
-    const uint32_t j = j0 + uint32_t(tb);
-    uint32_t vlen = 0, vsrc = 0, vo = 0;
-    if (j <= nkv) {
-      const uint32_t ko = M.kout[j];
-      vo = vout_of(M, j);
-      to_glb(O.key_off)[kvb + b + j] = ko;
-      to_glb(O.val_off)[kvb + b + j] = vo;
-      if (j < nkv) {
-        vsrc = vsrc_of(M, j);
-        vlen = vout_of(M, j + 1) - vo;
-        // value: 16-B chunks straight from the stage (long ones by the wave below)
-        if (vlen <= uint32_t(PBL_LANE_LONG)) {
-          const uint32_t nf = vlen & ~15u;
-          for (uint32_t c = 0; c < nf; c += 64) {
-            uint4 x[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-              if (c + 16 * u < nf) x[u] = V.ld16(int32_t(vsrc + c + 16 * u));
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-              if (c + 16 * u < nf)
-                *(gptr<u32x4_ug>)(vbytes + vo + c + 16 * u) = u32x4{x[u].x, x[u].y, x[u].z, x[u].w};
-          }
-          if (vlen & 15u) store_n(vbytes + vo + nf, V.ld16(int32_t(vsrc + nf)), vlen & 15u);
-        }
-        uint8_t fl = M.kvf[j];
-        to_glb(O.trailer)[kvb + j] = with_seq(mtrailer(M, V, int(j), &fl, flags), A.in.synthetic_seq_num, flags);
-        if (O.kv_flags) to_glb(O.kv_flags)[kvb + j] = fl;
-        if (O.entry_off) to_glb(O.entry_off)[kvb + j] = M.eoff[j];
-        // user key: 16-B chunks of its prefix chain
-        const uint32_t kl = M.klen[j];
-        const uint32_t ukl = raw ? kl : (kl >= 8 ? kl - 8 : 0u);
-        for (uint32_t c = 0; c < ukl; c += 16) {
-          const uint32_t n = ukl - c < 16 ? ukl - c : 16u;
-          uint4 w = make_uint4(0, 0, 0, 0);
-          mkey_part(w, M, V, int(j), ukl, c, c + n, 0);
-          store_n(kbytes + ko + c, w, n);
-        }
-      }
-    }
-    // long values: this wave, 16 B per lane per step
-    for (uint64_t lm = __ballot(j < nkv && vlen > uint32_t(PBL_LANE_LONG)); lm; lm &= lm - 1) {
-      const int s = __builtin_ctzll(lm);
-      const uint32_t ls = __shfl(vsrc, s, kWave), ll = __shfl(vlen, s, kWave), lo = __shfl(vo, s, kWave);
-      for (uint32_t c = 16u * l; c < ll; c += 16u * kWave) {
-        const uint32_t n = ll - c < 16 ? ll - c : 16u;
-        store_n(vbytes + lo + c, V.ld16(int32_t(ls + c)), n);
-      }
-    }
-  }
-  if (O.restarts)
-    for (uint32_t r = uint32_t(tb); r < nres; r += kEmit) to_glb(O.restarts)[rbb + r] = V.le32(roff + 4 * r);
-  PSTAMP(A, b, 8, tb == 0);
-#ifdef PBL_STAMPS
-  PSTAMP(A, b, 9 + (tb >> 6), (tb & 63) == 0);
-#endif
-}
-
 // The next block, held in registers by the emit waves between their loads
 // (after the emit stores) and the store to LDS after the iteration's first
 // barrier: kPfE granules per emit lane.
@@ -1222,14 +1067,8 @@ __device__ __forceinline__ void row_pipe_body(PLds& S, const Args& A, const Q& Q
       auto pf_issue = [&]() {
         if (pf_on) pf.load(A.in.blocks, nx_off, nx_len);
       };
-#if PBL_PIPE_LANE
-      if (prv.mode == kModeResolve) emit_lane(prv, S.x[(i + 1) & 1], A, pf_issue);
-      else pf_issue();
-      (void)excl;
-#else
       if (emit_resolve(prv, A, excl)) emit_write(prv, S.x[(i + 1) & 1], A, excl, pf_issue);
       else pf_issue();
-#endif
 #endif
     }
     __syncthreads();

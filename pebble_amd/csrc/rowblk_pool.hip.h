@@ -51,6 +51,9 @@ namespace pool {
 #ifndef PBL_POOL_VU
 #define PBL_POOL_VU 2
 #endif
+#ifndef PBL_POOL_PRIO
+#define PBL_POOL_PRIO 2  // the stage holder's issue priority (values run at 0)
+#endif
 constexpr int kNW = PBL_POOL_WAVES;      // waves per workgroup (one workgroup per CU)
 constexpr int kNS = PBL_POOL_STAGES;     // staging buffers per workgroup
 constexpr int kTPBP = kNW * kWave;
@@ -409,6 +412,10 @@ __device__ __forceinline__ uint32_t acquire(PoolLds& L) {
       }
     }
   }
+  // the stage holder's work (staging, walk, metadata, look-back, keys) gates
+  // every wave waiting for a stage: it wins issue arbitration against the
+  // waves copying values
+  if (PBL_POOL_PRIO) __builtin_amdgcn_s_setprio(PBL_POOL_PRIO);
   return __builtin_amdgcn_readfirstlane(__shfl(s, 0, kWave));
 }
 
@@ -417,6 +424,7 @@ __device__ __forceinline__ void release(PoolLds& L, uint32_t s) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   wave_sync();
   if (lane_id() == 0) __hip_atomic_fetch_or(&L.free_mask, 1u << s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (PBL_POOL_PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
 // General path for one block (wave-serial Iter.Next) on the staged block, the
@@ -661,6 +669,9 @@ __global__ void __launch_bounds__(kTPBP, 1) rowblk_pool_kernel(Args A) {
   const uint32_t nb = A.in.n_blocks;
   uint32_t* tick = reinterpret_cast<uint32_t*>(A.out.workspace);
   for (;;) {
+#ifdef PBL_STAMPS
+    const uint64_t t_acq = __builtin_amdgcn_s_memtime();
+#endif
     const uint32_t s = acquire(L);
     uint32_t t0 = 0;
     if (lane_id() == 0) t0 = g_atomic_add(tick, 1u);
@@ -670,6 +681,10 @@ __global__ void __launch_bounds__(kTPBP, 1) rowblk_pool_kernel(Args A) {
       break;
     }
     PSTAMP(A, t0, 0, lane_id() == 0);
+#ifdef PBL_STAMPS
+    if (lane_id() == 0)
+      reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(A.out.workspace) + ws_bytes(nb))[uint64_t(t0) * 16 + 8] = t_acq;
+#endif
     pool_block(L, s, W, A, t0);
   }
 }

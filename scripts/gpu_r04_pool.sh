@@ -10,3 +10,4 @@ $B --kernel pipe > $O/bench_pipe.json 2>$O/bench_pipe.err && echo pipe ok && \
 $B --kernel pool > $O/bench_pool.json 2>$O/bench_pool.err && echo pool ok && \
 PBL_LIB=exp/pool_w12.so $B --kernel pool > $O/bench_pool_w12.json 2>$O/bench_pool_w12.err && echo w12 ok
 for f in $O/bench_*.json; do python -c "import json,sys; d=json.load(open('$f')); print('$f', d['value'], d['roofline']['kernel_ms'], d['roofline']['frac'])"; done
+[ -f exp/pool_diag.so ] && PBL_LIB=exp/pool_diag.so timeout -k 10 200 python scripts/pool_stamps.py > $O/pool_stamps.txt 2>&1 && cat $O/pool_stamps.txt

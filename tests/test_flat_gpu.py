@@ -1,5 +1,5 @@
 """The one-wave-per-block row kernels (rowblk_flat.hip.h, batch flag
-PBL_KERNEL_FLAT; rowblk_run.hip.h, PBL_KERNEL_RUN) against the oracle: bit-exact on every output array, over the
+PBL_KERNEL_FLAT; rowblk_pool.hip.h, PBL_KERNEL_POOL; rowblk_global.hip.h, PBL_KERNEL_GLOBAL) against the oracle: bit-exact on every output array, over the
 same inputs as the pipeline's parity tests (reference blocks, synthetic
 configs, random and fuzzed blocks, value prefixes, blocks past the LDS limits,
 the general-path fallbacks)."""
@@ -15,7 +15,7 @@ from pebble_amd.rowblk import Writer, gen_row_blocks
 from test_rowblk_gpu import GOLDEN, assert_same, pack, random_block
 
 pytestmark = pytest.mark.gpu
-KERNELS = {"flat": N.PBL_KERNEL_FLAT, "run": N.PBL_KERNEL_RUN, "global": N.PBL_KERNEL_GLOBAL, "pool": N.PBL_KERNEL_POOL}
+KERNELS = {"flat": N.PBL_KERNEL_FLAT, "global": N.PBL_KERNEL_GLOBAL, "pool": N.PBL_KERNEL_POOL}
 FLAT = N.PBL_KERNEL_FLAT
 
 
