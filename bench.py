@@ -45,7 +45,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", choices=["row", "col", "mixed", "zipf", "transform", "cfg1"], default="row")
+    p.add_argument("--workload", choices=["row", "col", "mixed", "zipf", "rowmix", "transform", "cfg1"], default="row")
+    p.add_argument("--mix", choices=["zipf10", "tail8"], default="zipf10",
+                   help="rowmix: config-2 blocks with every 10th a Zipf block, or every 8th a short tail block")
     p.add_argument("--blocks", type=int, default=0, help="blocks per GPU (0 = the workload's config)")
     p.add_argument("--block-size", type=int, default=32768)
     p.add_argument("--restart-interval", type=int, default=16)
@@ -259,6 +261,17 @@ def main():
         wl = ("transform pass (SyntheticSeqNum, HideObsoletePoints, 12 B SyntheticPrefix) over " if a.workload ==
               "transform" else "") + (f"config2: {nb} x {a.block_size // 1024} KiB row-format blocks per GPU, restart interval "
               f"{a.restart_interval}, {a.key_len} B keys / {a.val_len} B values" + (", value prefix" if a.value_prefix else ""))
+    elif a.workload == "rowmix":
+        from pebble_amd.batch import gen_row_mix, varlen_hint
+        fmt = N.PBL_FMT_ROW
+        buf, off, lens, n_kv = gen_row_mix(seed, nb, a.mix, n_threads=16)
+        vl = varlen_hint(lens) and a.kernel == "auto"
+        kernel = ("glb_sizes_kernel+glb_scan_kernel+glb_values_kernel" if a.kernel == "global" or vl else
+                  {"single": "rowblk_decode_kernel", "flat": "rowblk_flat_kernel", "pool": "rowblk_pool_kernel"}.get(
+                      a.kernel, "rowblk_pipe_kernel"))
+        wl = (f"row-shape mix: {nb} row blocks per GPU, config-2 blocks with " +
+              ("every 10th a config-5 Zipf block (restart interval 16)" if a.mix == "zipf10" else
+               "every 8th a short table-tail block (2 / 4 / 8 KiB)"))
     elif a.workload == "col":
         fmt = N.PBL_FMT_COL_CRDB1
         buf, off, lens, n_kv = gen_col_blocks(seed, nb, a.block_size, n_threads=16)
@@ -391,7 +404,8 @@ def main():
         ab = alg_bytes(h_in, nb, 0) + alg_bytes(hres, nb, 0) - 24 * nb
     achieved = ab / (kern_ms * 1e-3) / 1e9
     traffic = None
-    tname = ("pmc_traffic.json" if a.workload == "row" else
+    tname = ("pmc_traffic.json" if a.workload == "row" and a.kernel == "auto" else
+             f"pmc_traffic_{a.kernel}.json" if a.workload == "row" else
              f"pmc_traffic_zipf_ri{a.restart_interval}.json" if a.workload == "zipf" and a.zipf_format == "row" else
              f"pmc_traffic_{a.workload}.json")
     tp = os.path.join(ROOT, "profiles", tname)
@@ -401,8 +415,9 @@ def main():
                 pt = json.load(f)
             same_zipf = a.workload != "zipf" or (pt.get("restart_interval") == a.restart_interval
                                                   and pt.get("zipf_format") == a.zipf_format)
+            # the PMC of THIS decode's kernels only (a file names the kernel(s) it measured)
             if (pt.get("workload_blocks") == nb and pt.get("block_size") == a.block_size
-                    and pt.get("workload", "row") == a.workload and same_zipf):
+                    and pt.get("workload", "row") == a.workload and same_zipf and pt.get("kernel") == kernel):
                 traffic = pt.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None

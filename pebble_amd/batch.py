@@ -303,3 +303,50 @@ def gen_zipf_blocks(seed: int, n_blocks: int, fmt: int = 0, restart_interval: in
     buf = buf[: used.value + 16].copy()
     buf[used.value:] = 0
     return buf, off, lens, int(n)
+
+
+def gen_row_mix(seed: int, n_blocks: int, kind: str = "zipf10", n_threads: int = 0):
+    """Row batches whose block shapes vary inside one batch (the shapes a
+    compaction or a multi-table read hands over), for the per-block kernel
+    routing: "zipf10" = config-2 blocks with every 10th block a config-5 Zipf
+    block (restart interval 16); "tail8" = config-2 blocks with every 8th block
+    a table's short last block (2, 4 or 8 KiB, the same 16 B / 100 B KVs).
+    Blocks packed at 8-B aligned offsets.  Returns (buf, off, lens, n_kv)."""
+    from .rowblk import gen_row_blocks
+    ids = np.arange(n_blocks)
+    if kind == "zipf10":
+        odd = ids % 10 == 9
+        a_buf, a_off, a_len, a_n = gen_row_blocks(seed, int((~odd).sum()), 32768, 16, 16, 100, n_threads=n_threads)
+        b_buf, b_off, b_len, b_n = gen_zipf_blocks(seed + 1, int(odd.sum()), N.PBL_FMT_ROW, 16, 32768,
+                                                   n_threads=n_threads)
+        parts = [(a_buf, a_off, a_len), (b_buf, b_off, b_len)]
+        src = np.where(odd, 1, 0)
+        n_kv = a_n + b_n
+    elif kind == "tail8":
+        odd = ids % 8 == 7
+        a_buf, a_off, a_len, a_n = gen_row_blocks(seed, int((~odd).sum()), 32768, 16, 16, 100, n_threads=n_threads)
+        parts, n_kv = [(a_buf, a_off, a_len)], a_n
+        src = np.zeros(n_blocks, np.int64)
+        tails = np.nonzero(odd)[0]
+        for k, bs in enumerate((2048, 4096, 8192)):
+            sel = tails[k::3]
+            t_buf, t_off, t_len, t_n = gen_row_blocks(seed + 1 + k, len(sel), bs, 16, 16, 100, n_threads=n_threads)
+            parts.append((t_buf, t_off, t_len))
+            src[sel] = 1 + k
+            n_kv += t_n
+    else:
+        raise ValueError(kind)
+    # the i-th block of each part, in batch order
+    nth = np.zeros(n_blocks, np.int64)
+    for p in range(len(parts)):
+        m = src == p
+        nth[m] = np.arange(int(m.sum()))
+    lens = np.array([parts[p][2][i] for p, i in zip(src, nth)], np.uint32)
+    slot = (lens.astype(np.uint64) + 7) // 8 * 8
+    off = np.concatenate([[0], np.cumsum(slot)[:-1]]).astype(np.uint64)
+    buf = np.zeros(int(slot.sum()) + 16, np.uint8)
+    for b in range(n_blocks):
+        pb, po, _ = parts[src[b]]
+        o = int(po[nth[b]])
+        buf[int(off[b]): int(off[b]) + int(lens[b])] = pb[o: o + int(lens[b])]
+    return buf, off, lens, int(n_kv)

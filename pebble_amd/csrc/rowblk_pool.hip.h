@@ -51,6 +51,9 @@ namespace pool {
 #ifndef PBL_POOL_VU
 #define PBL_POOL_VU 2
 #endif
+#ifndef PBL_POOL_VCOPY
+#define PBL_POOL_VCOPY 2  // value copy: 1 = 16-B output granules (bucket + window), 2 = 8 lanes per KV
+#endif
 #ifndef PBL_POOL_PRIO
 #define PBL_POOL_PRIO 2  // the stage holder's issue priority (values run at 0)
 #endif
@@ -393,6 +396,70 @@ __device__ __forceinline__ void copy_values(const Slot& W, gptr<const uint8_t> g
   }
 }
 
+// Value bytes of a block, 8 lanes per KV (PBL_POOL_VCOPY 2): lane c of a
+// group copies its value's 16-B chunks c, c + 8, ... from the block in global
+// memory to the output with plain (unaligned) 16-B loads and stores.  A
+// value's last chunk is the one that ENDS at the value's end, overlapping the
+// chunk before it, so every store writes bytes of its own value only and no
+// store is partial.  Two KVs per group per step, their loads in flight
+// together.  Values shorter than 16 B go byte by byte; values longer than
+// kWaveVal are copied by the whole wave, 1 KiB per instruction.
+constexpr uint32_t kWaveVal = 1024;
+__device__ __forceinline__ void copy_values_grp(const Slot& W, gptr<const uint8_t> g, uint32_t nkv,
+                                                gptr<uint8_t> vbytes) {
+  const int l = lane_id();
+  const uint32_t c = uint32_t(l) & 7u;
+  for (uint32_t j0 = 0; j0 < nkv; j0 += 16) {
+    uint32_t vo[2], vl[2], vs[2];
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      const uint32_t j = j0 + 8 * u + (uint32_t(l) >> 3);
+      const uint32_t a = j < nkv ? W.vp[j] : 0u, z = j < nkv ? W.vp[j + 1] : 0u;
+      vo[u] = a & 0xffffu;
+      vl[u] = (z & 0xffffu) - vo[u];
+      vs[u] = a >> 16;
+    }
+    uint4 x[2];
+    uint32_t oo[2];
+    bool has[2];
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      has[u] = vl[u] >= 16 && vl[u] <= kWaveVal && 16 * c < vl[u];
+      oo[u] = 16 * c < vl[u] - 16 ? 16 * c : vl[u] - 16;
+      if (has[u]) {
+        const u32x4 v = *(gptr<const u32x4_ug>)(g + vs[u] + oo[u]);
+        x[u] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; u++)
+      if (has[u]) *(gptr<u32x4_ug>)(vbytes + vo[u] + oo[u]) = u32x4{x[u].x, x[u].y, x[u].z, x[u].w};
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      if (vl[u] > 128 && vl[u] <= kWaveVal) {
+        for (uint32_t o = 16 * c + 128; o < vl[u]; o += 128) {
+          const uint32_t q = o < vl[u] - 16 ? o : vl[u] - 16;
+          *(gptr<u32x4_ug>)(vbytes + vo[u] + q) = *(gptr<const u32x4_ug>)(g + vs[u] + q);
+        }
+      } else if (vl[u] < 16) {
+        for (uint32_t o = c; o < vl[u]; o += 8) vbytes[vo[u] + o] = g[vs[u] + o];
+      }
+    }
+    // long values: the whole wave, 16 B per lane per step
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      for (uint64_t lm = __ballot(c == 0 && vl[u] > kWaveVal); lm; lm &= lm - 1) {
+        const int sl = __builtin_ctzll(lm);
+        const uint32_t ls = __shfl(vs[u], sl, kWave), ll = __shfl(vl[u], sl, kWave), lo = __shfl(vo[u], sl, kWave);
+        for (uint32_t o = 16u * l; o < ll; o += 16u * kWave) {
+          const uint32_t q = o < ll - 16 ? o : ll - 16;
+          *(gptr<u32x4_ug>)(vbytes + lo + q) = *(gptr<const u32x4_ug>)(g + ls + q);
+        }
+      }
+    }
+  }
+}
+
 // Take a free stage (lane 0 spins on the workgroup's mask); returns its index.
 __device__ __forceinline__ uint32_t acquire(PoolLds& L) {
   uint32_t s = 0;
@@ -579,12 +646,14 @@ __device__ __forceinline__ void pool_block(PoolLds& L, uint32_t s, Slot& W, cons
       if (l < 5) W.vp[nkv + l] = tvb;
       if (l == 0) S.kout[nkv] = uint16_t(tkb);
       wave_sync();
+#if PBL_POOL_VCOPY != 2
       // value buckets: the KV holding byte q * 128 of the block's values
       for (uint32_t j = l; j < nkv; j += kWave) {
         const uint32_t v0 = W.vp[j] & 0xffffu, v1 = W.vp[j + 1] & 0xffffu;
         for (uint32_t q = (v0 + 127) >> kVB; (q << kVB) < v1; q++) W.vbkt[q] = uint16_t(j);
       }
       wave_sync();
+#endif
       PSTAMP(A, b, 4, l == 0);
     }
   }
@@ -651,7 +720,11 @@ __device__ __forceinline__ void pool_block(PoolLds& L, uint32_t s, Slot& W, cons
   PSTAMP(A, b, 6, l == 0);
 
   // ---- values, global -> global --------------------------------------------
+#if PBL_POOL_VCOPY == 2
+  if (tvb) copy_values_grp(W, to_glb(gblk), nkv, to_glb(O.val_bytes) + vbb);
+#else
   if (tvb) copy_values(W, to_glb(gblk), blen, vbb, tvb, to_glb(O.val_bytes));
+#endif
   PSTAMP(A, b, 7, l == 0);
   wave_sync();  // (the slot is the next block's)
 }

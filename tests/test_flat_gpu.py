@@ -101,3 +101,16 @@ def test_flat_config2_full_size_sha(kern):
               "blk_kv_base", "blk_key_base", "blk_val_base", "blk_rst_base", "blk_status"):
         assert hashlib.sha256(gp[k].tobytes()).digest() == hashlib.sha256(gf[k].tobytes()).digest(), k
     assert gf["n_kv"] == n
+
+
+@pytest.mark.parametrize("mix", ["zipf10", "tail8"])
+def test_row_shape_mixes(mix, kern):
+    """Batches whose block shapes vary inside the batch (config-2 blocks with
+    Zipf blocks or short table-tail blocks interleaved), on every row kernel
+    and on the default routing."""
+    from pebble_amd.batch import gen_row_mix
+    buf, off, lens, n = gen_row_mix(77, 600, mix)
+    g = check(buf, off, lens, 0, f"mix={mix}", kern)
+    assert g["n_kv"] == n and g["status_mask"] == 0
+    g0 = check(buf, off, lens, 0, f"mix={mix} default", 0)
+    assert g0["n_kv"] == n
