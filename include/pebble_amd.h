@@ -77,6 +77,15 @@ enum {
 #define PBL_ROW_RAW_KEYS 0x4u     /* rowblk.RawIter semantics (rowblk_iter.go:1743-1794):
                                      keys are emitted whole, no trailer split, no
                                      first-key check; trailer[] = 0              */
+#define PBL_ROW_HIDE_OBSOLETE 0x8u /* blockiter.Transforms.HideObsoletePoints fused into
+                                     the decode (rowblk_iter.go:1168-1179; colblk
+                                     data_block.go:1680-1697): KVs whose trailer has
+                                     the obsolete bit (row) or whose isObsolete bit
+                                     is set (colblk) are not emitted; every count and
+                                     offset covers the visible KVs only, restart
+                                     words are kept.  Ignored with PBL_ROW_RAW_KEYS.
+                                     (The name is historical: it applies to colblk
+                                     batches too.)                                  */
 #define PBL_BATCH_VARLEN 0x100u   /* scheduling hint, no effect on results: block
                                      lengths vary widely (e.g. Zipf value sizes), so a
                                      colblk batch takes the one-block-per-workgroup

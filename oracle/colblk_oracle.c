@@ -388,6 +388,11 @@ uint64_t orc_colblk_scan_checksum(const uint8_t* blk, uint64_t len, uint32_t sch
 }
 
 static int decode_block(const uint8_t* blk, uint64_t len, uint32_t fmt, uint32_t flags, orc_block_out* o) {
+  if (fmt == FMT_ROW && (flags & FLAG_HIDE_OBSOLETE) && !(flags & FLAG_RAW_KEYS)) {
+    /* HideObsoletePoints: rowblk.Iter under blockiter.Transforms{HideObsoletePoints} */
+    const orc_transforms t = {0, 1, 0, NULL, 0, NULL, 0};
+    return orc_rowblk_decode_tf(blk, len, flags & ~FLAG_HIDE_OBSOLETE, &t, o);
+  }
   if (fmt == FMT_ROW) return orc_rowblk_decode(blk, len, flags, o);
   return orc_colblk_decode(blk, len, fmt, o);
 }

@@ -14,6 +14,7 @@ enum { FMT_ROW = 0, FMT_COL_DEFAULT = 1, FMT_COL_CRDB1 = 2 };
 #define FLAG_VALUE_PREFIX 0x1u
 #define FLAG_NO_VALUER 0x2u
 #define FLAG_RAW_KEYS 0x4u /* rowblk.RawIter (rowblk_iter.go:1743-1794) */
+#define FLAG_HIDE_OBSOLETE 0x8u /* blockiter.Transforms.HideObsoletePoints during the decode */
 
 #define KV_RESTART 0x01u
 #define KV_RESTART_SAMEPFX 0x02u

@@ -52,6 +52,7 @@ PBL_ROW_VALUE_PREFIX = 0x1
 PBL_ROW_NO_VALUER = 0x2
 PBL_ROW_RAW_KEYS = 0x4
 PBL_BATCH_VARLEN = 0x100
+PBL_ROW_HIDE_OBSOLETE = 0x8
 PBL_KERNEL_SINGLE = 0x200
 PBL_KERNEL_PIPE = 0x400
 PBL_KERNEL_FLAT = 0x800

@@ -28,6 +28,7 @@ colblk_decode_kernel(Args A) {
 // and the totals are cleared, for a batch whose blocks are all colblk.
 extern "C" int pbl_decode_batch_colblk(const pbl_block_batch* batch, pbl_decode_out* out, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (batch->flags & PBL_ROW_HIDE_OBSOLETE) return PBL_UNSUPPORTED;  // (fused for row batches only, so far)
   if (hipMemsetAsync(out->workspace, 0, pbl::ws_bytes(batch->n_blocks), st) != hipSuccess)
     return PBL_DEVICE_ERROR;
   pbl::Args a;

@@ -1103,17 +1103,32 @@ int launch_row_flat(const pbl::Args& a, hipStream_t st, bool values) {
 // big-block passes around it.
 int launch_row_pool(const pbl::Args& a, hipStream_t st, bool values) {
   const uint32_t nb = a.in.n_blocks;
+  const bool hide = (a.in.flags & PBL_ROW_HIDE_OBSOLETE) && !(a.in.flags & PBL_ROW_RAW_KEYS);
+  const void* fn = hide ? reinterpret_cast<const void*>(pbl::row::pool::rowblk_pool_kernel<true>)
+                        : reinterpret_cast<const void*>(pbl::row::pool::rowblk_pool_kernel<false>);
   int cus = 0;
-  const uint64_t grid = pbl::persistent_grid(st, pbl::kKRowPool,
-                                             reinterpret_cast<const void*>(pbl::row::pool::rowblk_pool_kernel),
+  const uint64_t grid = pbl::persistent_grid(st, pbl::kKRowPool, fn,
                                              (uint64_t(nb) + pbl::row::pool::kNW - 1) / pbl::row::pool::kNW, &cus,
                                              pbl::row::pool::kTPBP);
   if (!grid) return PBL_DEVICE_ERROR;
   const uint32_t small = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4));
   hipLaunchKernelGGL(pbl::row::pipe::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
-  hipLaunchKernelGGL(pbl::row::pool::rowblk_pool_kernel, dim3(uint32_t(grid)), dim3(pbl::row::pool::kTPBP), 0, st, a);
+  if (hide)
+    hipLaunchKernelGGL(pbl::row::pool::rowblk_pool_kernel<true>, dim3(uint32_t(grid)), dim3(pbl::row::pool::kTPBP), 0,
+                       st, a);
+  else
+    hipLaunchKernelGGL(pbl::row::pool::rowblk_pool_kernel<false>, dim3(uint32_t(grid)), dim3(pbl::row::pool::kTPBP),
+                       0, st, a);
   if (values) hipLaunchKernelGGL(pbl::row::pipe::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
+}
+
+// HideObsoletePoints fused into the decode: the row staging-pool kernel (and
+// the general walk it hands blocks to) and the colblk kernels implement it;
+// other row kernels are A/B forms only, so such batches always take the pool.
+bool hide_row(const pbl_block_batch* b) {
+  return (b->flags & PBL_ROW_HIDE_OBSOLETE) && !(b->flags & PBL_ROW_RAW_KEYS) && !b->block_format &&
+         b->format == PBL_FMT_ROW;
 }
 
 // Row batches walked from HBM (rowblk_global.hip.h): sizes, the 32 KiB-key
@@ -1200,6 +1215,7 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
   a.in = *batch;
   a.out = *out;
   if (batch->block_format) {
+    if ((batch->flags & PBL_ROW_HIDE_OBSOLETE) && !(batch->flags & PBL_ROW_RAW_KEYS)) return PBL_UNSUPPORTED;
     const int rc = launch_mixed(batch, a, st, batch->flags & PBL_KERNEL_SINGLE, true);
     if (rc != PBL_OK) return rc;
   } else {
@@ -1207,6 +1223,7 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
     // blocks).  PBL_KERNEL_SINGLE selects the one-block-per-workgroup
     // persistent kernel (kept for A/B measurement); the default is the pipeline.
     const bool single = (batch->flags & PBL_KERNEL_SINGLE) != 0;
+    if (hide_row(batch)) return launch_row_pool(a, st, true);
     if (!single && use_global(batch->flags)) return launch_row_global(a, st, true);
     if (!single && (batch->flags & PBL_KERNEL_POOL)) return launch_row_pool(a, st, true);
     if (!single && use_flat(batch->flags)) return launch_row_flat(a, st, true);
@@ -1245,6 +1262,8 @@ int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stre
   if (!batch->blocks || !batch->block_off || !batch->block_len || !out->workspace ||
       out->workspace_bytes < pbl::ws_alloc_bytes(batch->n_blocks))
     return PBL_INVALID_ARG;
+  if (batch->block_format && (batch->flags & PBL_ROW_HIDE_OBSOLETE) && !(batch->flags & PBL_ROW_RAW_KEYS))
+    return PBL_UNSUPPORTED;
   // the decode with every per-KV pointer NULL and zero capacities: each block
   // takes its overflow branch (sizes computed and published, nothing written);
   // the fixup then reports the statuses the decode would have had
@@ -1271,6 +1290,9 @@ int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stre
     // pointers), minus the big-block value pass
     if (batch->block_format) {
       rc = launch_mixed(batch, a, st, batch->flags & PBL_KERNEL_SINGLE, false);
+      if (rc != PBL_OK) return rc;
+    } else if (hide_row(batch)) {
+      rc = launch_row_pool(a, st, false);
       if (rc != PBL_OK) return rc;
     } else if (use_global(batch->flags)) {
       rc = launch_row_global(a, st, false);

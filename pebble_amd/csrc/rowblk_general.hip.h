@@ -165,6 +165,13 @@ __device__ __forceinline__ void slow_walk_t(const Src S, uint64_t len, uint32_t 
       ukl = 0;
       fl |= PBL_KV_INVALID_KEY;
     }
+    // blockiter.Transforms.HideObsoletePoints: the entry is skipped before its
+    // value is looked at (rowblk_iter.go:1168-1179); its key still feeds the
+    // prefix compression of the entries after it
+    if ((flags & PBL_ROW_HIDE_OBSOLETE) && (fl & PBL_KV_OBSOLETE)) {
+      offset = int64_t(vp) + vlen;
+      continue;
+    }
     uint64_t v = vp, vl = vlen;
     if ((flags & PBL_ROW_VALUE_PREFIX) && !(flags & PBL_ROW_RAW_KEYS) && (trailer & 0xff) == 1) {
       if (vl == 0) { status = PBL_CORRUPT_BOUNDS; break; }

@@ -67,14 +67,15 @@ constexpr int kVBkt = kMaxFastLen >> kVB;
 constexpr int kVU = PBL_POOL_VU;         // value granules per lane per step
 
 // A stage: the block bytes and the per-KV metadata the key emit reads.
-// m0[j] = key source offset | shared << 16 | internal key length << 32 |
-// prefix parent << 48.
+// m0[e] = key source offset | shared << 16 | internal key length << 32 |
+// prefix parent << 48, for every entry e of the block.
 struct Stage {
   uint4 x[kLdsBlkBytes / 16];  // the block, byte i at kPad + (boff & 15) + i
   uint64_t m0[kPKv];
-  uint16_t kout[kPKv + 1];     // user-key output offsets (block relative)
-  uint16_t eoff[kPKv];         // entry offsets (KVEncoding.Offset)
-  uint8_t kvf[kPKv];           // PBL_KV_* (OBSOLETE is added at emit time)
+  uint16_t kout[kPKv + 1];     // user-key output offsets (block relative), by visible index
+  uint16_t eoff[kPKv];         // entry offsets (KVEncoding.Offset), by visible index
+  uint16_t ent[kPKv];          // the entry of visible KV v (PBL_ROW_HIDE_OBSOLETE batches)
+  uint8_t kvf[kPKv];           // PBL_KV_* (OBSOLETE is added at emit time), by visible index
 };
 // A wave's slot: what the value copy needs after the stage is released.
 struct Slot {
@@ -151,105 +152,233 @@ __device__ __forceinline__ uint4 gld16(gptr<const uint8_t> g, int32_t i, uint32_
   return SlowGlb{g, blen}.ld16(i);
 }
 
-// Per-KV metadata of the parked entries of one run at final indices (acc = the
-// run's bases): the prefix parent is the nearest earlier entry of the run with
-// a smaller shared length (all-nearest-smaller-values, amortised O(1); the
-// previous entry and its parent kept in registers).
-__device__ __forceinline__ void park_meta(Stage& S, Slot& W, const View& V, const pipe::RunBuf& B, uint32_t flags,
-                                          bool vprefix, pipe::RunAcc& acc, pipe::ParState& P) {
-  uint32_t j = acc.cnt, kb = acc.kb, vb = acc.vb;
-  uint32_t prev_sh = 0, pp = 0, ppsh = 0;
-#pragma unroll
-  for (int k = 0; k < pipe::kRunBuf; k++) {
-    if (uint32_t(k) < B.cnt) {
-      const uint32_t pos = B.ea[k] & 0xffffu, sh = B.ea[k] >> 16;
-      const uint32_t un = B.eb[k] & 0x3fffu, h = (B.eb[k] >> 14) & 7u, vl = B.eb[k] >> 17;
-      const uint32_t kl = sh + un;
-      uint32_t vs = pos + h + un, vlen = vl;
-      uint8_t fl = 0;
-      if (k == 0) fl = uint8_t(PBL_KV_RESTART | ((B.rw >> 31) ? PBL_KV_RESTART_SAMEPFX : 0));
-      if (!(flags & PBL_ROW_RAW_KEYS) && kl < 8) fl |= PBL_KV_INVALID_KEY;
-      if (vprefix && kl >= 8 && (V.byte(pos + h + (kl - 8 - sh)) & 0xBF) == 1) {
-        const uint32_t pre = V.byte(vs);
-        if ((pre & 0xC0) == 0 || (flags & PBL_ROW_NO_VALUER)) { vs++; vlen--; }
-        else if ((pre & 0xC0) == 0x80) fl |= PBL_KV_VALBLK_HANDLE;
-        else fl |= PBL_KV_BLOB_HANDLE;
-      }
-      uint32_t par = j, parsh = 0;
-      if (sh != 0) {
-        uint32_t c = j - 1, csh = prev_sh;
-        if (csh >= sh) { c = pp; csh = ppsh; }
-        while (csh >= sh) {
-          c = m_par(S.m0[c]);
-          csh = m_sh(S.m0[c]);
-        }
-        par = c;
-        parsh = csh;
-      }
-      S.m0[j] = uint64_t(pos + h) | uint64_t(sh) << 16 | uint64_t(kl) << 32 | uint64_t(par) << 48;
-      S.kout[j] = uint16_t(kb);
-      S.eoff[j] = uint16_t(pos);
-      S.kvf[j] = fl;
-      W.vp[j] = vb | (vs << 16);
-      prev_sh = sh;
-      pp = par;
-      ppsh = parsh;
-      kb += (flags & PBL_ROW_RAW_KEYS) ? kl : (kl >= 8 ? kl - 8 : 0);
-      vb += vlen;
-      j++;
-    }
+// ---- the walk: lane per restart run ------------------------------------------
+// Entries are indexed in block order (the prefix-parent chain runs over every
+// entry); outputs by visible index (HideObsoletePoints drops obsolete entries
+// from the outputs, never from the chain).  Without hiding the two agree.
+struct PAcc {
+  uint32_t ne, cnt, kb, vb;  // entries, visible KVs, their user-key / value bytes
+};
+constexpr int kRunBuf = 16;
+// One run's head, parked in registers by the walk for the metadata pass.
+struct PRun {
+  uint32_t ea[kRunBuf];  // entry offset | hidden << 15 | shared << 16 | SET-with-value-prefix << 31
+  uint32_t eb[kRunBuf];  // unshared | header length << 14 | value length << 17
+  uint32_t n, rw, pos, e0, prev_kl, prev_kind;  // parked entries; where a longer run continues
+};
+
+// Whether an entry is hidden (HideObsoletePoints: the trailer's kind byte has
+// the obsolete bit, rowblk_iter.go:1168-1179) and whether its value carries a
+// value prefix (kind SET, :1192-1199).  The kind byte sits at key byte kl - 8:
+// in the entry's unshared bytes, or inside the shared prefix, where it is the
+// previous key's kind byte if that key has the same length.  Returns false
+// when the byte is elsewhere (the general walk takes the block).
+template <bool kHide>
+__device__ __forceinline__ bool entry_class(const View& V, uint32_t pos, uint32_t h, uint32_t sh, uint32_t kl,
+                                            uint32_t k, uint32_t prev_kl, uint32_t& prev_kind, uint32_t flags,
+                                            bool vprefix, bool& hidden, bool& setv) {
+  hidden = false;
+  setv = false;
+  if ((kHide || vprefix) && kl >= 8 && !(flags & PBL_ROW_RAW_KEYS)) {
+    uint32_t kind;
+    if (kl - 8 >= sh) kind = V.byte(pos + h + (kl - 8 - sh));
+    else if (k > 0 && prev_kl == kl) kind = prev_kind;
+    else return false;
+    hidden = kHide && (kind & 64u);
+    setv = vprefix && !hidden && (kind & 0xBFu) == 1;
+    prev_kind = kind;
   }
-  acc = pipe::RunAcc{j, kb, vb};
-  P = pipe::ParState{prev_sh, pp, ppsh};
+  return true;
 }
 
-// Per-KV metadata of entries [pos, e0) of a run, re-read from the stage
-// (`first` = pos is the restart point; P = the chain state before pos).
-__device__ __forceinline__ void span_meta(Stage& S, Slot& W, const View& V, uint32_t pos, uint32_t e0, uint32_t rw,
-                                          bool first, pipe::ParState P, uint32_t flags, bool vprefix,
-                                          pipe::RunAcc& acc) {
-  uint32_t j = acc.cnt, kb = acc.kb, vb = acc.vb;
-  uint32_t prev_sh = P.prev_sh, pp = P.pp, ppsh = P.ppsh;
+__device__ __forceinline__ uint32_t ukey_len(uint32_t kl, uint32_t flags) {
+  return (flags & PBL_ROW_RAW_KEYS) ? kl : (kl >= 8 ? kl - 8 : 0);
+}
+
+// Count entries [pos, e0) of a run whose first k entries were already counted
+// (prev_kl / prev_kind: the last one's).  `ok` clears where the run is not
+// walkable per run, `bad` sets on shared > len(previous key) (rowblk_iter.go:
+// 403), `vbad` on a visible SET value without its prefix byte.
+template <bool kHide>
+__device__ __forceinline__ void count_span(const View& V, uint32_t pos, uint32_t e0, uint32_t k, uint32_t prev_kl,
+                                           uint32_t prev_kind, uint32_t flags, bool vprefix, PAcc& acc, bool& ok,
+                                           bool& bad, bool& vbad) {
   while (pos < e0) {
     uint32_t sh, un, vl, h;
-    pipe::hdr2(V.ld8(pos), &sh, &un, &vl, &h);
+    const bool hok = pipe::hdr2(V.ld8(pos), &sh, &un, &vl, &h);
+    const uint32_t np = pos + h + un + vl;  // < 2^23: no overflow
+    if (!hok || (k == 0 && sh != 0) || np > e0) { ok = false; return; }
+    bad = bad || (k > 0 && sh > prev_kl);
     const uint32_t kl = sh + un;
+    bool hidden, setv;
+    if (!entry_class<kHide>(V, pos, h, sh, kl, k, prev_kl, prev_kind, flags, vprefix, hidden, setv)) {
+      ok = false;
+      return;
+    }
+    uint32_t vlen = vl;
+    if (setv) {
+      if (vl == 0) vbad = true;
+      else if ((V.byte(pos + h + un) & 0xC0) == 0 || (flags & PBL_ROW_NO_VALUER)) vlen--;
+    }
+    acc.ne++;
+    if (!hidden) {
+      acc.cnt++;
+      acc.kb += ukey_len(kl, flags);
+      acc.vb += vlen;
+    }
+    k++;
+    prev_kl = kl;
+    pos = np;
+  }
+}
+
+__device__ __forceinline__ bool run_bounds(const View& V, uint32_t r, uint32_t nres, uint32_t roff, uint32_t* rw,
+                                           uint32_t* e0) {
+  const uint32_t st = roff + 4 * r;
+  *rw = V.le32(st);
+  const uint32_t s0 = *rw & kRestartMask;
+  *e0 = (r + 1 < nres) ? (V.le32(st + 4) & kRestartMask) : roff;
+  return (r != 0 || s0 == 0) && s0 < *e0 && *e0 <= roff;
+}
+
+// Walk run r once, its first kRunBuf entries parked in registers (static
+// indices: no scratch); `over` sets if the run is longer.
+template <bool kHide>
+__device__ __forceinline__ void run_walk(const View& V, uint32_t r, uint32_t nres, uint32_t roff, uint32_t flags,
+                                         bool vprefix, PRun& B, PAcc& acc, bool& ok, bool& bad, bool& vbad,
+                                         bool& over) {
+  B.n = 0;
+  uint32_t e0;
+  if (!run_bounds(V, r, nres, roff, &B.rw, &e0)) { ok = false; return; }
+  uint32_t pos = B.rw & kRestartMask, n = 0, prev_kl = 0, prev_kind = 0;
+  bool go = true;
+#pragma unroll
+  for (int k = 0; k < kRunBuf; k++) {
+    if (go && pos < e0) {
+      uint32_t sh, un, vl, h;
+      const bool hok = pipe::hdr2(V.ld8(pos), &sh, &un, &vl, &h);
+      const uint32_t np = pos + h + un + vl;
+      bool hidden = false, setv = false;
+      if (!hok || (k == 0 && sh != 0) || np > e0) {
+        ok = false;
+        go = false;
+      } else {
+        bad = bad || (k > 0 && sh > prev_kl);
+        const uint32_t kl = sh + un;
+        if (!entry_class<kHide>(V, pos, h, sh, kl, uint32_t(k), prev_kl, prev_kind, flags, vprefix, hidden, setv)) {
+          ok = false;
+          go = false;
+        } else {
+          uint32_t vlen = vl;
+          if (setv) {
+            if (vl == 0) vbad = true;
+            else if ((V.byte(pos + h + un) & 0xC0) == 0 || (flags & PBL_ROW_NO_VALUER)) vlen--;
+          }
+          B.ea[k] = pos | uint32_t(hidden) << 15 | sh << 16 | uint32_t(setv) << 31;
+          B.eb[k] = un | (h << 14) | (vl << 17);
+          acc.ne++;
+          if (!hidden) {
+            acc.cnt++;
+            acc.kb += ukey_len(kl, flags);
+            acc.vb += vlen;
+          }
+          n++;
+          prev_kl = kl;
+          pos = np;
+        }
+      }
+    }
+  }
+  if (go && pos < e0) over = true;
+  B.n = n;
+  B.pos = pos;
+  B.e0 = e0;
+  B.prev_kl = prev_kl;
+  B.prev_kind = prev_kind;
+}
+
+// Chain and output state of the metadata pass, carried from one entry of a run
+// to the next: entry / visible index, key / value output offsets, the previous
+// entry's shared length, its prefix parent and that parent's shared length.
+struct MState {
+  uint32_t e, v, kb, vb, prev_sh, pp, ppsh;
+};
+
+// Per-KV metadata of one entry (validated by the walk).  The prefix parent is
+// the nearest earlier entry of the run with a smaller shared length (all-
+// nearest-smaller-values over the parents, amortised O(1)).
+template <bool kHide>
+__device__ __forceinline__ void entry_meta(Stage& S, Slot& W, const View& V, uint32_t pos, bool hidden, uint32_t sh,
+                                           uint32_t un, uint32_t h, uint32_t vl, bool setv, bool first, uint32_t rw,
+                                           uint32_t flags, MState& M) {
+  const uint32_t kl = sh + un;
+  uint32_t par = M.e, parsh = 0;
+  if (sh != 0) {
+    uint32_t c = M.e - 1, csh = M.prev_sh;
+    if (csh >= sh) { c = M.pp; csh = M.ppsh; }
+    while (csh >= sh) {
+      c = m_par(S.m0[c]);
+      csh = m_sh(S.m0[c]);
+    }
+    par = c;
+    parsh = csh;
+  }
+  S.m0[M.e] = uint64_t(pos + h) | uint64_t(sh) << 16 | uint64_t(kl) << 32 | uint64_t(par) << 48;
+  if (!(kHide && hidden)) {
     uint32_t vs = pos + h + un, vlen = vl;
     uint8_t fl = 0;
     if (first) fl = uint8_t(PBL_KV_RESTART | ((rw >> 31) ? PBL_KV_RESTART_SAMEPFX : 0));
     if (!(flags & PBL_ROW_RAW_KEYS) && kl < 8) fl |= PBL_KV_INVALID_KEY;
-    if (vprefix && kl >= 8 && (V.byte(pos + h + (kl - 8 - sh)) & 0xBF) == 1) {
+    if (setv) {
       const uint32_t pre = V.byte(vs);
       if ((pre & 0xC0) == 0 || (flags & PBL_ROW_NO_VALUER)) { vs++; vlen--; }
       else if ((pre & 0xC0) == 0x80) fl |= PBL_KV_VALBLK_HANDLE;
       else fl |= PBL_KV_BLOB_HANDLE;
     }
-    uint32_t par = j, parsh = 0;
-    if (sh != 0) {
-      uint32_t c = j - 1, csh = prev_sh;
-      if (csh >= sh) { c = pp; csh = ppsh; }
-      while (csh >= sh) {
-        c = m_par(S.m0[c]);
-        csh = m_sh(S.m0[c]);
-      }
-      par = c;
-      parsh = csh;
-    }
-    S.m0[j] = uint64_t(pos + h) | uint64_t(sh) << 16 | uint64_t(kl) << 32 | uint64_t(par) << 48;
-    S.kout[j] = uint16_t(kb);
-    S.eoff[j] = uint16_t(pos);
-    S.kvf[j] = fl;
-    W.vp[j] = vb | (vs << 16);
-    prev_sh = sh;
-    pp = par;
-    ppsh = parsh;
-    kb += (flags & PBL_ROW_RAW_KEYS) ? kl : (kl >= 8 ? kl - 8 : 0);
-    vb += vlen;
-    j++;
-    first = false;
+    S.kout[M.v] = uint16_t(M.kb);
+    S.eoff[M.v] = uint16_t(pos);
+    S.kvf[M.v] = fl;
+    if (kHide) S.ent[M.v] = uint16_t(M.e);
+    W.vp[M.v] = M.vb | (vs << 16);
+    M.kb += ukey_len(kl, flags);
+    M.vb += vlen;
+    M.v++;
+  }
+  M.prev_sh = sh;
+  M.pp = par;
+  M.ppsh = parsh;
+  M.e++;
+}
+
+// Metadata of the parked entries of a run.
+template <bool kHide>
+__device__ __forceinline__ void park_meta(Stage& S, Slot& W, const View& V, const PRun& B, uint32_t flags, MState& M) {
+#pragma unroll
+  for (int k = 0; k < kRunBuf; k++) {
+    if (uint32_t(k) < B.n)
+      entry_meta<kHide>(S, W, V, B.ea[k] & 0x7fffu, (B.ea[k] >> 15) & 1u, (B.ea[k] >> 16) & 0x7fffu,
+                        B.eb[k] & 0x3fffu, (B.eb[k] >> 14) & 7u, B.eb[k] >> 17, B.ea[k] >> 31, k == 0, B.rw, flags,
+                        M);
+  }
+}
+
+// Metadata of entries [pos, e0) of a run, re-read from the stage (k = entries
+// of the run before pos; prev_kl / prev_kind: the last one's).
+template <bool kHide>
+__device__ __forceinline__ void span_meta(Stage& S, Slot& W, const View& V, uint32_t pos, uint32_t e0, uint32_t rw,
+                                          uint32_t k, uint32_t prev_kl, uint32_t prev_kind, uint32_t flags,
+                                          bool vprefix, MState& M) {
+  while (pos < e0) {
+    uint32_t sh, un, vl, h;
+    pipe::hdr2(V.ld8(pos), &sh, &un, &vl, &h);
+    const uint32_t kl = sh + un;
+    bool hidden, setv;
+    entry_class<kHide>(V, pos, h, sh, kl, k, prev_kl, prev_kind, flags, vprefix, hidden, setv);
+    entry_meta<kHide>(S, W, V, pos, hidden, sh, un, h, vl, setv, k == 0, rw, flags, M);
+    k++;
+    prev_kl = kl;
     pos = pos + h + un + vl;
   }
-  acc = pipe::RunAcc{j, kb, vb};
 }
 
 // byte p of the internal key of KV j (source = max{i <= j : shared_i <= p})
@@ -557,6 +686,7 @@ __device__ __noinline__ void block_big(const Args A, uint32_t b, uint64_t boff, 
 }
 
 // One block on one wave, stage s held on entry and released before return.
+template <bool kHide>
 __device__ __forceinline__ void pool_block(PoolLds& L, uint32_t s, Slot& W, const Args& A, uint32_t b) {
   Stage& S = L.st[s];
   const int l = lane_id();
@@ -600,25 +730,32 @@ __device__ __forceinline__ void pool_block(PoolLds& L, uint32_t s, Slot& W, cons
     // lane l owns runs [r0, r1): contiguous, so a lane scan orders them
     const uint32_t R = (nres + kWave - 1) / kWave;
     const uint32_t r0 = min(uint32_t(l) * R, nres), r1 = min(r0 + R, nres);
-    pipe::RunAcc acc{0, 0, 0};
+    PAcc acc{0, 0, 0, 0};
     bool ok = true, bad = false, vbad = false, over = false;
-    pipe::RunBuf RB;
-    RB.cnt = 0;
-    RB.pos = RB.e0 = 0;
+    PRun RB;
+    RB.n = 0;
+    RB.pos = RB.e0 = RB.prev_kl = RB.prev_kind = RB.rw = 0;
     const bool single = R == 1;
     if (single) {
-      if (r0 < nres) pipe::run_walk(V, r0, nres, roff, flags, vprefix, RB, acc, ok, bad, vbad, over);
+      if (r0 < nres) run_walk<kHide>(V, r0, nres, roff, flags, vprefix, RB, acc, ok, bad, vbad, over);
       // a run longer than kRunBuf keeps its parked head and counts only its tail
-      if (over && ok) pipe::run_count_span(V, RB.pos, RB.e0, RB.cnt, RB.prev_kl, flags, vprefix, acc, ok, bad, vbad);
+      if (over && ok)
+        count_span<kHide>(V, RB.pos, RB.e0, RB.n, RB.prev_kl, RB.prev_kind, flags, vprefix, acc, ok, bad, vbad);
     } else {
-      for (uint32_t r = r0; r < r1 && ok; r++) pipe::run_count(V, r, nres, roff, flags, vprefix, acc, ok, bad, vbad);
+      for (uint32_t r = r0; r < r1 && ok; r++) {
+        uint32_t rw, e0;
+        if (!run_bounds(V, r, nres, roff, &rw, &e0)) ok = false;
+        else count_span<kHide>(V, rw & kRestartMask, e0, 0, 0, 0, flags, vprefix, acc, ok, bad, vbad);
+      }
     }
     const uint32_t ic = dpp_incl_scan(acc.cnt), ik = dpp_incl_scan(acc.kb), iv = dpp_incl_scan(acc.vb);
+    const uint32_t ie = kHide ? dpp_incl_scan(acc.ne) : ic;
     nkv = last_lane(ic);
     tkb = last_lane(ik);
     tvb = last_lane(iv);
+    const uint32_t nent = kHide ? last_lane(ie) : nkv;
     if (__ballot(bad)) status = PBL_CORRUPT_BOUNDS;
-    else if (__ballot(!ok) || nkv > uint32_t(kPKv) || tkb > kPKeyCap) slow = true;
+    else if (__ballot(!ok) || nent > uint32_t(kPKv) || tkb > kPKeyCap) slow = true;
     else if (__ballot(vbad)) status = PBL_CORRUPT_BOUNDS;  // Go: i.val[0] on an empty SET value
     if (status == PBL_OK && !slow) {
       // the sizes are final: publish, request the look-back windows, and write
@@ -628,19 +765,18 @@ __device__ __forceinline__ void pool_block(PoolLds& L, uint32_t s, Slot& W, cons
       published = true;
       if (b > 0) G.issue(LbPtrs(lb_state, nb), int64_t(b) - 1);
       PSTAMP(A, b, 3, l == 0);
-      pipe::RunAcc w{ic - acc.cnt, ik - acc.kb, iv - acc.vb};
+      MState M{ie - (kHide ? acc.ne : acc.cnt), ic - acc.cnt, ik - acc.kb, iv - acc.vb, 0, 0, 0};
       if (single) {
         if (r0 < nres) {
-          pipe::ParState P;
-          park_meta(S, W, V, RB, flags, vprefix, w, P);
-          if (over) span_meta(S, W, V, RB.pos, RB.e0, RB.rw, false, P, flags, vprefix, w);
+          park_meta<kHide>(S, W, V, RB, flags, M);
+          if (over) span_meta<kHide>(S, W, V, RB.pos, RB.e0, RB.rw, RB.n, RB.prev_kl, RB.prev_kind, flags, vprefix, M);
         }
       } else {
         for (uint32_t r = r0; r < r1; r++) {
-          const uint32_t st = roff + 4 * r;
-          const uint32_t rw = V.le32(st);
-          const uint32_t e0 = (r + 1 < nres) ? (V.le32(st + 4) & kRestartMask) : roff;
-          span_meta(S, W, V, rw & kRestartMask, e0, rw, true, pipe::ParState{0, 0, 0}, flags, vprefix, w);
+          uint32_t rw, e0;
+          run_bounds(V, r, nres, roff, &rw, &e0);
+          M.prev_sh = M.pp = M.ppsh = 0;
+          span_meta<kHide>(S, W, V, rw & kRestartMask, e0, rw, 0, 0, 0, flags, vprefix, M);
         }
       }
       if (l < 5) W.vp[nkv + l] = tvb;
@@ -701,9 +837,10 @@ __device__ __forceinline__ void pool_block(PoolLds& L, uint32_t s, Slot& W, cons
     to_glb(O.key_off)[kvb + b + j] = S.kout[j];
     to_glb(O.val_off)[kvb + b + j] = W.vp[j] & 0xffffu;
     if (j < nkv) {
-      const uint64_t m = S.m0[j];
+      const uint32_t e = kHide ? uint32_t(S.ent[j]) : j;
+      const uint64_t m = S.m0[e];
       uint8_t fl = S.kvf[j];
-      to_glb(O.trailer)[kvb + j] = with_seq(trailer_of(S, V, int(j), m, &fl, flags), A.in.synthetic_seq_num, flags);
+      to_glb(O.trailer)[kvb + j] = with_seq(trailer_of(S, V, int(e), m, &fl, flags), A.in.synthetic_seq_num, flags);
       if (O.kv_flags) to_glb(O.kv_flags)[kvb + j] = fl;
       if (O.entry_off) to_glb(O.entry_off)[kvb + j] = S.eoff[j];
       const uint32_t ukl = raw ? m_klen(m) : (m_klen(m) >= 8 ? m_klen(m) - 8 : 0u);
@@ -734,6 +871,7 @@ __device__ __forceinline__ void pool_block(PoolLds& L, uint32_t s, Slot& W, cons
 // Deadlock-free for any residency: a wave takes a ticket only while holding a
 // stage, and waits (in the look-back) only on smaller tickets, all of them
 // taken by waves that hold a stage or no longer need one.
+template <bool kHide>
 __global__ void __launch_bounds__(kTPBP, 1) rowblk_pool_kernel(Args A) {
   __shared__ PoolLds L;
   if (threadIdx.x == 0) L.free_mask = (1u << kNS) - 1u;
@@ -758,7 +896,7 @@ __global__ void __launch_bounds__(kTPBP, 1) rowblk_pool_kernel(Args A) {
     if (lane_id() == 0)
       reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(A.out.workspace) + ws_bytes(nb))[uint64_t(t0) * 16 + 8] = t_acq;
 #endif
-    pool_block(L, s, W, A, t0);
+    pool_block<kHide>(L, s, W, A, t0);
   }
 }
 

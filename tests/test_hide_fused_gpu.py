@@ -1,0 +1,77 @@
+"""HideObsoletePoints fused into the decode (batch flag PBL_ROW_HIDE_OBSOLETE:
+rowblk_iter.go:1168-1179) on the device against the oracle's decode under the
+same flag (tests/test_oracle_hide.py pins that against the transform
+restatement): bit-exact on every output array for random blocks, versioned
+keys whose shared prefix reaches the kind byte, value prefixes, blocks past
+the fast path's limits and past the 32 KiB stage; config-2 blocks (no obsolete
+points) decode as without the flag."""
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+from pebble_amd import _native as N
+from pebble_amd.batch import BlockBatch, DecodeError, decode
+from pebble_amd.rowblk import gen_row_blocks
+from rowutil import mvcc_block
+from test_rowblk_gpu import assert_same, pack, random_block
+
+pytestmark = pytest.mark.gpu
+HIDE = N.PBL_ROW_HIDE_OBSOLETE
+
+
+def check(buf, off, lens, flags, ctx):
+    o = oracle.decode_batch(buf, off, lens, 0, None, flags | HIDE)
+    g = decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, flags | HIDE)).to_host()
+    assert_same(g, o, ctx)
+    return g
+
+
+@pytest.mark.parametrize("flags", [0, N.PBL_ROW_VALUE_PREFIX, N.PBL_ROW_VALUE_PREFIX | N.PBL_ROW_NO_VALUER])
+def test_random_and_versioned_blocks(flags):
+    rng = random.Random(60 + flags)
+    blocks = [random_block(rng)[0] for _ in range(200)]
+    blocks += [mvcc_block(rng, rng.randint(1, 380), rng.choice([1, 2, 16, 33]), rng.random() < 0.5,
+                          rng.random() < 0.7) for _ in range(200)]
+    rng.shuffle(blocks)
+    g = check(*pack(blocks), flags, f"hide flags={flags}")
+    plain = oracle.decode_batch(*pack(blocks), 0, None, flags)
+    assert g["n_kv"] < plain["n_kv"]
+
+
+def test_general_path_blocks():
+    # > 400 entries (the fast path's cap), runs longer than 16, corrupt blocks
+    rng = random.Random(61)
+    blocks = [mvcc_block(rng, 900, 1, False, True), mvcc_block(rng, 600, 64, True, True),
+              mvcc_block(rng, 300, 40, False, False)]
+    for _ in range(40):
+        b = bytearray(mvcc_block(rng, rng.randint(1, 200), 16))
+        b[rng.randrange(len(b))] ^= 1 << rng.randrange(8)
+        blocks.append(bytes(b))
+    check(*pack(blocks), N.PBL_ROW_VALUE_PREFIX, "general")
+    check(*pack(blocks), 0, "general, no prefix")
+
+
+def test_blocks_past_the_stage():
+    rng = random.Random(62)
+    blocks = [mvcc_block(rng, 2500, 16) for _ in range(3)] + [mvcc_block(rng, 100, 16) for _ in range(20)]
+    assert max(len(b) for b in blocks) > 32768
+    check(*pack(blocks), 0, "big blocks")
+
+
+def test_config2_without_obsolete_points_is_unchanged():
+    buf, off, lens, n = gen_row_blocks(3, 3000, 32768, 16, 16, 100)
+    a = decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, HIDE)).to_host()
+    b = decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, 0)).to_host()
+    for k in ("trailer", "kv_flags", "entry_off", "key_off", "val_off", "key_bytes", "val_bytes", "restarts",
+              "blk_kv_base", "blk_key_base", "blk_val_base", "blk_status"):
+        assert np.array_equal(a[k], b[k]), k
+    assert a["n_kv"] == n
+
+
+def test_not_fused_for_colblk_or_mixed():
+    from pebble_amd.colblk import gen_col_blocks
+    buf, off, lens, n = gen_col_blocks(1, 20, 32768)
+    with pytest.raises(DecodeError, match="UNSUPPORTED"):
+        decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_COL_CRDB1, HIDE))
