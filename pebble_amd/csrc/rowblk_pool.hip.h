@@ -48,11 +48,14 @@ namespace pool {
 #ifndef PBL_POOL_STAGES
 #define PBL_POOL_STAGES 3
 #endif
-#ifndef PBL_POOL_VU
-#define PBL_POOL_VU 2
+#ifndef PBL_POOL_EARLY
+#define PBL_POOL_EARLY 0  // 1: the per-KV metadata in the wave's slot; the stage is released after the walk
 #endif
-#ifndef PBL_POOL_VCOPY
-#define PBL_POOL_VCOPY 2  // value copy: 1 = 16-B output granules (bucket + window), 2 = 8 lanes per KV
+#ifndef PBL_POOL_AHEAD
+#define PBL_POOL_AHEAD 0  // 1 (with PBL_POOL_EARLY): a released stage is refilled at once with the next ticket's block
+#endif
+#ifndef PBL_POOL_SLEEP
+#define PBL_POOL_SLEEP 1  // s_sleep units (64 cycles) between polls of the stage mask
 #endif
 #ifndef PBL_POOL_PRIO
 #define PBL_POOL_PRIO 2  // the stage holder's issue priority (values run at 0)
@@ -60,33 +63,46 @@ namespace pool {
 constexpr int kNW = PBL_POOL_WAVES;      // waves per workgroup (one workgroup per CU)
 constexpr int kNS = PBL_POOL_STAGES;     // staging buffers per workgroup
 constexpr int kTPBP = kNW * kWave;
-constexpr int kPKv = 400;                // KVs per block on the fast path
+constexpr int kPKv = PBL_POOL_EARLY ? 300 : 400;  // entries per block on the fast path
 constexpr uint32_t kPKeyCap = 65535;     // user-key bytes per block on the fast path (u16 offsets)
-constexpr int kVB = 7;                   // value output bucket = 128 B
-constexpr int kVBkt = kMaxFastLen >> kVB;
-constexpr int kVU = PBL_POOL_VU;         // value granules per lane per step
 
-// A stage: the block bytes and the per-KV metadata the key emit reads.
-// m0[e] = key source offset | shared << 16 | internal key length << 32 |
-// prefix parent << 48, for every entry e of the block.
+// Per-KV metadata of one block.  m0[e] = key source offset | shared << 16 |
+// internal key length << 32 | prefix parent << 48, for every entry e; the rest
+// by visible index (entries minus hidden obsolete points).
+struct Meta {
+  uint64_t m0[kPKv];
+  uint16_t kout[kPKv + 1];     // user-key output offsets (block relative)
+  uint16_t eoff[kPKv];         // entry offsets (KVEncoding.Offset)
+  uint16_t ent[kPKv];          // the entry of visible KV v (PBL_ROW_HIDE_OBSOLETE batches)
+  uint8_t kvf[kPKv];           // PBL_KV_* (OBSOLETE is added at emit time)
+};
+// A stage: the block bytes (and, unless PBL_POOL_EARLY, the metadata the key
+// emit reads from the stage).
 struct Stage {
   uint4 x[kLdsBlkBytes / 16];  // the block, byte i at kPad + (boff & 15) + i
-  uint64_t m0[kPKv];
-  uint16_t kout[kPKv + 1];     // user-key output offsets (block relative), by visible index
-  uint16_t eoff[kPKv];         // entry offsets (KVEncoding.Offset), by visible index
-  uint16_t ent[kPKv];          // the entry of visible KV v (PBL_ROW_HIDE_OBSOLETE batches)
-  uint8_t kvf[kPKv];           // PBL_KV_* (OBSOLETE is added at emit time), by visible index
+#if !PBL_POOL_EARLY
+  Meta m;
+#endif
 };
-// A wave's slot: what the value copy needs after the stage is released.
+// A wave's slot: what the emit needs after the stage is released.
 struct Slot {
   uint32_t vp[kPKv + 5];       // value output offset | value source offset << 16;
-                               // entries nkv..nkv+4 hold the value total (window reads)
-  uint16_t vbkt[kVBkt];        // KV holding value output byte q * 128
+                               // entries nkv..nkv+4 hold the value total
+#if PBL_POOL_EARLY
+  Meta m;
+#endif
 };
+// Stage ring state (PBL_POOL_AHEAD): tk[s] = kTkFree, kTkHeld, or the ticket
+// whose block has been (or is being) staged into s by the wave that released
+// it ("parked"); rdy[s] = 1 once that wave saw its LDS-DMA land.
+constexpr uint32_t kTkFree = 0xffffffffu, kTkHeld = 0xfffffffeu;
 struct PoolLds {
   Stage st[kNS];
   Slot sl[kNW];
   uint32_t free_mask;          // bit s: stage s is free
+  uint32_t tk[kNS], rdy[kNS], pblen[kNS];
+  uint64_t pboff[kNS];
+  uint32_t inflight;           // parks between their ticket and their tk[] store
 };
 static_assert(sizeof(PoolLds) <= 163840, "one pool workgroup per CU");
 
@@ -308,7 +324,7 @@ struct MState {
 // the nearest earlier entry of the run with a smaller shared length (all-
 // nearest-smaller-values over the parents, amortised O(1)).
 template <bool kHide>
-__device__ __forceinline__ void entry_meta(Stage& S, Slot& W, const View& V, uint32_t pos, bool hidden, uint32_t sh,
+__device__ __forceinline__ void entry_meta(Meta& Mt, Slot& W, const View& V, uint32_t pos, bool hidden, uint32_t sh,
                                            uint32_t un, uint32_t h, uint32_t vl, bool setv, bool first, uint32_t rw,
                                            uint32_t flags, MState& M) {
   const uint32_t kl = sh + un;
@@ -317,13 +333,13 @@ __device__ __forceinline__ void entry_meta(Stage& S, Slot& W, const View& V, uin
     uint32_t c = M.e - 1, csh = M.prev_sh;
     if (csh >= sh) { c = M.pp; csh = M.ppsh; }
     while (csh >= sh) {
-      c = m_par(S.m0[c]);
-      csh = m_sh(S.m0[c]);
+      c = m_par(Mt.m0[c]);
+      csh = m_sh(Mt.m0[c]);
     }
     par = c;
     parsh = csh;
   }
-  S.m0[M.e] = uint64_t(pos + h) | uint64_t(sh) << 16 | uint64_t(kl) << 32 | uint64_t(par) << 48;
+  Mt.m0[M.e] = uint64_t(pos + h) | uint64_t(sh) << 16 | uint64_t(kl) << 32 | uint64_t(par) << 48;
   if (!(kHide && hidden)) {
     uint32_t vs = pos + h + un, vlen = vl;
     uint8_t fl = 0;
@@ -335,10 +351,10 @@ __device__ __forceinline__ void entry_meta(Stage& S, Slot& W, const View& V, uin
       else if ((pre & 0xC0) == 0x80) fl |= PBL_KV_VALBLK_HANDLE;
       else fl |= PBL_KV_BLOB_HANDLE;
     }
-    S.kout[M.v] = uint16_t(M.kb);
-    S.eoff[M.v] = uint16_t(pos);
-    S.kvf[M.v] = fl;
-    if (kHide) S.ent[M.v] = uint16_t(M.e);
+    Mt.kout[M.v] = uint16_t(M.kb);
+    Mt.eoff[M.v] = uint16_t(pos);
+    Mt.kvf[M.v] = fl;
+    if (kHide) Mt.ent[M.v] = uint16_t(M.e);
     W.vp[M.v] = M.vb | (vs << 16);
     M.kb += ukey_len(kl, flags);
     M.vb += vlen;
@@ -352,11 +368,11 @@ __device__ __forceinline__ void entry_meta(Stage& S, Slot& W, const View& V, uin
 
 // Metadata of the parked entries of a run.
 template <bool kHide>
-__device__ __forceinline__ void park_meta(Stage& S, Slot& W, const View& V, const PRun& B, uint32_t flags, MState& M) {
+__device__ __forceinline__ void park_meta(Meta& Mt, Slot& W, const View& V, const PRun& B, uint32_t flags, MState& M) {
 #pragma unroll
   for (int k = 0; k < kRunBuf; k++) {
     if (uint32_t(k) < B.n)
-      entry_meta<kHide>(S, W, V, B.ea[k] & 0x7fffu, (B.ea[k] >> 15) & 1u, (B.ea[k] >> 16) & 0x7fffu,
+      entry_meta<kHide>(Mt, W, V, B.ea[k] & 0x7fffu, (B.ea[k] >> 15) & 1u, (B.ea[k] >> 16) & 0x7fffu,
                         B.eb[k] & 0x3fffu, (B.eb[k] >> 14) & 7u, B.eb[k] >> 17, B.ea[k] >> 31, k == 0, B.rw, flags,
                         M);
   }
@@ -365,7 +381,7 @@ __device__ __forceinline__ void park_meta(Stage& S, Slot& W, const View& V, cons
 // Metadata of entries [pos, e0) of a run, re-read from the stage (k = entries
 // of the run before pos; prev_kl / prev_kind: the last one's).
 template <bool kHide>
-__device__ __forceinline__ void span_meta(Stage& S, Slot& W, const View& V, uint32_t pos, uint32_t e0, uint32_t rw,
+__device__ __forceinline__ void span_meta(Meta& Mt, Slot& W, const View& V, uint32_t pos, uint32_t e0, uint32_t rw,
                                           uint32_t k, uint32_t prev_kl, uint32_t prev_kind, uint32_t flags,
                                           bool vprefix, MState& M) {
   while (pos < e0) {
@@ -374,21 +390,35 @@ __device__ __forceinline__ void span_meta(Stage& S, Slot& W, const View& V, uint
     const uint32_t kl = sh + un;
     bool hidden, setv;
     entry_class<kHide>(V, pos, h, sh, kl, k, prev_kl, prev_kind, flags, vprefix, hidden, setv);
-    entry_meta<kHide>(S, W, V, pos, hidden, sh, un, h, vl, setv, k == 0, rw, flags, M);
+    entry_meta<kHide>(Mt, W, V, pos, hidden, sh, un, h, vl, setv, k == 0, rw, flags, M);
     k++;
     prev_kl = kl;
     pos = pos + h + un + vl;
   }
 }
 
-// byte p of the internal key of KV j (source = max{i <= j : shared_i <= p})
-__device__ __forceinline__ uint32_t key_byte(const Stage& S, const View& V, int j, uint32_t p) {
-  uint64_t m = S.m0[j];
-  while (p < m_sh(m)) m = S.m0[--j];
+// The block's bytes for the key emit: the stage (LDS) or the block in global
+// memory (PBL_POOL_EARLY: the stage is gone by then).  ld16 windows may start
+// up to 15 bytes before the block.
+struct GSrc {
+  gptr<const uint8_t> g;
+  uint32_t blen, end16;
+  __device__ __forceinline__ uint32_t byte(uint32_t i) const { return g[i]; }
+  __device__ __forceinline__ uint64_t ld8(uint32_t i) const { return *(gptr<const u64_ug>)(g + i); }
+  __device__ __forceinline__ uint32_t le32(uint32_t i) const { return *(gptr<const u32_ug>)(g + i); }
+  __device__ __forceinline__ uint4 ld16(int32_t i) const { return gld16(g, i, blen, end16); }
+};
+
+// byte p of the internal key of entry j (source = max{i <= j : shared_i <= p})
+template <class Src>
+__device__ __forceinline__ uint32_t key_byte(const Meta& Mt, const Src& V, int j, uint32_t p) {
+  uint64_t m = Mt.m0[j];
+  while (p < m_sh(m)) m = Mt.m0[--j];
   return V.byte(m_ksrc(m) + p - m_sh(m));
 }
 
-__device__ __forceinline__ uint64_t trailer_of(const Stage& S, const View& V, int j, uint64_t m, uint8_t* fl,
+template <class Src>
+__device__ __forceinline__ uint64_t trailer_of(const Meta& Mt, const Src& V, int j, uint64_t m, uint8_t* fl,
                                                uint32_t flags) {
   if (flags & PBL_ROW_RAW_KEYS) return 0;
   const uint32_t kl = m_klen(m);
@@ -399,16 +429,17 @@ __device__ __forceinline__ uint64_t trailer_of(const Stage& S, const View& V, in
     raw = V.ld8(m_ksrc(m) + (kl - 8 - sh));
   } else {
     raw = 0;
-    for (int i = 0; i < 8; i++) raw |= uint64_t(key_byte(S, V, j, kl - 8 + i)) << (8 * i);
+    for (int i = 0; i < 8; i++) raw |= uint64_t(key_byte(Mt, V, j, kl - 8 + i)) << (8 * i);
   }
   if (raw & 64u) *fl |= PBL_KV_OBSOLETE;
   return raw & kTrailerObsoleteMask;
 }
 
 // Key bytes [c, c + n) of KV m (n <= 16) merged from the segments of its prefix
-// chain: each an LDS read that starts where the chunk's first byte would sit in
-// that entry (at most 15 bytes before the block: the stage's front pad).
-__device__ __forceinline__ uint4 key_chunk(const Stage& S, const View& V, uint64_t m, uint32_t c, uint32_t n) {
+// chain: each a 16-B read that starts where the chunk's first byte would sit in
+// that entry (at most 15 bytes before the block).
+template <class Src>
+__device__ __forceinline__ uint4 key_chunk(const Meta& Mt, const Src& V, uint64_t m, uint32_t c, uint32_t n) {
   const uint32_t ce = c + n;
   uint32_t cur = ce;
   uint4 w = make_uint4(0, 0, 0, 0);
@@ -423,148 +454,177 @@ __device__ __forceinline__ uint4 key_chunk(const Stage& S, const View& V, uint64
     }
     if (lo_i <= c) break;
     cur = lo_i;
-    m = S.m0[m_par(m)];
+    m = Mt.m0[m_par(m)];
   }
   return w;
 }
 
-__device__ __forceinline__ void put16(gptr<uint8_t> base, uint64_t a, const uint4& w, uint32_t lo, uint32_t hi) {
-  if (lo == 0 && hi == 16) *(gptr<u32x4>)(base + a) = u32x4{w.x, w.y, w.z, w.w};
-  else store_partial16(base + a, w, lo, hi);
-}
-
-// Value bytes of a block at output [vbb, vbb + tvb): one 16-B aligned output
-// granule per lane, kVU granules per step with their loads in flight
-// together.  (1) bucket -> first KV; (2) a 5-word window of packed
-// (vout | vsrc) words -> the KV holding the granule's first byte and the next
-// one; (3) both source segments loaded from the block in global memory at
-// once, merged when the granule straddles two values.  Granules touching 3+
-// values (values < 16 B) or more than 3 bucket steps take the general loop.
-__device__ __forceinline__ void copy_values(const Slot& W, gptr<const uint8_t> g, uint32_t blen, uint64_t vbb,
-                                            uint32_t tvb, gptr<uint8_t> vbytes) {
+// Keys, offsets, trailers, flags and entry offsets of a block's visible KVs:
+// lane per KV, the key merged from its prefix chain's segments.
+template <bool kHide, class Src>
+__device__ __forceinline__ void emit_keys(const Meta& Mt, const Slot& W, const Src& V, const Args& A, uint32_t b,
+                                          uint32_t nkv, uint64_t kvb, uint64_t kbb) {
   const int l = lane_id();
-  const uint32_t end16 = uint32_t(((uint64_t(g) + blen + 15) & ~uint64_t(15)) - uint64_t(g));
-  const uint64_t d0 = vbb, d1 = vbb + tvb;
-  for (uint64_t a = (d0 & ~uint64_t(15)) + 16 * uint64_t(l); a < d1; a += 16 * kVU * kWave) {
-    uint4 w[kVU];
-    uint32_t lo[kVU], hi[kVU], o[kVU], oe[kVU], j0[kVU];
-    bool live[kVU];
-#pragma unroll
-    for (int u = 0; u < kVU; u++) {
-      const uint64_t gq = a + uint64_t(u) * 16 * kWave;
-      live[u] = gq < d1;
-      lo[u] = gq < d0 ? uint32_t(d0 - gq) : 0u;
-      hi[u] = !live[u] ? 0u : (gq + 16 <= d1 ? 16u : uint32_t(d1 - gq));
-      o[u] = live[u] ? uint32_t(gq + lo[u] - d0) : 0u;
-      oe[u] = live[u] ? uint32_t(gq + hi[u] - d0) : 0u;
-      j0[u] = W.vbkt[o[u] >> kVB];
-    }
-    uint32_t vw[kVU][5];
-#pragma unroll
-    for (int u = 0; u < kVU; u++)
-#pragma unroll
-      for (int k = 0; k < 5; k++) vw[u][k] = W.vp[j0[u] + k];
-    uint4 ga[kVU], gb[kVU];
-    uint32_t sa[kVU], ea[kVU], sb[kVU], eb[kVU];
-    bool gen[kVU];
-#pragma unroll
-    for (int u = 0; u < kVU; u++) {
-      const uint32_t q = o[u];
-      const bool s1 = (vw[u][1] & 0xffff) <= q;
-      const bool s2 = s1 && (vw[u][2] & 0xffff) <= q;
-      const bool s3 = s2 && (vw[u][3] & 0xffff) <= q;
-      const uint32_t k = uint32_t(s1) + uint32_t(s2) + uint32_t(s3);
-      const uint32_t A0 = k == 0 ? vw[u][0] : k == 1 ? vw[u][1] : k == 2 ? vw[u][2] : vw[u][3];
-      const uint32_t A1 = k == 0 ? vw[u][1] : k == 1 ? vw[u][2] : k == 2 ? vw[u][3] : vw[u][4];
-      const uint32_t A2 = k == 0 ? vw[u][2] : k == 1 ? vw[u][3] : k == 2 ? vw[u][4] : vw[u][4];
-      const uint32_t v0 = A0 & 0xffff, v1 = A1 & 0xffff, v2 = A2 & 0xffff;
-      gen[u] = live[u] && ((s3 && (vw[u][4] & 0xffff) <= q) || (oe[u] > v1 && oe[u] > v2) || k == 3);
-      sa[u] = q;
-      ea[u] = oe[u] < v1 ? oe[u] : v1;
-      sb[u] = v1;
-      eb[u] = oe[u] < v2 ? oe[u] : v2;
-      const uint32_t gqa = uint32_t(d0 + sa[u] - (a + uint64_t(u) * 16 * kWave));
-      ga[u] = live[u] && !gen[u] ? gld16(g, int32_t(A0 >> 16) + int32_t(sa[u] - v0) - int32_t(gqa), blen, end16)
-                                 : make_uint4(0, 0, 0, 0);
-      const uint32_t gqb = gqa + (sb[u] - sa[u]);
-      gb[u] = live[u] && !gen[u] && oe[u] > v1 ? gld16(g, int32_t(A1 >> 16) - int32_t(gqb), blen, end16)
-                                               : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int u = 0; u < kVU; u++) {
-      if (!live[u]) continue;
-      const uint64_t gq = a + uint64_t(u) * 16 * kWave;
-      if (!gen[u]) {
-        const uint32_t gqa = uint32_t(d0 + sa[u] - gq);
-        if (gqa == 0 && ea[u] - sa[u] == 16) {
-          w[u] = ga[u];
-        } else {
-          w[u] = make_uint4(0, 0, 0, 0);
-          merge16(w[u], ga[u], gqa, gqa + (ea[u] - sa[u]));
-          if (oe[u] > sb[u]) {
-            const uint32_t gqb = gqa + (sb[u] - sa[u]);
-            merge16(w[u], gb[u], gqb, gqb + (eb[u] - sb[u]));
-          }
-        }
-      } else {
-        uint32_t j = j0[u];
-        while ((W.vp[j + 1] & 0xffffu) <= o[u]) j++;
-        w[u] = make_uint4(0, 0, 0, 0);
-        for (;;) {
-          const uint32_t v0 = W.vp[j] & 0xffffu, v1 = W.vp[j + 1] & 0xffffu;
-          const uint32_t s_ = o[u] > v0 ? o[u] : v0, e_ = oe[u] < v1 ? oe[u] : v1;
-          const uint32_t q = uint32_t(d0 + s_ - gq);
-          merge16(w[u], gld16(g, int32_t(W.vp[j] >> 16) + int32_t(s_ - v0) - int32_t(q), blen, end16), q,
-                  q + (e_ - s_));
-          if (v1 >= oe[u]) break;
-          j++;
-        }
+  const uint32_t flags = A.in.flags;
+  const pbl_decode_out& O = A.out;
+  const gptr<uint8_t> kbytes = to_glb(O.key_bytes) + kbb;
+  const bool raw = (flags & PBL_ROW_RAW_KEYS) != 0;
+  for (uint32_t j = l; j <= nkv; j += kWave) {
+    to_glb(O.key_off)[kvb + b + j] = Mt.kout[j];
+    to_glb(O.val_off)[kvb + b + j] = W.vp[j] & 0xffffu;
+    if (j < nkv) {
+      const uint32_t e = kHide ? uint32_t(Mt.ent[j]) : j;
+      const uint64_t m = Mt.m0[e];
+      uint8_t fl = Mt.kvf[j];
+      to_glb(O.trailer)[kvb + j] = with_seq(trailer_of(Mt, V, int(e), m, &fl, flags), A.in.synthetic_seq_num, flags);
+      if (O.kv_flags) to_glb(O.kv_flags)[kvb + j] = fl;
+      if (O.entry_off) to_glb(O.entry_off)[kvb + j] = Mt.eoff[j];
+      const uint32_t ukl = raw ? m_klen(m) : (m_klen(m) >= 8 ? m_klen(m) - 8 : 0u);
+      const uint32_t ko = Mt.kout[j];
+      for (uint32_t c = 0; c < ukl; c += 16) {
+        const uint32_t n = ukl - c < 16 ? ukl - c : 16u;
+        store_n(kbytes + ko + c, key_chunk(Mt, V, m, c, n), n);
       }
-      put16(vbytes, gq, w[u], lo[u], hi[u]);
     }
   }
 }
 
-// Value bytes of a block, 8 lanes per KV (PBL_POOL_VCOPY 2): lane c of a
-// group copies its value's 16-B chunks c, c + 8, ... from the block in global
-// memory to the output with plain (unaligned) 16-B loads and stores.  A
-// value's last chunk is the one that ENDS at the value's end, overlapping the
-// chunk before it, so every store writes bytes of its own value only and no
-// store is partial.  Two KVs per group per step, their loads in flight
-// together.  Values shorter than 16 B go byte by byte; values longer than
-// kWaveVal are copied by the whole wave, 1 KiB per instruction.
+// emit_keys for the block in GLOBAL memory (PBL_POOL_EARLY): the loads are
+// L2 / MALL round trips, so kKU KVs per lane go through three phases together:
+// their metadata from the slot, then every global load (the trailer's 8 bytes;
+// the user key's segments: its own unshared bytes and, for a key that shares
+// a prefix, its prefix parent's bytes), then the merges and stores.  The fast
+// form covers keys of at most 16 bytes whose prefix chain ends at the parent
+// (a restart-interval row block: the parent is the run's first key) with the
+// trailer in the entry's own bytes; the rest take emit_keys' general form.
+#ifndef PBL_POOL_KU
+#define PBL_POOL_KU 3
+#endif
+constexpr int kKU = PBL_POOL_KU;
+template <bool kHide>
+__device__ __forceinline__ void emit_keys_glb(const Meta& Mt, const Slot& W, const GSrc& V, const Args& A, uint32_t b,
+                                              uint32_t nkv, uint64_t kvb, uint64_t kbb) {
+  const int l = lane_id();
+  const uint32_t flags = A.in.flags;
+  const pbl_decode_out& O = A.out;
+  const gptr<uint8_t> kbytes = to_glb(O.key_bytes) + kbb;
+  const bool raw = (flags & PBL_ROW_RAW_KEYS) != 0;
+  for (uint32_t j0 = 0; j0 <= nkv; j0 += kWave * kKU) {
+    uint32_t ko[kKU], vo[kKU], eo[kKU], ukl[kKU], sh[kKU], e[kKU];
+    uint64_t m[kKU], mp[kKU];
+    uint8_t fl[kKU];
+    bool fast[kKU];
+#pragma unroll
+    for (int u = 0; u < kKU; u++) {
+      const uint32_t j = j0 + kWave * u + l;
+      ko[u] = j <= nkv ? uint32_t(Mt.kout[j]) : 0u;
+      vo[u] = j <= nkv ? (W.vp[j] & 0xffffu) : 0u;
+      e[u] = kHide ? (j < nkv ? uint32_t(Mt.ent[j]) : 0u) : j;
+      m[u] = j < nkv ? Mt.m0[e[u]] : 0ull;
+      fl[u] = j < nkv ? Mt.kvf[j] : uint8_t(0);
+      eo[u] = j < nkv ? uint32_t(Mt.eoff[j]) : 0u;
+      const uint32_t kl = m_klen(m[u]);
+      sh[u] = m_sh(m[u]);
+      ukl[u] = raw ? kl : (kl >= 8 ? kl - 8 : 0u);
+      mp[u] = (j < nkv && sh[u] != 0) ? Mt.m0[m_par(m[u])] : 0ull;
+      fast[u] = ukl[u] <= 16 && (sh[u] == 0 || m_sh(mp[u]) == 0) && (raw || kl < 8 || kl - 8 >= sh[u]);
+    }
+    uint64_t tr[kKU];
+    uint4 ka[kKU], kp[kKU];
+#pragma unroll
+    for (int u = 0; u < kKU; u++) {
+      const uint32_t j = j0 + kWave * u + l;
+      const uint32_t kl = m_klen(m[u]);
+      tr[u] = 0;
+      if (j < nkv && fast[u] && !raw && kl >= 8) tr[u] = V.ld8(m_ksrc(m[u]) + (kl - 8 - sh[u]));
+      if (j < nkv && fast[u] && ukl[u]) ka[u] = V.ld16(int32_t(m_ksrc(m[u])) - int32_t(sh[u]));
+      if (j < nkv && fast[u] && ukl[u] && sh[u]) kp[u] = V.ld16(int32_t(m_ksrc(mp[u])));
+    }
+#pragma unroll
+    for (int u = 0; u < kKU; u++) {
+      const uint32_t j = j0 + kWave * u + l;
+      if (j > nkv) continue;
+      to_glb(O.key_off)[kvb + b + j] = ko[u];
+      to_glb(O.val_off)[kvb + b + j] = vo[u];
+      if (j == nkv) continue;
+      uint64_t t;
+      uint8_t f = fl[u];
+      if (!fast[u]) {
+        t = trailer_of(Mt, V, int(e[u]), m[u], &f, flags);
+        for (uint32_t c = 0; c < ukl[u]; c += 16) {
+          const uint32_t n = ukl[u] - c < 16 ? ukl[u] - c : 16u;
+          store_n(kbytes + ko[u] + c, key_chunk(Mt, V, m[u], c, n), n);
+        }
+      } else {
+        const uint32_t kl = m_klen(m[u]);
+        if (raw) t = 0;
+        else if (kl < 8) t = kKindInvalid;
+        else {
+          if (tr[u] & 64u) f |= PBL_KV_OBSOLETE;
+          t = tr[u] & kTrailerObsoleteMask;
+        }
+        if (ukl[u]) {
+          const uint32_t n = ukl[u], lo = sh[u] < n ? sh[u] : n;
+          uint4 w = ka[u];
+          if (lo) {
+            w = make_uint4(0, 0, 0, 0);
+            merge16(w, ka[u], lo, n);
+            merge16(w, kp[u], 0, lo);
+          }
+          store_n(kbytes + ko[u], w, n);
+        }
+      }
+      to_glb(O.trailer)[kvb + j] = with_seq(t, A.in.synthetic_seq_num, flags);
+      if (O.kv_flags) to_glb(O.kv_flags)[kvb + j] = f;
+      if (O.entry_off) to_glb(O.entry_off)[kvb + j] = eo[u];
+    }
+  }
+}
+
+// Value bytes of a block, 8 lanes per KV: lane c of a group copies its
+// value's 16-B chunks c, c + 8, ... from the block in global memory to the
+// output with plain (unaligned) 16-B loads and stores.  A value's last chunk
+// is the one that ENDS at the value's end, overlapping the chunk before it, so
+// every store writes bytes of its own value only and no store is partial.
+// kVG KVs per group per step, all their first chunks loaded before any store:
+// the loads are L2 / MALL round trips, and a step costs about one of them.
+// Values shorter than 16 B go byte by byte; values longer than kWaveVal are
+// copied by the whole wave, four 16-B chunks per lane in flight.
+#ifndef PBL_POOL_VG
+#define PBL_POOL_VG 8
+#endif
+constexpr int kVG = PBL_POOL_VG;
 constexpr uint32_t kWaveVal = 1024;
 __device__ __forceinline__ void copy_values_grp(const Slot& W, gptr<const uint8_t> g, uint32_t nkv,
                                                 gptr<uint8_t> vbytes) {
   const int l = lane_id();
   const uint32_t c = uint32_t(l) & 7u;
-  for (uint32_t j0 = 0; j0 < nkv; j0 += 16) {
-    uint32_t vo[2], vl[2], vs[2];
+  for (uint32_t j0 = 0; j0 < nkv; j0 += 8 * kVG) {
+    uint32_t vo[kVG], vl[kVG], vs[kVG];
 #pragma unroll
-    for (int u = 0; u < 2; u++) {
+    for (int u = 0; u < kVG; u++) {
       const uint32_t j = j0 + 8 * u + (uint32_t(l) >> 3);
       const uint32_t a = j < nkv ? W.vp[j] : 0u, z = j < nkv ? W.vp[j + 1] : 0u;
       vo[u] = a & 0xffffu;
       vl[u] = (z & 0xffffu) - vo[u];
       vs[u] = a >> 16;
     }
-    uint4 x[2];
-    uint32_t oo[2];
-    bool has[2];
+    // (every lane loads, from the block's first bytes when it has no chunk:
+    // no conditionally defined registers)
+    u32x4 x[kVG];
+    uint32_t q[kVG];
+    bool has[kVG];
 #pragma unroll
-    for (int u = 0; u < 2; u++) {
+    for (int u = 0; u < kVG; u++) {
       has[u] = vl[u] >= 16 && vl[u] <= kWaveVal && 16 * c < vl[u];
-      oo[u] = 16 * c < vl[u] - 16 ? 16 * c : vl[u] - 16;
-      if (has[u]) {
-        const u32x4 v = *(gptr<const u32x4_ug>)(g + vs[u] + oo[u]);
-        x[u] = make_uint4(v.x, v.y, v.z, v.w);
-      }
+      q[u] = has[u] ? (16 * c < vl[u] - 16 ? 16 * c : vl[u] - 16) : 0u;
+      x[u] = *(gptr<const u32x4_ug>)(g + (has[u] ? vs[u] + q[u] : 0u));
     }
 #pragma unroll
-    for (int u = 0; u < 2; u++)
-      if (has[u]) *(gptr<u32x4_ug>)(vbytes + vo[u] + oo[u]) = u32x4{x[u].x, x[u].y, x[u].z, x[u].w};
+    for (int u = 0; u < kVG; u++)
+      if (has[u]) *(gptr<u32x4_ug>)(vbytes + vo[u] + q[u]) = x[u];
 #pragma unroll
-    for (int u = 0; u < 2; u++) {
+    for (int u = 0; u < kVG; u++) {
       if (vl[u] > 128 && vl[u] <= kWaveVal) {
         for (uint32_t o = 16 * c + 128; o < vl[u]; o += 128) {
           const uint32_t q = o < vl[u] - 16 ? o : vl[u] - 16;
@@ -574,15 +634,26 @@ __device__ __forceinline__ void copy_values_grp(const Slot& W, gptr<const uint8_
         for (uint32_t o = c; o < vl[u]; o += 8) vbytes[vo[u] + o] = g[vs[u] + o];
       }
     }
-    // long values: the whole wave, 16 B per lane per step
+  }
+  // long values: the whole wave, four 16-B chunks per lane in flight
+  for (uint32_t j0 = 0; j0 < nkv; j0 += kWave) {
+    const uint32_t j = j0 + uint32_t(l);
+    const uint32_t a = j < nkv ? W.vp[j] : 0u, z = j < nkv ? W.vp[j + 1] : 0u;
+    const uint32_t len = (z & 0xffffu) - (a & 0xffffu);
+    for (uint64_t lm = __ballot(j < nkv && len > kWaveVal); lm; lm &= lm - 1) {
+      const int sl = __builtin_ctzll(lm);
+      const uint32_t ls = __shfl(a >> 16, sl, kWave), ll = __shfl(len, sl, kWave), lo = __shfl(a & 0xffffu, sl, kWave);
+      for (uint32_t o0 = 16u * l; o0 < ll; o0 += 64u * kWave) {
+        u32x4 y[4];
 #pragma unroll
-    for (int u = 0; u < 2; u++) {
-      for (uint64_t lm = __ballot(c == 0 && vl[u] > kWaveVal); lm; lm &= lm - 1) {
-        const int sl = __builtin_ctzll(lm);
-        const uint32_t ls = __shfl(vs[u], sl, kWave), ll = __shfl(vl[u], sl, kWave), lo = __shfl(vo[u], sl, kWave);
-        for (uint32_t o = 16u * l; o < ll; o += 16u * kWave) {
-          const uint32_t q = o < ll - 16 ? o : ll - 16;
-          *(gptr<u32x4_ug>)(vbytes + lo + q) = *(gptr<const u32x4_ug>)(g + ls + q);
+        for (int k = 0; k < 4; k++) {
+          const uint32_t o = o0 + 16u * kWave * k, q = o < ll - 16 ? o : ll - 16;
+          y[k] = *(gptr<const u32x4_ug>)(g + ls + (o < ll ? q : 0u));
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t o = o0 + 16u * kWave * k, q = o < ll - 16 ? o : ll - 16;
+          if (o < ll) *(gptr<u32x4_ug>)(vbytes + lo + q) = y[k];
         }
       }
     }
@@ -604,7 +675,7 @@ __device__ __forceinline__ uint32_t acquire(PoolLds& L) {
           break;
         }
       } else {
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(PBL_POOL_SLEEP);
       }
     }
   }
@@ -613,6 +684,142 @@ __device__ __forceinline__ uint32_t acquire(PoolLds& L) {
   // waves copying values
   if (PBL_POOL_PRIO) __builtin_amdgcn_s_setprio(PBL_POOL_PRIO);
   return __builtin_amdgcn_readfirstlane(__shfl(s, 0, kWave));
+}
+
+// The block [boff, boff + blen) into stage S by LDS-DMA (granule g of the 16-B
+// aligned range at x[1 + g]); the caller waits vmcnt(0) before reading it.
+__device__ __forceinline__ void stage_dma(Stage& S, const uint8_t* blocks, uint64_t boff, uint32_t blen) {
+  const int l = lane_id();
+  const uint64_t a0 = boff & ~uint64_t(15), a1 = (boff + blen + 15) & ~uint64_t(15);
+  const uint32_t n16 = uint32_t((a1 - a0) >> 4);
+  const gptr<const uint8_t> base = to_glb(blocks + a0);
+  for (uint32_t g0 = 0; g0 < n16; g0 += kWave) {
+    if (g0 + l < n16)
+      __builtin_amdgcn_global_load_lds((gptr<const void>)(base + 16ull * (g0 + l)),
+                                       (lptr<void>)to_lds_ptr(reinterpret_cast<void*>(&S.x[1 + g0])), 16, 0, 0);
+  }
+}
+
+// ---- the stage ring (PBL_POOL_AHEAD) -------------------------------------------
+// A wave done with a stage takes the next ticket and starts that block's
+// LDS-DMA into the stage before it goes on with its own block ("parks" it);
+// the next free wave picks the parked stage with the SMALLEST ticket and finds
+// the block staged.  The DMA round trip thus overlaps the parker's look-back
+// instead of sitting inside a stage hold.  Deadlock freedom: a wave picks
+// only the smallest parked ticket, and only while no park is between its
+// ticket and its tk[] store (inflight), so every ticket smaller than a picked
+// one has been picked too; a wave's look-back waits only on smaller tickets,
+// so the smallest unfinished ticket is always held by a wave that can go on,
+// or parked while some wave is free to pick it.
+struct Work {
+  uint32_t s, t, blen;
+  uint64_t boff;
+  bool staged;
+};
+
+// Park stage s: the next ticket's block is staged into it (or the stage is
+// freed when the tickets are exhausted).  Returns whether the caller must
+// later mark it ready (after its own vmcnt(0)).
+__device__ __forceinline__ bool park(PoolLds& L, uint32_t s, const Args& A) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of the stage has completed
+  wave_sync();
+  const uint32_t nb = A.in.n_blocks;
+  uint32_t t = 0;
+  if (lane_id() == 0) {
+    __hip_atomic_fetch_add(&L.inflight, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    t = g_atomic_add(reinterpret_cast<uint32_t*>(A.out.workspace), 1u);
+  }
+  t = __builtin_amdgcn_readfirstlane(__shfl(t, 0, kWave));
+  bool dma = false;
+  if (t < nb) {
+    const uint64_t boff = to_glb(A.in.block_off)[t];
+    const uint32_t blen = to_glb(A.in.block_len)[t];
+    dma = blen <= kMaxFastLen;
+    if (dma) stage_dma(L.st[s], A.in.blocks, boff, blen);
+    if (lane_id() == 0) {
+      L.pboff[s] = boff;
+      L.pblen[s] = blen;
+      __hip_atomic_store(&L.rdy[s], dma ? 0u : 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_store(&L.tk[s], t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  } else if (lane_id() == 0) {
+    __hip_atomic_store(&L.tk[s], kTkFree, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  if (lane_id() == 0) __hip_atomic_fetch_sub(&L.inflight, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (PBL_POOL_PRIO) __builtin_amdgcn_s_setprio(0);
+  return dma;
+}
+
+// Mark the stage this wave parked as staged (its DMA has landed: vmcnt(0)).
+__device__ __forceinline__ void mark_ready(PoolLds& L, uint32_t s) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  wave_sync();
+  if (lane_id() == 0) __hip_atomic_store(&L.rdy[s], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// The next block for this wave: the smallest parked ticket (waiting for its
+// DMA to land), or a free stage and a fresh ticket.  w.t >= n_blocks: done.
+__device__ __forceinline__ Work get_work(PoolLds& L, const Args& A) {
+  const uint32_t nb = A.in.n_blocks;
+  uint32_t r[5] = {0, 0, 0, 0, 0};  // s, t, blen, boff lo, boff hi | staged << 31
+  if (lane_id() == 0) {
+    for (;;) {
+      if (__hip_atomic_load(&L.inflight, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0) {
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      uint32_t best = kTkHeld, bs = kNS, fs = kNS;
+      for (uint32_t q = 0; q < uint32_t(kNS); q++) {
+        const uint32_t x = __hip_atomic_load(&L.tk[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (x < best) { best = x; bs = q; }
+        if (x == kTkFree) fs = q;
+      }
+      if (bs < uint32_t(kNS)) {
+        uint32_t want = best;
+        if (__hip_atomic_compare_exchange_strong(&L.tk[bs], &want, kTkHeld, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP)) {
+          while (__hip_atomic_load(&L.rdy[bs], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+            __builtin_amdgcn_s_sleep(1);
+          const uint64_t boff = L.pboff[bs];
+          r[0] = bs; r[1] = best; r[2] = L.pblen[bs];
+          r[3] = uint32_t(boff); r[4] = uint32_t(boff >> 32) | 0x80000000u;
+          break;
+        }
+        continue;
+      }
+      if (fs < uint32_t(kNS)) {
+        uint32_t want = kTkFree;
+        if (__hip_atomic_compare_exchange_strong(&L.tk[fs], &want, kTkHeld, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP)) {
+          // a fresh ticket (counted in flight so no picker passes a smaller one)
+          __hip_atomic_fetch_add(&L.inflight, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const uint32_t t = g_atomic_add(reinterpret_cast<uint32_t*>(A.out.workspace), 1u);
+          __hip_atomic_fetch_sub(&L.inflight, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (t >= nb) {
+            __hip_atomic_store(&L.tk[fs], kTkFree, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          } else {
+            const uint64_t boff = to_glb(A.in.block_off)[t];
+            r[2] = to_glb(A.in.block_len)[t];
+            r[3] = uint32_t(boff);
+            r[4] = uint32_t(boff >> 32);  // (not staged: the caller stages it)
+          }
+          r[0] = fs; r[1] = t < nb ? t : nb;
+          break;
+        }
+        continue;
+      }
+      __builtin_amdgcn_s_sleep(PBL_POOL_SLEEP);
+    }
+  }
+  Work w;
+  w.s = __builtin_amdgcn_readfirstlane(__shfl(r[0], 0, kWave));
+  w.t = __builtin_amdgcn_readfirstlane(__shfl(r[1], 0, kWave));
+  w.blen = __builtin_amdgcn_readfirstlane(__shfl(r[2], 0, kWave));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(__shfl(r[4], 0, kWave));
+  w.boff = uint64_t(__builtin_amdgcn_readfirstlane(__shfl(r[3], 0, kWave))) | uint64_t(hi & 0x7fffffffu) << 32;
+  w.staged = (hi >> 31) != 0;
+  if (PBL_POOL_PRIO && w.t < nb) __builtin_amdgcn_s_setprio(PBL_POOL_PRIO);
+  return w;
 }
 
 // Return stage s to the pool once every LDS read of it has completed.
@@ -627,7 +834,7 @@ __device__ __forceinline__ void release(PoolLds& L, uint32_t s) {
 // stage's metadata area as its key buffer; a key that outgrows it re-runs from
 // global memory with the whole stage as the key buffer.  Resolves its own
 // look-back and writes every output.  Out of line: rare and large.
-__device__ __noinline__ void block_slow(Stage& S, const Args A, uint32_t b, uint64_t boff, uint32_t blen) {
+__device__ __noinline__ void block_slow(Stage& S, Meta& Mt, const Args A, uint32_t b, uint64_t boff, uint32_t blen) {
   const int l = lane_id();
   const uint32_t nb = A.in.n_blocks, flags = A.in.flags;
   const pbl_decode_out& O = A.out;
@@ -636,8 +843,8 @@ __device__ __noinline__ void block_slow(Stage& S, const Args A, uint32_t b, uint
   uint64_t dummy[kNumComp] = {0, 0, 0, 0}, excl[kNumComp];
   const uint8_t* src = reinterpret_cast<const uint8_t*>(S.x) + kPad + (boff & 15);
   bool from_lds = true;
-  uint8_t* keybuf = reinterpret_cast<uint8_t*>(S.m0);
-  uint32_t keycap = uint32_t(sizeof(Stage) - offsetof(Stage, m0)) & ~15u;
+  uint8_t* keybuf = reinterpret_cast<uint8_t*>(Mt.m0);
+  uint32_t keycap = uint32_t(sizeof(Meta)) & ~15u;
   slow_walk(src, true, blen, flags, A.in.synthetic_seq_num, keybuf, keycap, kPassCount, O, b, dummy, &ss);
   if (ss.status == PBL_UNSUPPORTED) {
     from_lds = false;
@@ -687,12 +894,37 @@ __device__ __noinline__ void block_big(const Args A, uint32_t b, uint64_t boff, 
 
 // One block on one wave, stage s held on entry and released before return.
 template <bool kHide>
-__device__ __forceinline__ void pool_block(PoolLds& L, uint32_t s, Slot& W, const Args& A, uint32_t b) {
+__device__ __forceinline__ void pool_block(PoolLds& L, const Work& wk, Slot& W, const Args& A) {
+  const uint32_t s = wk.s, b = wk.t;
   Stage& S = L.st[s];
+  // (PBL_POOL_AHEAD) the stage this wave parked, to be marked ready once its
+  // DMA has landed; every exit below marks it
+  uint32_t pend = kNS;
+#if PBL_POOL_AHEAD
+#define PBL_STAGE_DONE()                   \
+  do {                                     \
+    if (park(L, s, A)) pend = s;           \
+  } while (0)
+#define PBL_MARK_PENDING()                 \
+  do {                                     \
+    if (pend < uint32_t(kNS)) {            \
+      mark_ready(L, pend);                 \
+      pend = kNS;                          \
+    }                                      \
+  } while (0)
+#else
+#define PBL_STAGE_DONE() release(L, s)
+#define PBL_MARK_PENDING() do {} while (0)
+#endif
+#if PBL_POOL_EARLY
+  Meta& Mt = W.m;
+#else
+  Meta& Mt = S.m;
+#endif
   const int l = lane_id();
   const uint32_t nb = A.in.n_blocks, flags = A.in.flags;
-  const uint64_t boff = to_glb(A.in.block_off)[b];
-  const uint32_t blen = to_glb(A.in.block_len)[b];
+  const uint64_t boff = wk.boff;
+  const uint32_t blen = wk.blen;
   const bool vprefix = (flags & PBL_ROW_VALUE_PREFIX) && !(flags & PBL_ROW_RAW_KEYS);
   uint8_t* ws = reinterpret_cast<uint8_t*>(A.out.workspace);
   uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
@@ -700,21 +932,15 @@ __device__ __forceinline__ void pool_block(PoolLds& L, uint32_t s, Slot& W, cons
   const pbl_decode_out& O = A.out;
 
   if (blen > kMaxFastLen) {
-    release(L, s);
+    PBL_STAGE_DONE();
     block_big(A, b, boff, blen);
+    PBL_MARK_PENDING();
     return;
   }
 
   PSTAMP(A, b, 1, l == 0);
-  {  // stage: the block by LDS-DMA (granule g of the 16-B aligned range at x[1 + g])
-    const uint64_t a0 = boff & ~uint64_t(15), a1 = (boff + blen + 15) & ~uint64_t(15);
-    const uint32_t n16 = uint32_t((a1 - a0) >> 4);
-    const gptr<const uint8_t> base = to_glb(A.in.blocks + a0);
-    for (uint32_t g0 = 0; g0 < n16; g0 += kWave) {
-      if (g0 + l < n16)
-        __builtin_amdgcn_global_load_lds((gptr<const void>)(base + 16ull * (g0 + l)),
-                                         (lptr<void>)to_lds_ptr(reinterpret_cast<void*>(&S.x[1 + g0])), 16, 0, 0);
-    }
+  if (!wk.staged) {  // the block by LDS-DMA
+    stage_dma(S, A.in.blocks, boff, blen);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync();
   }
@@ -768,37 +994,36 @@ __device__ __forceinline__ void pool_block(PoolLds& L, uint32_t s, Slot& W, cons
       MState M{ie - (kHide ? acc.ne : acc.cnt), ic - acc.cnt, ik - acc.kb, iv - acc.vb, 0, 0, 0};
       if (single) {
         if (r0 < nres) {
-          park_meta<kHide>(S, W, V, RB, flags, M);
-          if (over) span_meta<kHide>(S, W, V, RB.pos, RB.e0, RB.rw, RB.n, RB.prev_kl, RB.prev_kind, flags, vprefix, M);
+          park_meta<kHide>(Mt, W, V, RB, flags, M);
+          if (over) span_meta<kHide>(Mt, W, V, RB.pos, RB.e0, RB.rw, RB.n, RB.prev_kl, RB.prev_kind, flags, vprefix, M);
         }
       } else {
         for (uint32_t r = r0; r < r1; r++) {
           uint32_t rw, e0;
           run_bounds(V, r, nres, roff, &rw, &e0);
           M.prev_sh = M.pp = M.ppsh = 0;
-          span_meta<kHide>(S, W, V, rw & kRestartMask, e0, rw, 0, 0, 0, flags, vprefix, M);
+          span_meta<kHide>(Mt, W, V, rw & kRestartMask, e0, rw, 0, 0, 0, flags, vprefix, M);
         }
       }
       if (l < 5) W.vp[nkv + l] = tvb;
-      if (l == 0) S.kout[nkv] = uint16_t(tkb);
+      if (l == 0) Mt.kout[nkv] = uint16_t(tkb);
       wave_sync();
-#if PBL_POOL_VCOPY != 2
-      // value buckets: the KV holding byte q * 128 of the block's values
-      for (uint32_t j = l; j < nkv; j += kWave) {
-        const uint32_t v0 = W.vp[j] & 0xffffu, v1 = W.vp[j + 1] & 0xffffu;
-        for (uint32_t q = (v0 + 127) >> kVB; (q << kVB) < v1; q++) W.vbkt[q] = uint16_t(j);
-      }
-      wave_sync();
-#endif
       PSTAMP(A, b, 4, l == 0);
     }
   }
 
   if (status == PBL_OK && slow) {
-    block_slow(S, A, b, boff, blen);
-    release(L, s);
+    block_slow(S, Mt, A, b, boff, blen);
+    PBL_STAGE_DONE();
+    PBL_MARK_PENDING();
     return;
   }
+#if PBL_POOL_EARLY
+  PBL_STAGE_DONE();  // everything after this reads the slot and the block in global memory
+  const GSrc KS{to_glb(gblk), blen, uint32_t(((uint64_t(gblk) + blen + 15) & ~uint64_t(15)) - uint64_t(gblk))};
+#else
+  const View& KS = V;
+#endif
 
   const bool okb = status == PBL_OK;
   const uint64_t agg[kNumComp] = {okb ? nkv : 0, okb ? tkb : 0, okb ? tvb : 0, okb ? nres : 0};
@@ -808,6 +1033,7 @@ __device__ __forceinline__ void pool_block(PoolLds& L, uint32_t s, Slot& W, cons
     if (b > 0) G.issue(LbPtrs(lb_state, nb), int64_t(b) - 1);
   }
   lb_finish(lb_state, nb, b, agg, excl, &O.totals->status_mask, G);
+  PBL_MARK_PENDING();
   PSTAMP(A, b, 5, l == 0);
   if (okb && overflows(O, excl, agg)) status = PBL_OVERFLOW;
   if (l == 0) {
@@ -818,53 +1044,37 @@ __device__ __forceinline__ void pool_block(PoolLds& L, uint32_t s, Slot& W, cons
     write_block_meta(O, b, nb, status, excl, agg, false);
   }
   if (status != PBL_OK) {
-    release(L, s);
+    if (!PBL_POOL_EARLY) release(L, s);
     return;
   }
   if (nkv == 0) {  // a block with no entries: its lone N+1 offsets
     if (l == 0) {
-      S.kout[0] = 0;
+      Mt.kout[0] = 0;
       W.vp[0] = 0;
     }
     wave_sync();
   }
 
-  // ---- keys and per-KV arrays from the stage: lane per KV --------------------
+  // ---- keys and per-KV arrays: lane per KV ------------------------------------
   const uint64_t kvb = excl[0], kbb = excl[1], vbb = excl[2], rbb = excl[3];
-  const gptr<uint8_t> kbytes = to_glb(O.key_bytes) + kbb;
-  const bool raw = (flags & PBL_ROW_RAW_KEYS) != 0;
-  for (uint32_t j = l; j <= nkv; j += kWave) {
-    to_glb(O.key_off)[kvb + b + j] = S.kout[j];
-    to_glb(O.val_off)[kvb + b + j] = W.vp[j] & 0xffffu;
-    if (j < nkv) {
-      const uint32_t e = kHide ? uint32_t(S.ent[j]) : j;
-      const uint64_t m = S.m0[e];
-      uint8_t fl = S.kvf[j];
-      to_glb(O.trailer)[kvb + j] = with_seq(trailer_of(S, V, int(e), m, &fl, flags), A.in.synthetic_seq_num, flags);
-      if (O.kv_flags) to_glb(O.kv_flags)[kvb + j] = fl;
-      if (O.entry_off) to_glb(O.entry_off)[kvb + j] = S.eoff[j];
-      const uint32_t ukl = raw ? m_klen(m) : (m_klen(m) >= 8 ? m_klen(m) - 8 : 0u);
-      const uint32_t ko = S.kout[j];
-      for (uint32_t c = 0; c < ukl; c += 16) {
-        const uint32_t n = ukl - c < 16 ? ukl - c : 16u;
-        store_n(kbytes + ko + c, key_chunk(S, V, m, c, n), n);
-      }
-    }
-  }
+#if PBL_POOL_EARLY
+  emit_keys_glb<kHide>(Mt, W, KS, A, b, nkv, kvb, kbb);
+#else
+  emit_keys<kHide>(Mt, W, KS, A, b, nkv, kvb, kbb);
+#endif
   if (O.restarts)
-    for (uint32_t r = l; r < nres; r += kWave) to_glb(O.restarts)[rbb + r] = V.le32(roff + 4 * r);
-  release(L, s);
+    for (uint32_t r = l; r < nres; r += kWave) to_glb(O.restarts)[rbb + r] = KS.le32(roff + 4 * r);
+  if (!PBL_POOL_EARLY) release(L, s);
   PSTAMP(A, b, 6, l == 0);
 
   // ---- values, global -> global --------------------------------------------
-#if PBL_POOL_VCOPY == 2
   if (tvb) copy_values_grp(W, to_glb(gblk), nkv, to_glb(O.val_bytes) + vbb);
-#else
-  if (tvb) copy_values(W, to_glb(gblk), blen, vbb, tvb, to_glb(O.val_bytes));
-#endif
   PSTAMP(A, b, 7, l == 0);
   wave_sync();  // (the slot is the next block's)
 }
+
+#undef PBL_STAGE_DONE
+#undef PBL_MARK_PENDING
 
 // The persistent kernel: one workgroup of kNW waves per CU, each wave an
 // independent loop of (acquire a stage, take a ticket, decode the block).
@@ -874,21 +1084,45 @@ __device__ __forceinline__ void pool_block(PoolLds& L, uint32_t s, Slot& W, cons
 template <bool kHide>
 __global__ void __launch_bounds__(kTPBP, 1) rowblk_pool_kernel(Args A) {
   __shared__ PoolLds L;
-  if (threadIdx.x == 0) L.free_mask = (1u << kNS) - 1u;
+  if (threadIdx.x == 0) {
+    L.free_mask = (1u << kNS) - 1u;
+    L.inflight = 0;
+  }
+  if (threadIdx.x < uint32_t(kNS)) {
+    L.tk[threadIdx.x] = kTkFree;
+    L.rdy[threadIdx.x] = 0;
+  }
   __syncthreads();
   Slot& W = L.sl[wave_id()];
   const uint32_t nb = A.in.n_blocks;
+#if PBL_POOL_AHEAD
+  static_assert(PBL_POOL_EARLY, "the stage ring parks a stage right after the walk");
+  for (;;) {
+#ifdef PBL_STAMPS
+    const uint64_t t_acq = __builtin_amdgcn_s_memtime();
+#endif
+    const Work wk = get_work(L, A);
+    if (wk.t >= nb) break;
+    PSTAMP(A, wk.t, 0, lane_id() == 0);
+#ifdef PBL_STAMPS
+    if (lane_id() == 0)
+      reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(A.out.workspace) + ws_bytes(nb))[uint64_t(wk.t) * 16 + 8] = t_acq;
+#endif
+    pool_block<kHide>(L, wk, W, A);
+  }
+#else
   uint32_t* tick = reinterpret_cast<uint32_t*>(A.out.workspace);
   for (;;) {
 #ifdef PBL_STAMPS
     const uint64_t t_acq = __builtin_amdgcn_s_memtime();
 #endif
-    const uint32_t s = acquire(L);
+    Work wk;
+    wk.s = acquire(L);
     uint32_t t0 = 0;
     if (lane_id() == 0) t0 = g_atomic_add(tick, 1u);
     t0 = __builtin_amdgcn_readfirstlane(__shfl(t0, 0, kWave));
     if (t0 >= nb) {
-      release(L, s);
+      release(L, wk.s);
       break;
     }
     PSTAMP(A, t0, 0, lane_id() == 0);
@@ -896,8 +1130,13 @@ __global__ void __launch_bounds__(kTPBP, 1) rowblk_pool_kernel(Args A) {
     if (lane_id() == 0)
       reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(A.out.workspace) + ws_bytes(nb))[uint64_t(t0) * 16 + 8] = t_acq;
 #endif
-    pool_block<kHide>(L, s, W, A, t0);
+    wk.t = t0;
+    wk.boff = to_glb(A.in.block_off)[t0];
+    wk.blen = to_glb(A.in.block_len)[t0];
+    wk.staged = false;
+    pool_block<kHide>(L, wk, W, A);
   }
+#endif
 }
 
 }  // namespace pool

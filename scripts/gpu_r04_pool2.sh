@@ -3,7 +3,7 @@
 # SQ PMC passes.
 set -o pipefail
 O=gpurun_out/r04/pool2; mkdir -p $O
-PBL_LIB=exp/pool_p16.so timeout -k 10 300 python -u -m pytest tests/test_flat_gpu.py -k pool -x -q --timeout 200 --timeout-method thread > $O/pytest_p16.log 2>&1; rc=$?; tail -2 $O/pytest_p16.log
+timeout -k 10 300 python -u -m pytest tests/test_flat_gpu.py tests/test_hide_fused_gpu.py -k 'pool or hide or fused or random or general or past or config2 or colblk' -x -q --timeout 200 --timeout-method thread > $O/pytest_p16.log 2>&1; rc=$?; tail -2 $O/pytest_p16.log
 [ $rc -eq 0 ] || { grep -E "Error|assert|differs|FAIL" $O/pytest_p16.log | head -30; exit $rc; }
 B="timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e"
 for v in p16 p16v1 p12; do PBL_LIB=exp/pool_$v.so $B --kernel pool > $O/bench_$v.json 2>$O/bench_$v.err || exit 1; done

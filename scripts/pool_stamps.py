@@ -3,7 +3,8 @@
 PBL_LIB=<diag .so>) on a config-2 batch.  Stamps (rowblk_pool.hip.h): 8
 acquire start, 0 stage acquired + ticket, 1 descriptor read, 2 staged (DMA
 landed), 3 walk + scan + publish, 4 metadata + value buckets, 5 look-back
-resolved, 6 keys / per-KV arrays written and stage released, 7 values done.
+resolved, 6 keys / per-KV arrays written (and the stage released, unless
+PBL_POOL_EARLY released it at 4), 7 values done.
 Read the shares; the stamps perturb timing."""
 import os
 import sys
@@ -27,8 +28,8 @@ ws_state = 256 + 10 * nb * 8
 st = out.workspace[ws_state: ws_state + nb * 16 * 8].view(torch.int64).view(nb, 16).cpu().numpy()
 phases = [("acquire stage + ticket", 8, 0), ("descriptor", 0, 1), ("stage (DMA round trip)", 1, 2),
           ("walk + scan + publish", 2, 3), ("metadata + buckets", 3, 4), ("look-back finish", 4, 5),
-          ("keys + per-KV (stage held)", 5, 6), ("values (global)", 6, 7), ("stage held", 0, 6),
-          ("block total", 8, 7)]
+          ("keys + per-KV", 5, 6), ("values (global)", 6, 7), ("stage held (keys from the stage)", 0, 6),
+          ("stage held (PBL_POOL_EARLY)", 0, 4), ("block total", 8, 7)]
 for nm, a, z in phases:
     m = (st[:, a] > 0) & (st[:, z] > 0)
     d = (st[m, z] - st[m, a]).astype(np.float64)
