@@ -64,8 +64,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the host->device->host (PCIe-inclusive) pass")
     p.add_argument("--e2e-chunk", type=int, default=2048, help="blocks per PCIe pipeline chunk")
-    p.add_argument("--kernel", choices=["auto", "single", "pipe", "flat", "global", "pool"], default="auto",
-                   help="A/B: PBL_KERNEL_SINGLE / PBL_KERNEL_PIPE / PBL_KERNEL_FLAT batch flags")
+    p.add_argument("--kernel", choices=["auto", "single", "pipe", "pool"], default="auto",
+                   help="A/B: PBL_KERNEL_SINGLE / PBL_KERNEL_PIPE batch flags (auto = pool for row batches)")
     p.add_argument("--launch-check", action="store_true",
                    help="launcher self-test without a GPU: N gloo ranks report in, rank 0 prints one JSON line")
     p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
@@ -246,7 +246,8 @@ def main():
 
     nb = a.blocks or (131072 if a.workload == "mixed" else 65536)
     flags = N.PBL_ROW_VALUE_PREFIX if a.value_prefix else 0
-    flags |= {"auto": 0, "single": N.PBL_KERNEL_SINGLE, "pipe": N.PBL_KERNEL_PIPE, "flat": N.PBL_KERNEL_FLAT, "global": N.PBL_KERNEL_GLOBAL, "pool": N.PBL_KERNEL_POOL}[a.kernel]
+    flags |= {"auto": 0, "single": N.PBL_KERNEL_SINGLE, "pipe": N.PBL_KERNEL_PIPE, "pool": N.PBL_KERNEL_POOL}[a.kernel]
+    row_kernel = {"single": "rowblk_decode_kernel", "pipe": "rowblk_pipe_kernel"}.get(a.kernel, "rowblk_pool_kernel")
     seed = a.seed + 7919 * rank
     t0 = time.time()
     block_fmt = None
@@ -254,21 +255,17 @@ def main():
         fmt = N.PBL_FMT_ROW
         buf, off, lens, n_kv = gen_row_blocks(seed, nb, a.block_size, a.restart_interval, a.key_len, a.val_len,
                                               a.value_prefix, n_threads=16)
-        kernel = {"single": "rowblk_decode_kernel", "flat": "rowblk_flat_kernel", "pool": "rowblk_pool_kernel",
-                  "global": "glb_sizes_kernel+glb_scan_kernel+glb_values_kernel"}.get(a.kernel, "rowblk_pipe_kernel")
+        kernel = row_kernel
         if a.workload == "transform":
             kernel = "tf_count_kernel+tf_scan_kernel+tf_scatter_kernel"
         wl = ("transform pass (SyntheticSeqNum, HideObsoletePoints, 12 B SyntheticPrefix) over " if a.workload ==
               "transform" else "") + (f"config2: {nb} x {a.block_size // 1024} KiB row-format blocks per GPU, restart interval "
               f"{a.restart_interval}, {a.key_len} B keys / {a.val_len} B values" + (", value prefix" if a.value_prefix else ""))
     elif a.workload == "rowmix":
-        from pebble_amd.batch import gen_row_mix, varlen_hint
+        from pebble_amd.batch import gen_row_mix
         fmt = N.PBL_FMT_ROW
         buf, off, lens, n_kv = gen_row_mix(seed, nb, a.mix, n_threads=16)
-        vl = varlen_hint(lens) and a.kernel == "auto"
-        kernel = ("glb_sizes_kernel+glb_scan_kernel+glb_values_kernel" if a.kernel == "global" or vl else
-                  {"single": "rowblk_decode_kernel", "flat": "rowblk_flat_kernel", "pool": "rowblk_pool_kernel"}.get(
-                      a.kernel, "rowblk_pipe_kernel"))
+        kernel = row_kernel
         wl = (f"row-shape mix: {nb} row blocks per GPU, config-2 blocks with " +
               ("every 10th a config-5 Zipf block (restart interval 16)" if a.mix == "zipf10" else
                "every 8th a short table-tail block (2 / 4 / 8 KiB)"))
@@ -283,15 +280,10 @@ def main():
         fmt = N.PBL_FMT_ROW if a.zipf_format == "row" else N.PBL_FMT_COL_DEFAULT
         buf, off, lens, n_kv = gen_zipf_blocks(seed, nb, fmt, a.restart_interval, a.block_size, n_threads=16)
         from pebble_amd.batch import varlen_hint
-        # (a Zipf colblk batch carries PBL_BATCH_VARLEN: one-block-per-workgroup kernel)
-        # (a VARLEN row batch is walked from HBM, a VARLEN colblk batch takes the
-        # one-block-per-workgroup kernel, unless --kernel names another)
+        # (a VARLEN colblk batch takes the one-block-per-workgroup kernel unless
+        # --kernel names another; row batches ignore the hint)
         vl = varlen_hint(lens) and a.kernel not in ("pipe", "single")
-        kernel = (("glb_sizes_kernel+glb_scan_kernel+glb_values_kernel" if a.kernel == "global" or
-                   (vl and a.kernel == "auto") else
-                   "rowblk_pool_kernel" if a.kernel == "pool" else
-                   "rowblk_flat_kernel" if a.kernel == "flat" else
-                   "rowblk_decode_kernel" if a.kernel == "single" else "rowblk_pipe_kernel") if fmt == N.PBL_FMT_ROW
+        kernel = (row_kernel if fmt == N.PBL_FMT_ROW
                   else "colblk_decode_kernel" if vl or a.kernel == "single" else "colblk_pipe_kernel")
         wl = (f"config5: {nb} variable-length blocks per GPU targeting {a.block_size // 1024} KiB, "
               + (f"row format, restart interval {a.restart_interval}" if fmt == N.PBL_FMT_ROW

@@ -90,25 +90,22 @@ enum {
                                      lengths vary widely (e.g. Zipf value sizes), so a
                                      colblk batch takes the one-block-per-workgroup
                                      kernel, whose look-back does not convoy behind
-                                     long blocks, and a row batch is walked from HBM
-                                     by a wave per block (rowblk_global.hip.h).
-                                     The caller knows the lengths on the host
-                                     (block handles carry them).                   */
+                                     long blocks.  Row batches ignore it: their
+                                     kernel picks a path per block.  The caller knows
+                                     the lengths on the host (block handles carry
+                                     them).                                        */
 #define PBL_KERNEL_SINGLE 0x200u  /* A/B measurement, no effect on results: the
                                      one-block-per-workgroup kernels instead of the
-                                     persistent pipelines                          */
-#define PBL_KERNEL_PIPE 0x400u    /* A/B measurement, no effect on results: the
-                                     pipelines even for a PBL_BATCH_VARLEN batch   */
-#define PBL_KERNEL_FLAT 0x800u    /* A/B measurement, no effect on results: row
-                                     batches on the one-wave-per-block kernel
-                                     (rowblk_flat.hip.h) even without VARLEN        */
-/* 0x1000u: retired (the run-major row kernel, removed; the bit is ignored)       */
-#define PBL_KERNEL_GLOBAL 0x2000u /* A/B measurement, no effect on results: row
-                                     batches walked from HBM by a wave per block in
-                                     three launches (rowblk_global.hip.h)           */
-#define PBL_KERNEL_POOL 0x4000u   /* A/B measurement, no effect on results: row
-                                     batches on the staging-pool kernel
-                                     (rowblk_pool.hip.h)                            */
+                                     persistent ones                               */
+#define PBL_KERNEL_PIPE 0x400u    /* A/B measurement, no effect on results: row
+                                     batches on the two-stage pipeline
+                                     (rowblk_pipe.hip.h), colblk batches on theirs
+                                     even with PBL_BATCH_VARLEN                    */
+/* 0x800u, 0x1000u, 0x2000u: retired A/B kernels (one-wave-per-block flat, run-
+   major, HBM-walking row kernels; removed, the bits are ignored)               */
+#define PBL_KERNEL_POOL 0x4000u   /* row batches on the staging-pool kernel
+                                     (rowblk_pool.hip.h): the default; the bit is
+                                     accepted for older callers                    */
 
 /* per-KV flag byte (kv_flags[]) */
 #define PBL_KV_RESTART 0x01u       /* entry offset is a restart point            */

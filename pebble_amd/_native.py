@@ -55,8 +55,6 @@ PBL_BATCH_VARLEN = 0x100
 PBL_ROW_HIDE_OBSOLETE = 0x8
 PBL_KERNEL_SINGLE = 0x200
 PBL_KERNEL_PIPE = 0x400
-PBL_KERNEL_FLAT = 0x800
-PBL_KERNEL_GLOBAL = 0x2000
 PBL_KERNEL_POOL = 0x4000
 
 PBL_KV_RESTART = 0x01

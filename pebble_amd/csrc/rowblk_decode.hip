@@ -799,9 +799,7 @@ __global__ void __launch_bounds__(kTPB, 3) rowblk_decode_kernel(Args A) {
 }
 
 #include "rowblk_pipe.hip.h"
-#include "rowblk_flat.hip.h"
 #include "rowblk_pool.hip.h"
-#include "rowblk_global.hip.h"
 
 // Mixed row + colblk batch (config 4): per-block format from block_format[];
 // both paths share the ticket order and the look-back state.
@@ -1067,38 +1065,6 @@ uint64_t persistent_grid(hipStream_t st, PersistentKernel k, const void* fn, uin
 }  // namespace pbl
 
 namespace {
-// Row batches take the flat kernel when asked (PBL_KERNEL_FLAT) or when their
-// block lengths vary widely (PBL_BATCH_VARLEN, unless PBL_KERNEL_PIPE): on
-// config 5 it measured 542 / 499 / 619 GiB/s against the pipeline's 495 / 340 /
-// 598 at restart intervals 16 / 32 / 1 (profiles/r03/zipf_ab_*.json).
-bool use_flat(uint32_t flags) { return (flags & PBL_KERNEL_FLAT) != 0; }
-// VARLEN row batches (unless an A/B flag names a kernel) are walked from HBM
-// (rowblk_global.hip.h): config 5 574 / 584 / 551 GiB/s at restart intervals
-// 16 / 32 / 1 against the flat kernel's 541 / 499 / 614
-// (profiles/r03_final/ab_zipf_global_*.json, bench_zipf_ri*.json).
-bool use_global(uint32_t flags) {
-  return (flags & PBL_KERNEL_GLOBAL) ||
-         ((flags & PBL_BATCH_VARLEN) && !(flags & (PBL_KERNEL_PIPE | PBL_KERNEL_FLAT | PBL_KERNEL_POOL)));
-}
-
-// Row batches on the flat kernel (rowblk_flat.hip.h): blocks past its length
-// limit are sized before it and written after it (values = false: the size pass).
-int launch_row_flat(const pbl::Args& a, hipStream_t st, bool values) {
-  const uint32_t nb = a.in.n_blocks;
-  int cus = 0;
-  const uint64_t grid = pbl::persistent_grid(st, pbl::kKRowFlat,
-                                             reinterpret_cast<const void*>(pbl::row::flat::rowblk_flat_kernel),
-                                             (uint64_t(nb) + pbl::row::flat::kFW - 1) / pbl::row::flat::kFW, &cus,
-                                             pbl::row::flat::kFTPB);
-  if (!grid) return PBL_DEVICE_ERROR;
-  const uint32_t small = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4));
-  hipLaunchKernelGGL(pbl::row::pipe::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
-  hipLaunchKernelGGL(pbl::row::flat::rowblk_flat_kernel, dim3(uint32_t(grid)), dim3(pbl::row::flat::kFTPB), 0, st,
-                     a);
-  if (values) hipLaunchKernelGGL(pbl::row::pipe::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
-  return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
-}
-
 // Row batches on the staging-pool kernel (rowblk_pool.hip.h), with the same
 // big-block passes around it.
 int launch_row_pool(const pbl::Args& a, hipStream_t st, bool values) {
@@ -1129,29 +1095,6 @@ int launch_row_pool(const pbl::Args& a, hipStream_t st, bool values) {
 bool hide_row(const pbl_block_batch* b) {
   return (b->flags & PBL_ROW_HIDE_OBSOLETE) && !(b->flags & PBL_ROW_RAW_KEYS) && !b->block_format &&
          b->format == PBL_FMT_ROW;
-}
-
-// Row batches walked from HBM (rowblk_global.hip.h): sizes, the 32 KiB-key
-// sizes, the tile scan, then (values) the outputs.
-int launch_row_global(const pbl::Args& a, hipStream_t st, bool values) {
-  const uint32_t nb = a.in.n_blocks;
-  int dev = 0, cus = 0;
-  if (hipStreamGetDevice(st, &dev) != hipSuccess && hipGetDevice(&dev) != hipSuccess) return PBL_DEVICE_ERROR;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-    return PBL_DEVICE_ERROR;
-  // (the size walk takes 35 VGPRs: 8 waves per SIMD; the values walk 117: 4)
-  const uint32_t walk = uint32_t(std::min<uint64_t>(nb, uint64_t(cus) * 32));
-  const uint32_t vwalk = uint32_t(std::min<uint64_t>(nb, uint64_t(cus) * 4 * PBL_GLB_WAVES));
-  const uint32_t small = uint32_t(std::min<uint64_t>((uint64_t(nb) + pbl::kWave - 1) / pbl::kWave, uint64_t(cus) * 4));
-  const uint32_t tiles = uint32_t(std::min<uint64_t>(pbl::row::glb::glb_tiles(nb), uint64_t(cus)));
-  hipLaunchKernelGGL(pbl::row::glb::glb_sizes_kernel, dim3(walk), dim3(pbl::kWave), 0, st, a);
-  hipLaunchKernelGGL(pbl::row::glb::glb_sizes_big_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
-  hipLaunchKernelGGL(pbl::row::glb::glb_scan_kernel, dim3(tiles), dim3(pbl::kTPB), 0, st, a);
-  if (values) {
-    hipLaunchKernelGGL(pbl::row::glb::glb_values_kernel, dim3(vwalk), dim3(pbl::kWave), 0, st, a);
-    hipLaunchKernelGGL(pbl::row::glb::glb_values_big_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
-  }
-  return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }
 
 // Mixed batches: PBL_KERNEL_SINGLE keeps the one-block-per-workgroup kernel
@@ -1219,14 +1162,12 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
     const int rc = launch_mixed(batch, a, st, batch->flags & PBL_KERNEL_SINGLE, true);
     if (rc != PBL_OK) return rc;
   } else {
-    // persistent grid: as many workgroups as can be resident (never more than
-    // blocks).  PBL_KERNEL_SINGLE selects the one-block-per-workgroup
-    // persistent kernel (kept for A/B measurement); the default is the pipeline.
+    // Row batches take the staging-pool kernel (every block shape: the fast
+    // path, the general walk, the big-block passes around it; HideObsoletePoints
+    // fused).  PBL_KERNEL_SINGLE / PBL_KERNEL_PIPE keep the one-block-per-
+    // workgroup kernel and the two-stage pipeline for A/B measurement.
     const bool single = (batch->flags & PBL_KERNEL_SINGLE) != 0;
-    if (hide_row(batch)) return launch_row_pool(a, st, true);
-    if (!single && use_global(batch->flags)) return launch_row_global(a, st, true);
-    if (!single && (batch->flags & PBL_KERNEL_POOL)) return launch_row_pool(a, st, true);
-    if (!single && use_flat(batch->flags)) return launch_row_flat(a, st, true);
+    if (hide_row(batch) || !(batch->flags & (PBL_KERNEL_SINGLE | PBL_KERNEL_PIPE))) return launch_row_pool(a, st, true);
     const void* fn = single ? reinterpret_cast<const void*>(pbl::row::rowblk_decode_kernel)
                             : reinterpret_cast<const void*>(pbl::row::pipe::rowblk_pipe_kernel);
     int cus = 0;
@@ -1291,17 +1232,8 @@ int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stre
     if (batch->block_format) {
       rc = launch_mixed(batch, a, st, batch->flags & PBL_KERNEL_SINGLE, false);
       if (rc != PBL_OK) return rc;
-    } else if (hide_row(batch)) {
+    } else if (hide_row(batch) || !(batch->flags & PBL_KERNEL_PIPE)) {
       rc = launch_row_pool(a, st, false);
-      if (rc != PBL_OK) return rc;
-    } else if (use_global(batch->flags)) {
-      rc = launch_row_global(a, st, false);
-      if (rc != PBL_OK) return rc;
-    } else if (batch->flags & PBL_KERNEL_POOL) {
-      rc = launch_row_pool(a, st, false);
-      if (rc != PBL_OK) return rc;
-    } else if (use_flat(batch->flags)) {
-      rc = launch_row_flat(a, st, false);
       if (rc != PBL_OK) return rc;
     } else {
       int cus = 0;

@@ -43,19 +43,22 @@
 namespace pool {
 
 #ifndef PBL_POOL_WAVES
-#define PBL_POOL_WAVES 16
+#define PBL_POOL_WAVES 8
 #endif
 #ifndef PBL_POOL_STAGES
 #define PBL_POOL_STAGES 3
 #endif
 #ifndef PBL_POOL_EARLY
-#define PBL_POOL_EARLY 0  // 1: the per-KV metadata in the wave's slot; the stage is released after the walk
+#define PBL_POOL_EARLY 1  // 1: the per-KV metadata in the wave's slot; the stage is released after the walk
 #endif
 #ifndef PBL_POOL_AHEAD
 #define PBL_POOL_AHEAD 0  // 1 (with PBL_POOL_EARLY): a released stage is refilled at once with the next ticket's block
 #endif
 #ifndef PBL_POOL_SLEEP
-#define PBL_POOL_SLEEP 1  // s_sleep units (64 cycles) between polls of the stage mask
+#define PBL_POOL_SLEEP 8  // s_sleep units (64 cycles) between polls of the stage mask
+#endif
+#ifndef PBL_POOL_PARKPRIO
+#define PBL_POOL_PARKPRIO 0
 #endif
 #ifndef PBL_POOL_PRIO
 #define PBL_POOL_PRIO 2  // the stage holder's issue priority (values run at 0)
@@ -501,83 +504,115 @@ __device__ __forceinline__ void emit_keys(const Meta& Mt, const Slot& W, const S
 #define PBL_POOL_KU 3
 #endif
 constexpr int kKU = PBL_POOL_KU;
+// One batch of the key emit: kKU KVs per lane, j = j0 + kWave * u + lane.
+// Only what the loads produced (and the metadata words they were addressed
+// by) is held between the loads and the stores; the rest is re-read from the
+// slot at store time (cheaper than the registers across a look-back wait).
+struct KBatch {
+  uint64_t m[kKU], mp[kKU], tr[kKU];
+  uint4 ka[kKU], kp[kKU];
+};
+
+__device__ __forceinline__ bool key_fast(uint64_t m, uint64_t mp, bool raw) {
+  const uint32_t kl = m_klen(m), sh = m_sh(m), ukl = raw ? kl : (kl >= 8 ? kl - 8 : 0u);
+  return ukl <= 16 && (sh == 0 || m_sh(mp) == 0) && (raw || kl < 8 || kl - 8 >= sh);
+}
+
+// The batch's metadata words from the slot, then every global load it needs.
 template <bool kHide>
-__device__ __forceinline__ void emit_keys_glb(const Meta& Mt, const Slot& W, const GSrc& V, const Args& A, uint32_t b,
-                                              uint32_t nkv, uint64_t kvb, uint64_t kbb) {
+__device__ __forceinline__ void key_load(const Meta& Mt, const GSrc& V, bool raw, uint32_t j0, uint32_t nkv,
+                                         KBatch& K) {
+  const int l = lane_id();
+#pragma unroll
+  for (int u = 0; u < kKU; u++) {
+    const uint32_t j = j0 + kWave * u + l;
+    const uint32_t e = kHide ? (j < nkv ? uint32_t(Mt.ent[j]) : 0u) : j;
+    K.m[u] = j < nkv ? Mt.m0[e] : 0ull;
+    K.mp[u] = (j < nkv && m_sh(K.m[u]) != 0) ? Mt.m0[m_par(K.m[u])] : 0ull;
+  }
+#pragma unroll
+  for (int u = 0; u < kKU; u++) {
+    const uint32_t j = j0 + kWave * u + l;
+    const uint64_t m = K.m[u];
+    const uint32_t kl = m_klen(m), sh = m_sh(m), ukl = raw ? kl : (kl >= 8 ? kl - 8 : 0u);
+    const bool fast = j < nkv && key_fast(m, K.mp[u], raw);
+    K.tr[u] = 0;
+    if (fast && !raw && kl >= 8) K.tr[u] = V.ld8(m_ksrc(m) + (kl - 8 - sh));
+    if (fast && ukl) K.ka[u] = V.ld16(int32_t(m_ksrc(m)) - int32_t(sh));
+    if (fast && ukl && sh) K.kp[u] = V.ld16(int32_t(m_ksrc(K.mp[u])));
+  }
+}
+
+// The batch's merges and stores (the general form for KVs off the fast form).
+template <bool kHide>
+__device__ __forceinline__ void key_store(const Meta& Mt, const Slot& W, const GSrc& V, const Args& A, uint32_t b,
+                                          uint32_t j0, uint32_t nkv, uint64_t kvb, uint64_t kbb, const KBatch& K) {
   const int l = lane_id();
   const uint32_t flags = A.in.flags;
   const pbl_decode_out& O = A.out;
   const gptr<uint8_t> kbytes = to_glb(O.key_bytes) + kbb;
   const bool raw = (flags & PBL_ROW_RAW_KEYS) != 0;
-  for (uint32_t j0 = 0; j0 <= nkv; j0 += kWave * kKU) {
-    uint32_t ko[kKU], vo[kKU], eo[kKU], ukl[kKU], sh[kKU], e[kKU];
-    uint64_t m[kKU], mp[kKU];
-    uint8_t fl[kKU];
-    bool fast[kKU];
 #pragma unroll
-    for (int u = 0; u < kKU; u++) {
-      const uint32_t j = j0 + kWave * u + l;
-      ko[u] = j <= nkv ? uint32_t(Mt.kout[j]) : 0u;
-      vo[u] = j <= nkv ? (W.vp[j] & 0xffffu) : 0u;
-      e[u] = kHide ? (j < nkv ? uint32_t(Mt.ent[j]) : 0u) : j;
-      m[u] = j < nkv ? Mt.m0[e[u]] : 0ull;
-      fl[u] = j < nkv ? Mt.kvf[j] : uint8_t(0);
-      eo[u] = j < nkv ? uint32_t(Mt.eoff[j]) : 0u;
-      const uint32_t kl = m_klen(m[u]);
-      sh[u] = m_sh(m[u]);
-      ukl[u] = raw ? kl : (kl >= 8 ? kl - 8 : 0u);
-      mp[u] = (j < nkv && sh[u] != 0) ? Mt.m0[m_par(m[u])] : 0ull;
-      fast[u] = ukl[u] <= 16 && (sh[u] == 0 || m_sh(mp[u]) == 0) && (raw || kl < 8 || kl - 8 >= sh[u]);
-    }
-    uint64_t tr[kKU];
-    uint4 ka[kKU], kp[kKU];
-#pragma unroll
-    for (int u = 0; u < kKU; u++) {
-      const uint32_t j = j0 + kWave * u + l;
-      const uint32_t kl = m_klen(m[u]);
-      tr[u] = 0;
-      if (j < nkv && fast[u] && !raw && kl >= 8) tr[u] = V.ld8(m_ksrc(m[u]) + (kl - 8 - sh[u]));
-      if (j < nkv && fast[u] && ukl[u]) ka[u] = V.ld16(int32_t(m_ksrc(m[u])) - int32_t(sh[u]));
-      if (j < nkv && fast[u] && ukl[u] && sh[u]) kp[u] = V.ld16(int32_t(m_ksrc(mp[u])));
-    }
-#pragma unroll
-    for (int u = 0; u < kKU; u++) {
-      const uint32_t j = j0 + kWave * u + l;
-      if (j > nkv) continue;
-      to_glb(O.key_off)[kvb + b + j] = ko[u];
-      to_glb(O.val_off)[kvb + b + j] = vo[u];
-      if (j == nkv) continue;
-      uint64_t t;
-      uint8_t f = fl[u];
-      if (!fast[u]) {
-        t = trailer_of(Mt, V, int(e[u]), m[u], &f, flags);
-        for (uint32_t c = 0; c < ukl[u]; c += 16) {
-          const uint32_t n = ukl[u] - c < 16 ? ukl[u] - c : 16u;
-          store_n(kbytes + ko[u] + c, key_chunk(Mt, V, m[u], c, n), n);
-        }
-      } else {
-        const uint32_t kl = m_klen(m[u]);
-        if (raw) t = 0;
-        else if (kl < 8) t = kKindInvalid;
-        else {
-          if (tr[u] & 64u) f |= PBL_KV_OBSOLETE;
-          t = tr[u] & kTrailerObsoleteMask;
-        }
-        if (ukl[u]) {
-          const uint32_t n = ukl[u], lo = sh[u] < n ? sh[u] : n;
-          uint4 w = ka[u];
-          if (lo) {
-            w = make_uint4(0, 0, 0, 0);
-            merge16(w, ka[u], lo, n);
-            merge16(w, kp[u], 0, lo);
-          }
-          store_n(kbytes + ko[u], w, n);
-        }
+  for (int u = 0; u < kKU; u++) {
+    const uint32_t j = j0 + kWave * u + l;
+    if (j > nkv) continue;
+    const uint32_t ko = Mt.kout[j];
+    to_glb(O.key_off)[kvb + b + j] = ko;
+    to_glb(O.val_off)[kvb + b + j] = W.vp[j] & 0xffffu;
+    if (j == nkv) continue;
+    const uint64_t m = K.m[u];
+    const uint32_t kl = m_klen(m), sh = m_sh(m), ukl = raw ? kl : (kl >= 8 ? kl - 8 : 0u);
+    uint64_t t;
+    uint8_t f = Mt.kvf[j];
+    if (!key_fast(m, K.mp[u], raw)) {
+      const uint32_t e = kHide ? uint32_t(Mt.ent[j]) : j;
+      t = trailer_of(Mt, V, int(e), m, &f, flags);
+      for (uint32_t c = 0; c < ukl; c += 16) {
+        const uint32_t n = ukl - c < 16 ? ukl - c : 16u;
+        store_n(kbytes + ko + c, key_chunk(Mt, V, m, c, n), n);
       }
-      to_glb(O.trailer)[kvb + j] = with_seq(t, A.in.synthetic_seq_num, flags);
-      if (O.kv_flags) to_glb(O.kv_flags)[kvb + j] = f;
-      if (O.entry_off) to_glb(O.entry_off)[kvb + j] = eo[u];
+    } else {
+      if (raw) t = 0;
+      else if (kl < 8) t = kKindInvalid;
+      else {
+        if (K.tr[u] & 64u) f |= PBL_KV_OBSOLETE;
+        t = K.tr[u] & kTrailerObsoleteMask;
+      }
+      if (ukl) {
+        const uint32_t lo = sh < ukl ? sh : ukl;
+        uint4 w = K.ka[u];
+        if (lo) {
+          w = make_uint4(0, 0, 0, 0);
+          merge16(w, K.ka[u], lo, ukl);
+          merge16(w, K.kp[u], 0, lo);
+        }
+        store_n(kbytes + ko, w, ukl);
+      }
     }
+    to_glb(O.trailer)[kvb + j] = with_seq(t, A.in.synthetic_seq_num, flags);
+    if (O.kv_flags) to_glb(O.kv_flags)[kvb + j] = f;
+    if (O.entry_off) to_glb(O.entry_off)[kvb + j] = Mt.eoff[j];
+  }
+}
+
+// emit_keys for the block in GLOBAL memory (PBL_POOL_EARLY): the loads are
+// L2 / MALL round trips, so kKU KVs per lane go through three phases together:
+// their metadata from the slot, then every global load (the trailer's 8 bytes;
+// the user key's segments: its own unshared bytes and, for a key that shares
+// a prefix, its prefix parent's bytes), then the merges and stores.  The fast
+// form covers keys of at most 16 bytes whose prefix chain ends at the parent
+// (a restart-interval row block: the parent is the run's first key) with the
+// trailer in the entry's own bytes; the rest take emit_keys' general form.
+// The first batch (K) was loaded by the caller, before its look-back wait.
+template <bool kHide>
+__device__ __forceinline__ void emit_keys_glb(const Meta& Mt, const Slot& W, const GSrc& V, const Args& A, uint32_t b,
+                                              uint32_t nkv, uint64_t kvb, uint64_t kbb, const KBatch& K) {
+  const bool raw = (A.in.flags & PBL_ROW_RAW_KEYS) != 0;
+  key_store<kHide>(Mt, W, V, A, b, 0, nkv, kvb, kbb, K);
+  for (uint32_t j0 = kWave * kKU; j0 <= nkv; j0 += kWave * kKU) {
+    KBatch N;
+    key_load<kHide>(Mt, V, raw, j0, nkv, N);
+    key_store<kHide>(Mt, W, V, A, b, j0, nkv, kvb, kbb, N);
   }
 }
 
@@ -591,48 +626,76 @@ __device__ __forceinline__ void emit_keys_glb(const Meta& Mt, const Slot& W, con
 // Values shorter than 16 B go byte by byte; values longer than kWaveVal are
 // copied by the whole wave, four 16-B chunks per lane in flight.
 #ifndef PBL_POOL_VG
-#define PBL_POOL_VG 8
+#define PBL_POOL_VG 4
 #endif
 constexpr int kVG = PBL_POOL_VG;
 constexpr uint32_t kWaveVal = 1024;
-__device__ __forceinline__ void copy_values_grp(const Slot& W, gptr<const uint8_t> g, uint32_t nkv,
-                                                gptr<uint8_t> vbytes) {
-  const int l = lane_id();
-  const uint32_t c = uint32_t(l) & 7u;
-  for (uint32_t j0 = 0; j0 < nkv; j0 += 8 * kVG) {
-    uint32_t vo[kVG], vl[kVG], vs[kVG];
+// One step of the value copy: kVG KVs per 8-lane group, j = j0 + 8 u + lane / 8.
+// Only the loaded chunks are held between a step's loads and its stores (the
+// offsets are re-read from the slot).
+struct VBatch {
+  u32x4 x[kVG];
+};
+struct VSeg {
+  uint32_t vo, vl, vs, q;
+  bool has;
+};
+__device__ __forceinline__ VSeg val_seg(const Slot& W, uint32_t nkv, uint32_t j) {
+  const uint32_t c = uint32_t(lane_id()) & 7u;
+  const uint32_t a = j < nkv ? W.vp[j] : 0u, z = j < nkv ? W.vp[j + 1] : 0u;
+  VSeg S;
+  S.vo = a & 0xffffu;
+  S.vl = (z & 0xffffu) - S.vo;
+  S.vs = a >> 16;
+  S.has = S.vl >= 16 && S.vl <= kWaveVal && 16 * c < S.vl;
+  S.q = S.has ? (16 * c < S.vl - 16 ? 16 * c : S.vl - 16) : 0u;
+  return S;
+}
+
+// The step's first chunks from the block (every lane loads, from the block's
+// first bytes when it has no chunk: no conditionally defined registers).
+__device__ __forceinline__ void val_load(const Slot& W, gptr<const uint8_t> g, uint32_t nkv, uint32_t j0, VBatch& B) {
+  const uint32_t jl = j0 + (uint32_t(lane_id()) >> 3);
 #pragma unroll
-    for (int u = 0; u < kVG; u++) {
-      const uint32_t j = j0 + 8 * u + (uint32_t(l) >> 3);
-      const uint32_t a = j < nkv ? W.vp[j] : 0u, z = j < nkv ? W.vp[j + 1] : 0u;
-      vo[u] = a & 0xffffu;
-      vl[u] = (z & 0xffffu) - vo[u];
-      vs[u] = a >> 16;
-    }
-    // (every lane loads, from the block's first bytes when it has no chunk:
-    // no conditionally defined registers)
-    u32x4 x[kVG];
-    uint32_t q[kVG];
-    bool has[kVG];
+  for (int u = 0; u < kVG; u++) {
+    const VSeg S = val_seg(W, nkv, jl + 8 * u);
+    B.x[u] = *(gptr<const u32x4_ug>)(g + (S.has ? S.vs + S.q : 0u));
+  }
+}
+
+__device__ __forceinline__ void val_store(const Slot& W, uint32_t nkv, uint32_t j0, const VBatch& B,
+                                          gptr<const uint8_t> g, gptr<uint8_t> vbytes) {
+  const uint32_t c = uint32_t(lane_id()) & 7u, jl = j0 + (uint32_t(lane_id()) >> 3);
 #pragma unroll
-    for (int u = 0; u < kVG; u++) {
-      has[u] = vl[u] >= 16 && vl[u] <= kWaveVal && 16 * c < vl[u];
-      q[u] = has[u] ? (16 * c < vl[u] - 16 ? 16 * c : vl[u] - 16) : 0u;
-      x[u] = *(gptr<const u32x4_ug>)(g + (has[u] ? vs[u] + q[u] : 0u));
-    }
-#pragma unroll
-    for (int u = 0; u < kVG; u++)
-      if (has[u]) *(gptr<u32x4_ug>)(vbytes + vo[u] + q[u]) = x[u];
-#pragma unroll
-    for (int u = 0; u < kVG; u++) {
-      if (vl[u] > 128 && vl[u] <= kWaveVal) {
-        for (uint32_t o = 16 * c + 128; o < vl[u]; o += 128) {
-          const uint32_t q = o < vl[u] - 16 ? o : vl[u] - 16;
-          *(gptr<u32x4_ug>)(vbytes + vo[u] + q) = *(gptr<const u32x4_ug>)(g + vs[u] + q);
-        }
-      } else if (vl[u] < 16) {
-        for (uint32_t o = c; o < vl[u]; o += 8) vbytes[vo[u] + o] = g[vs[u] + o];
+  for (int u = 0; u < kVG; u++) {
+    const VSeg S = val_seg(W, nkv, jl + 8 * u);
+    if (S.has) *(gptr<u32x4_ug>)(vbytes + S.vo + S.q) = B.x[u];
+    if (S.vl > 128 && S.vl <= kWaveVal) {
+      for (uint32_t o = 16 * c + 128; o < S.vl; o += 128) {
+        const uint32_t q = o < S.vl - 16 ? o : S.vl - 16;
+        *(gptr<u32x4_ug>)(vbytes + S.vo + q) = *(gptr<const u32x4_ug>)(g + S.vs + q);
       }
+    } else if (S.vl < 16) {
+      for (uint32_t o = c; o < S.vl; o += 8) vbytes[S.vo + o] = g[S.vs + o];
+    }
+  }
+}
+
+// Steps are software-pipelined: step i + 1's loads are issued before step i's
+// stores (vmcnt retires loads and stores in issue order, so a load issued
+// after a store would wait for that store's acknowledgement too).  B: step 0,
+// loaded by the caller.
+__device__ __forceinline__ void copy_values_grp(const Slot& W, gptr<const uint8_t> g, uint32_t nkv,
+                                                gptr<uint8_t> vbytes, VBatch& B) {
+  const int l = lane_id();
+  for (uint32_t j0 = 0; j0 < nkv; j0 += 8 * kVG) {
+    if (j0 + 8 * kVG < nkv) {
+      VBatch N;
+      val_load(W, g, nkv, j0 + 8 * kVG, N);
+      val_store(W, nkv, j0, B, g, vbytes);
+      B = N;
+    } else {
+      val_store(W, nkv, j0, B, g, vbytes);
     }
   }
   // long values: the whole wave, four 16-B chunks per lane in flight
@@ -746,7 +809,9 @@ __device__ __forceinline__ bool park(PoolLds& L, uint32_t s, const Args& A) {
     __hip_atomic_store(&L.tk[s], kTkFree, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   if (lane_id() == 0) __hip_atomic_fetch_sub(&L.inflight, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  if (PBL_POOL_PRIO) __builtin_amdgcn_s_setprio(0);
+  // (PBL_POOL_PARKPRIO: a wave whose parked DMA gates the next picker keeps its
+  // priority until it has marked the stage ready)
+  if (PBL_POOL_PRIO && !(PBL_POOL_PARKPRIO && dma)) __builtin_amdgcn_s_setprio(0);
   return dma;
 }
 
@@ -755,6 +820,7 @@ __device__ __forceinline__ void mark_ready(PoolLds& L, uint32_t s) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   wave_sync();
   if (lane_id() == 0) __hip_atomic_store(&L.rdy[s], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (PBL_POOL_PRIO && PBL_POOL_PARKPRIO) __builtin_amdgcn_s_setprio(0);
 }
 
 // The next block for this wave: the smallest parked ticket (waiting for its
@@ -1018,12 +1084,25 @@ __device__ __forceinline__ void pool_block(PoolLds& L, const Work& wk, Slot& W, 
     PBL_MARK_PENDING();
     return;
   }
+  const gptr<const uint8_t> gb = to_glb(gblk);
 #if PBL_POOL_EARLY
   PBL_STAGE_DONE();  // everything after this reads the slot and the block in global memory
-  const GSrc KS{to_glb(gblk), blen, uint32_t(((uint64_t(gblk) + blen + 15) & ~uint64_t(15)) - uint64_t(gblk))};
+  const GSrc KS{gb, blen, uint32_t(((uint64_t(gblk) + blen + 15) & ~uint64_t(15)) - uint64_t(gblk))};
+  // the first key batch, the first value step and the first restarts need no
+  // output offsets: their loads go out before the look-back wait
+  const bool raw = (flags & PBL_ROW_RAW_KEYS) != 0;
+  KBatch K;
+  VBatch VB;
+  uint32_t rs0 = 0;
+  if (published) {
+    key_load<kHide>(Mt, KS, raw, 0, nkv, K);
+    val_load(W, gb, nkv, 0, VB);
+    if (O.restarts && uint32_t(l) < nres) rs0 = KS.le32(roff + 4 * l);
+  }
 #else
   const View& KS = V;
 #endif
+  PBL_MARK_PENDING();
 
   const bool okb = status == PBL_OK;
   const uint64_t agg[kNumComp] = {okb ? nkv : 0, okb ? tkb : 0, okb ? tvb : 0, okb ? nres : 0};
@@ -1033,7 +1112,6 @@ __device__ __forceinline__ void pool_block(PoolLds& L, const Work& wk, Slot& W, 
     if (b > 0) G.issue(LbPtrs(lb_state, nb), int64_t(b) - 1);
   }
   lb_finish(lb_state, nb, b, agg, excl, &O.totals->status_mask, G);
-  PBL_MARK_PENDING();
   PSTAMP(A, b, 5, l == 0);
   if (okb && overflows(O, excl, agg)) status = PBL_OVERFLOW;
   if (l == 0) {
@@ -1058,17 +1136,27 @@ __device__ __forceinline__ void pool_block(PoolLds& L, const Work& wk, Slot& W, 
   // ---- keys and per-KV arrays: lane per KV ------------------------------------
   const uint64_t kvb = excl[0], kbb = excl[1], vbb = excl[2], rbb = excl[3];
 #if PBL_POOL_EARLY
-  emit_keys_glb<kHide>(Mt, W, KS, A, b, nkv, kvb, kbb);
+  if (!published) {
+    key_load<kHide>(Mt, KS, raw, 0, nkv, K);
+    val_load(W, gb, nkv, 0, VB);
+    if (O.restarts && uint32_t(l) < nres) rs0 = KS.le32(roff + 4 * l);
+  }
+  if (O.restarts && uint32_t(l) < nres) to_glb(O.restarts)[rbb + l] = rs0;
+  emit_keys_glb<kHide>(Mt, W, KS, A, b, nkv, kvb, kbb, K);
+  if (O.restarts)
+    for (uint32_t r = kWave + l; r < nres; r += kWave) to_glb(O.restarts)[rbb + r] = KS.le32(roff + 4 * r);
 #else
   emit_keys<kHide>(Mt, W, KS, A, b, nkv, kvb, kbb);
-#endif
   if (O.restarts)
     for (uint32_t r = l; r < nres; r += kWave) to_glb(O.restarts)[rbb + r] = KS.le32(roff + 4 * r);
-  if (!PBL_POOL_EARLY) release(L, s);
+  release(L, s);
+  VBatch VB;
+  val_load(W, gb, nkv, 0, VB);
+#endif
   PSTAMP(A, b, 6, l == 0);
 
   // ---- values, global -> global --------------------------------------------
-  if (tvb) copy_values_grp(W, to_glb(gblk), nkv, to_glb(O.val_bytes) + vbb);
+  if (tvb) copy_values_grp(W, gb, nkv, to_glb(O.val_bytes) + vbb, VB);
   PSTAMP(A, b, 7, l == 0);
   wave_sync();  // (the slot is the next block's)
 }

@@ -50,7 +50,7 @@ elif workload == "mixed":
 else:
     buf, off, lens, n = gen_row_blocks(42, nb, 32768, 16, 16, 100, n_threads=16)
     b = BlockBatch.from_host(buf, off, lens, "cuda")
-b.flags |= int(os.environ.get("PROF_FLAGS", "0"), 0)  # e.g. PBL_KERNEL_FLAT (0x800) for A/B profiles
+b.flags |= int(os.environ.get("PROF_FLAGS", "0"), 0)  # e.g. PBL_KERNEL_PIPE (0x400) for A/B profiles
 if workload == "transform":
     # the config-2 batch decoded once, then transformed `iters` times
     from pebble_amd.transforms import TransformPlan, Transforms

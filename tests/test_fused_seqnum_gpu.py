@@ -2,8 +2,8 @@
 synthetic_seq_num): a batch decoded with the field set
 equals the oracle's decode followed by its SetSeqNum transform
 (oracle.transform_batch, rowblk_iter.go:1168-1191; data_block.go:1693-1695),
-bit-exact on every array -- row batches on every row kernel (pipeline, flat,
-one-block-per-workgroup; blocks past the LDS stage on the slow walk; invalid
+bit-exact on every array -- row batches on every row kernel (the pool default, the
+pipeline, one-block-per-workgroup; blocks past the LDS stage on the slow walk; invalid
 keys keep the Invalid trailer; corrupt blocks), colblk batches of both
 schemas, a mixed batch and raw-key batches (no seqnums)."""
 import ctypes
@@ -44,7 +44,7 @@ def big_row_blocks(rng):
     return out
 
 
-@pytest.mark.parametrize("kernel", [0, N.PBL_KERNEL_FLAT, N.PBL_KERNEL_GLOBAL, N.PBL_KERNEL_SINGLE, N.PBL_KERNEL_POOL])
+@pytest.mark.parametrize("kernel", [0, N.PBL_KERNEL_PIPE, N.PBL_KERNEL_SINGLE])
 @pytest.mark.parametrize("seq", SEQS)
 def test_row_batches(kernel, seq):
     rng = random.Random(seq % 1000 + kernel)

@@ -1,8 +1,9 @@
-"""The one-wave-per-block row kernels (rowblk_flat.hip.h, batch flag
-PBL_KERNEL_FLAT; rowblk_pool.hip.h, PBL_KERNEL_POOL; rowblk_global.hip.h, PBL_KERNEL_GLOBAL) against the oracle: bit-exact on every output array, over the
-same inputs as the pipeline's parity tests (reference blocks, synthetic
-configs, random and fuzzed blocks, value prefixes, blocks past the LDS limits,
-the general-path fallbacks)."""
+"""The row kernels -- the staging-pool kernel (rowblk_pool.hip.h, the
+default; batch flag PBL_KERNEL_POOL) and the two-stage pipeline kept for A/B
+(rowblk_pipe.hip.h, PBL_KERNEL_PIPE) -- against the oracle: bit-exact on every
+output array, over reference blocks, synthetic configs, random and fuzzed
+blocks, value prefixes, blocks past the LDS limits, the general-path fallbacks
+and batches whose block shapes vary."""
 import os
 import random
 
@@ -15,8 +16,7 @@ from pebble_amd.rowblk import Writer, gen_row_blocks
 from test_rowblk_gpu import GOLDEN, assert_same, pack, random_block
 
 pytestmark = pytest.mark.gpu
-KERNELS = {"flat": N.PBL_KERNEL_FLAT, "global": N.PBL_KERNEL_GLOBAL, "pool": N.PBL_KERNEL_POOL}
-FLAT = N.PBL_KERNEL_FLAT
+KERNELS = {"pool": N.PBL_KERNEL_POOL, "pipe": N.PBL_KERNEL_PIPE}
 
 
 @pytest.fixture(params=sorted(KERNELS))
@@ -24,7 +24,7 @@ def kern(request):
     return KERNELS[request.param]
 
 
-def check(buf, off, lens, flags=0, ctx="", kern=FLAT):
+def check(buf, off, lens, flags=0, ctx="", kern=0):
     from pebble_amd.batch import BlockBatch, decode
     o = oracle.rowblk_decode_batch(buf, off, lens, flags)
     g = decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, flags | kern)).to_host()
@@ -32,7 +32,7 @@ def check(buf, off, lens, flags=0, ctx="", kern=FLAT):
     return g
 
 
-def test_flat_hamlet_and_golden(golden, kern):
+def test_hamlet_and_golden(golden, kern):
     g = golden["h_no_compression"]
     blob = np.fromfile(os.path.join(GOLDEN, "h_no_compression_blocks.bin"), np.uint8)
     blob = np.concatenate([blob, np.zeros(16, np.uint8)])
@@ -46,14 +46,14 @@ def test_flat_hamlet_and_golden(golden, kern):
 @pytest.mark.parametrize("ri", [1, 2, 16, 17, 32, 64])
 @pytest.mark.parametrize("kl,vl", [(16, 100), (8, 0), (64, 7), (24, 1000)])
 @pytest.mark.parametrize("vp", [False, True])
-def test_flat_synthetic_batches(ri, kl, vl, vp, kern):
+def test_synthetic_batches(ri, kl, vl, vp, kern):
     for bs in (4096, 32768):
         buf, off, lens, n = gen_row_blocks(1000 + ri + kl + vl, 48, bs, ri, kl, vl, vp)
         g = check(buf, off, lens, N.PBL_ROW_VALUE_PREFIX if vp else 0, f"ri={ri} kl={kl} vl={vl} vp={vp} bs={bs}", kern)
         assert g["n_kv"] == n
 
 
-def test_flat_random_blocks(kern):
+def test_random_blocks(kern):
     rng = random.Random(4321)
     for flags in (0, N.PBL_ROW_VALUE_PREFIX, N.PBL_ROW_VALUE_PREFIX | N.PBL_ROW_NO_VALUER, N.PBL_ROW_RAW_KEYS):
         blocks = [random_block(rng)[0] for _ in range(300)]
@@ -61,7 +61,7 @@ def test_flat_random_blocks(kern):
             check(*pack(blocks, align), flags, f"random flags={flags} align={align}", kern)
 
 
-def test_flat_fuzzed_blocks(kern):
+def test_fuzzed_blocks(kern):
     rng = random.Random(98)
     blocks = []
     for _ in range(400):
@@ -82,7 +82,7 @@ def test_flat_fuzzed_blocks(kern):
 
 
 @pytest.mark.parametrize("bs", [65536, 200000])
-def test_flat_blocks_past_the_limit(bs, kern):
+def test_blocks_past_the_limit(bs, kern):
     buf, off, lens, n = gen_row_blocks(5, 6, bs, 16, 16, 100)
     small = gen_row_blocks(6, 10, 32768, 16, 16, 100)
     blocks = [bytes(buf[o:o + l]) for o, l in zip(off, lens)] + [bytes(small[0][o:o + l]) for o, l in zip(small[1], small[2])]
@@ -91,16 +91,19 @@ def test_flat_blocks_past_the_limit(bs, kern):
     check(*pack(blocks), 0, f"bs={bs}", kern)
 
 
-def test_flat_config2_full_size_sha(kern):
+def test_config2_full_size_sha_pool_vs_pipe():
+    """The full config-2 batch: the default (pool) and the pipeline agree on
+    every array (each is checked against the oracle at reduced size above and
+    in test_baseline_configs_gpu.py)."""
     import hashlib
     from pebble_amd.batch import BlockBatch, decode
     buf, off, lens, n = gen_row_blocks(42, 65536, 32768, 16, 16, 100, n_threads=16)
     gp = decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, N.PBL_KERNEL_PIPE)).to_host()
-    gf = decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, kern)).to_host()
+    gf = decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, 0)).to_host()
     for k in ("trailer", "kv_flags", "entry_off", "key_off", "val_off", "key_bytes", "val_bytes", "restarts",
               "blk_kv_base", "blk_key_base", "blk_val_base", "blk_rst_base", "blk_status"):
         assert hashlib.sha256(gp[k].tobytes()).digest() == hashlib.sha256(gf[k].tobytes()).digest(), k
-    assert gf["n_kv"] == n
+    assert gf["n_kv"] == n and int(gf["n_slow_blocks"]) == 0
 
 
 @pytest.mark.parametrize("mix", ["zipf10", "tail8"])
