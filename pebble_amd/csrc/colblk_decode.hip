@@ -21,6 +21,17 @@ colblk_decode_kernel(Args A) {
   col_block(s, A, ticket, A.in.format);
 }
 
+// The same with HideObsoletePoints fused (PBL_ROW_HIDE_OBSOLETE batches).
+__global__ void __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(PBL_COL_SINGLE_WAVES)))
+colblk_hide_kernel(Args A) {
+  __shared__ Lds s;
+  __shared__ uint32_t ticket;
+  uint32_t* ticket_ctr = reinterpret_cast<uint32_t*>(A.out.workspace);
+  if (threadIdx.x == 0) ticket = atomicAdd(ticket_ctr, 1u);
+  __syncthreads();
+  col_block<true>(s, A, ticket, A.in.format);
+}
+
 }  // namespace col
 }  // namespace pbl
 
@@ -28,7 +39,6 @@ colblk_decode_kernel(Args A) {
 // and the totals are cleared, for a batch whose blocks are all colblk.
 extern "C" int pbl_decode_batch_colblk(const pbl_block_batch* batch, pbl_decode_out* out, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (batch->flags & PBL_ROW_HIDE_OBSOLETE) return PBL_UNSUPPORTED;  // (fused for row batches only, so far)
   if (hipMemsetAsync(out->workspace, 0, pbl::ws_bytes(batch->n_blocks), st) != hipSuccess)
     return PBL_DEVICE_ERROR;
   pbl::Args a;
@@ -41,7 +51,9 @@ extern "C" int pbl_decode_batch_colblk(const pbl_block_batch* batch, pbl_decode_
   // convoys behind long blocks).
   const uint32_t f = batch->flags;
   const bool single = (f & PBL_KERNEL_SINGLE) || ((f & PBL_BATCH_VARLEN) && !(f & PBL_KERNEL_PIPE));
-  if (single) {
+  if (f & PBL_ROW_HIDE_OBSOLETE) {
+    hipLaunchKernelGGL(pbl::col::colblk_hide_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
+  } else if (single) {
     hipLaunchKernelGGL(pbl::col::colblk_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
   } else {
     const uint64_t grid = pbl::persistent_grid(st, pbl::kKColPipe,

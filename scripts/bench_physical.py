@@ -5,7 +5,7 @@ are produced by the device itself (a first verify pass reports `computed`,
 which is written into the trailers; the timed passes then verify them all OK).
 Snappy: the same blocks compressed on the host (pyarrow), decompressed on the
 device; also a text-like corpus (~2x for snappy) and zstd (level 3, Pebble's
-uvarint length prefix) on both.  Prints one JSON line.
+uvarint length prefix) on both; every block distinct.  Prints one JSON line.
 Usage: bench_physical.py [n_blocks] [reps] [codecs, e.g. snappy,zstd]"""
 import json
 import os
@@ -78,15 +78,21 @@ def uvarint(n):
 
 
 def words_blocks(n_distinct=256, vocab=512, seed=5):
-    """Text-like 32 KiB blocks (a 512-word vocabulary: snappy ~2x, zstd ~3x)."""
+    """Text-like 32 KiB blocks (a 512-word vocabulary: snappy ~2x, zstd ~3x),
+    every block distinct."""
     rng = np.random.default_rng(seed)
     alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789", np.uint8)
-    words = [bytes(alpha[rng.integers(0, len(alpha), int(k))]) + b" " for k in rng.integers(2, 9, vocab)]
-    out = []
-    for _ in range(n_distinct):
-        ids = rng.integers(0, vocab, 8000)
-        out.append(b"".join(words[i] for i in ids)[:32768])
-    return out
+    wl = rng.integers(2, 9, vocab)
+    W = np.zeros((vocab, 9), np.uint8)
+    for i in range(vocab):
+        W[i, :wl[i]] = alpha[rng.integers(0, len(alpha), int(wl[i]))]
+        W[i, wl[i]] = ord(" ")
+    keep = np.arange(9)[None, :] <= wl[:, None]
+    ids = rng.integers(0, vocab, 12_000_000)
+    text = W[ids][keep[ids]]  # ~66 MB of words; block i = a 32 KiB window at a random offset
+    stride = (len(text) - 32768) // n_distinct  # distinct offsets, in random order
+    starts = rng.permutation(np.arange(n_distinct) * stride + rng.integers(0, stride, n_distinct))
+    return [text[a:a + 32768].tobytes() for a in starts]
 
 
 def codec_run(raw_blocks, codec, n):
@@ -95,8 +101,10 @@ def codec_run(raw_blocks, codec, n):
     (checked), time pbl_decompress_blocks."""
     ind = 1 if codec == "snappy" else 7
     c = pa.Codec(codec) if codec == "snappy" else pa.Codec("zstd", compression_level=3)
-    comp = [c.compress(b, asbytes=True) if codec == "snappy" else uvarint(len(b)) + c.compress(b, asbytes=True)
-            for b in raw_blocks]
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(16) as ex:
+        comp = list(ex.map(lambda b: c.compress(b, asbytes=True) if codec == "snappy"
+                           else uvarint(len(b)) + c.compress(b, asbytes=True), raw_blocks))
     k = len(comp)
     cl = np.array([len(comp[i % k]) for i in range(n)], np.uint32)
     coff = np.zeros(n, np.uint64)
@@ -130,9 +138,9 @@ def codec_run(raw_blocks, codec, n):
 
 cfg2 = [buf[int(o):int(o) + int(ln)].tobytes() for o, ln in zip(off, lens)]
 codecs = sys.argv[3].split(",") if len(sys.argv) > 3 else ["snappy", "zstd"]
-words = words_blocks()
+words = words_blocks(nb)
 for codec in codecs:
-    # config-2 blocks (random values: ratio ~1.0) and text-like blocks (ratio ~2-3)
-    res[codec] = codec_run(cfg2 if codec == "snappy" else cfg2[:4096], codec, nb)
+    # config-2 blocks (random values: ratio ~1.0) and text-like blocks (ratio ~2-3), all distinct
+    res[codec] = codec_run(cfg2, codec, nb)
     res[codec + "_words"] = codec_run(words, codec, nb)
 print(json.dumps(res), flush=True)

@@ -4,7 +4,9 @@ same flag (tests/test_oracle_hide.py pins that against the transform
 restatement): bit-exact on every output array for random blocks, versioned
 keys whose shared prefix reaches the kind byte, value prefixes, blocks past
 the fast path's limits and past the 32 KiB stage; config-2 blocks (no obsolete
-points) decode as without the flag."""
+points) decode as without the flag.  Colblk batches (the isObsolete bitmap,
+data_block.go:1680-1697) against oracle.transform_batch(hide) over the
+oracle's plain decode."""
 import random
 
 import numpy as np
@@ -14,6 +16,8 @@ import oracle
 from pebble_amd import _native as N
 from pebble_amd.batch import BlockBatch, DecodeError, decode
 from pebble_amd.rowblk import gen_row_blocks
+from colutil import build_block, random_rows
+from pebble_amd.colblk import SCHEMA_CRDB1, SCHEMA_DEFAULT
 from rowutil import mvcc_block
 from test_rowblk_gpu import assert_same, pack, random_block
 
@@ -41,7 +45,7 @@ def test_random_and_versioned_blocks(flags):
 
 
 def test_general_path_blocks():
-    # > 400 entries (the fast path's cap), runs longer than 16, corrupt blocks
+    # more entries than a slot holds (288 / 336), runs longer than 16, corrupt blocks
     rng = random.Random(61)
     blocks = [mvcc_block(rng, 900, 1, False, True), mvcc_block(rng, 600, 64, True, True),
               mvcc_block(rng, 300, 40, False, False)]
@@ -70,8 +74,42 @@ def test_config2_without_obsolete_points_is_unchanged():
     assert a["n_kv"] == n
 
 
-def test_not_fused_for_colblk_or_mixed():
+@pytest.mark.parametrize("schema", [SCHEMA_DEFAULT, SCHEMA_CRDB1])
+def test_colblk_batches(schema):
+    rng = random.Random(70 + schema)
+    blocks = []
+    for _ in range(120):
+        rows = random_rows(rng, schema, rng.choice([1, 5, 17, 100, 300, 700]), shared=rng.choice([0, 3]),
+                           val_len=(0, rng.choice([3, 50, 400])))
+        blocks.append(build_block(schema, rows, rng.choice([1, 4, 16]))[0])
+    for i in range(0, 120, 23):  # a few corrupt blocks stay failed
+        b = bytearray(blocks[i])
+        b[rng.randrange(len(b))] ^= 0x5A
+        blocks[i] = bytes(b)
+    buf, off, lens = pack(blocks)
+    plain = oracle.decode_batch(buf, off, lens, schema, None, 0)
+    o = oracle.transform_batch(plain, 0, True)
+    for seq in (0, 4242):
+        bb = BlockBatch.from_host(buf, off, lens, "cuda", schema, HIDE)
+        bb.synthetic_seq_num = seq
+        g = decode(bb).to_host()
+        assert_same(g, oracle.transform_batch(plain, seq, True) if seq else o, f"colblk schema={schema} seq={seq}")
+    assert 0 < g["n_kv"] < plain["n_kv"]
+
+
+def test_colblk_config3_shaped():
     from pebble_amd.colblk import gen_col_blocks
-    buf, off, lens, n = gen_col_blocks(1, 20, 32768)
+    buf, off, lens, n = gen_col_blocks(1, 64, 32768)
+    o = oracle.transform_batch(oracle.decode_batch(buf, off, lens, N.PBL_FMT_COL_CRDB1, None, 0), 0, True)
+    g = decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_COL_CRDB1, HIDE)).to_host()
+    assert_same(g, o, "config-3 shaped")
+
+
+def test_not_fused_for_mixed():
+    rng = random.Random(71)
+    rows = random_rows(rng, SCHEMA_CRDB1, 20)
+    blocks = [build_block(SCHEMA_CRDB1, rows, 16)[0], random_block(rng)[0]]
+    buf, off, lens = pack(blocks)
     with pytest.raises(DecodeError, match="UNSUPPORTED"):
-        decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_COL_CRDB1, HIDE))
+        decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, HIDE,
+                                    block_format=np.array([SCHEMA_CRDB1, N.PBL_FMT_ROW], np.uint8)))
