@@ -799,8 +799,10 @@ __device__ __forceinline__ void col_rows_hide(Lds& s, const Args& A, uint32_t b,
   const bool ok = s.status == PBL_OK;
   const uint64_t agg[kNumComp] = {ok ? n_tot : 0ull, ok ? kb_tot : 0ull, ok ? vb_tot : 0ull, 0ull};
   if (wave_id() == 0) {
+    // publish first (block 0's aggregate IS its inclusive prefix: without the
+    // publish its successors would wait for a prefix nobody stores)
     uint64_t excl[kNumComp];
-    lb_resolve(lb_state, nb, b, agg, excl, &O.totals->status_mask);
+    lookback(lb_state, nb, b, agg, excl, &O.totals->status_mask);
     if (lane_id() == 0) {
       uint32_t status = s.status;
       if (ok && overflows(O, excl, agg)) status = PBL_OVERFLOW;

@@ -33,7 +33,7 @@ KERNELS = KERNEL.split("+")
 for f in glob.glob(os.path.join(src, "*", "*_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         for k in KERNELS:
-            if k + "(" in r["Kernel_Name"]:
+            if k + "(" in r["Kernel_Name"] or k + "<" in r["Kernel_Name"]:
                 pmc[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
 means = collections.defaultdict(float)
 for (k, c), v in pmc.items():
@@ -42,7 +42,7 @@ means = dict(means)
 stats = {}
 for r in csv.DictReader(open(os.path.join(src, "trace", "trace_kernel_stats.csv"))):
     for k in KERNELS:
-        if k + "(" in r["Name"]:
+        if k + "(" in r["Name"] or k + "<" in r["Name"]:
             if not stats:
                 stats = {"calls": int(r["Calls"]), "avg_ns": 0.0, "min_ns": 0.0, "max_ns": 0.0}
             stats["avg_ns"] += float(r["AverageNs"])
