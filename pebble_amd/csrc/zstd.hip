@@ -56,8 +56,17 @@ __device__ inline bool uvarint32(gptr<const uint8_t> p, uint32_t n, uint32_t* v,
 __device__ unsigned long long g_zstd_prof[8];  // diagnostic build only
 #endif
 
+}  // namespace zstd
+}  // namespace pbl
+#include "zstd_fast.hip.h"
+namespace pbl {
+namespace zstd {
+
+// Every zstd block the batch path (zstd_fast.hip.h) did not take; `ws` is that
+// path's workspace (null: every zstd block).
 __global__ void __launch_bounds__(kWave) zstd_kernel(const pbl_phys_batch B, uint8_t* out, const uint64_t* out_off,
-                                                     const uint32_t* out_cap, uint32_t* out_len, uint32_t* status) {
+                                                     const uint32_t* out_cap, uint32_t* out_len, uint32_t* status,
+                                                     const void* ws) {
   __shared__ Lds L;
   const uint32_t lane = lane_id();
 #ifdef PBL_ZSTD_STAMPS
@@ -70,6 +79,7 @@ __global__ void __launch_bounds__(kWave) zstd_kernel(const pbl_phys_batch B, uin
     const uint64_t boff = to_glb(B.block_off)[b];
     const gptr<const uint8_t> src = to_glb(B.bytes + boff);
     if (src[n] != PBL_COMPRESSION_ZSTD) continue;
+    if (ws && to_glb(FastWs::at(const_cast<void*>(ws), B.n_blocks).desc)[b].fast) continue;  // zstd_exec_kernel's
     uint32_t st = PBL_OK, D = 0, used = 0;
     const uint32_t cap = to_glb(out_cap)[b];
     if (!uvarint32(src, n, &D, &used)) st = PBL_CORRUPT_COMPRESSION;
@@ -134,11 +144,35 @@ __global__ void __launch_bounds__(kWave) zstd_kernel(const pbl_phys_batch B, uin
 
 // Launched by pbl_decompress_blocks (physical.hip) after the snappy kernel: it
 // handles exactly the blocks whose indicator is zstd.
+// The batch path runs in a stream-ordered workspace (hipMallocAsync, freed on
+// the stream after the last launch); without one (PBL_ZSTD_FAST=0 builds, or
+// the allocation failing) zstd_kernel decodes every zstd block.
+#ifndef PBL_ZSTD_FAST
+#define PBL_ZSTD_FAST 1
+#endif
 hipError_t launch_zstd(const pbl_phys_batch& batch, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                        uint32_t* out_len, uint32_t* status, hipStream_t st) {
-  const uint32_t grid = std::min<uint32_t>(batch.n_blocks, 2048);
-  hipLaunchKernelGGL(zstd::zstd_kernel, dim3(grid), dim3(kWave), 0, st, batch, out, out_off, out_cap, out_len, status);
-  return hipGetLastError();
+  const uint32_t n = batch.n_blocks;
+  void* ws = nullptr;
+  if (PBL_ZSTD_FAST && hipMallocAsync(&ws, zstd::FastWs::bytes(n), st) != hipSuccess) {
+    (void)hipGetLastError();
+    ws = nullptr;
+  }
+  if (ws) {
+    if (hipMemsetAsync(ws, 0, sizeof(zstd::WsHdr), st) != hipSuccess) return hipGetLastError();
+    hipLaunchKernelGGL(zstd::zstd_prep_kernel, dim3(std::min<uint32_t>(n, 8192)), dim3(kWave), 0, st, batch, out, out_off,
+                       out_cap, ws);
+    hipLaunchKernelGGL(zstd::zstd_lit_kernel, dim3((4ull * n + 255) / 256), dim3(256), 0, st, batch, out, out_off, ws);
+    hipLaunchKernelGGL(zstd::zstd_seq_kernel, dim3((n + 255) / 256), dim3(256), 0, st, batch, ws);
+    hipLaunchKernelGGL(zstd::zstd_exec_kernel, dim3(std::min<uint32_t>(n, 4096)), dim3(kWave), 0, st, batch, out,
+                       out_off, out_len, status, ws);
+  }
+  const uint32_t grid = std::min<uint32_t>(n, 2048);
+  hipLaunchKernelGGL(zstd::zstd_kernel, dim3(grid), dim3(kWave), 0, st, batch, out, out_off, out_cap, out_len, status,
+                     static_cast<const void*>(ws));
+  const hipError_t e = hipGetLastError();
+  if (ws) (void)hipFreeAsync(ws, st);
+  return e;
 }
 
 }  // namespace pbl

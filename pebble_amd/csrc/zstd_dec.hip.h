@@ -197,8 +197,8 @@ __device__ inline bool fse_build(lptr<uint32_t> T, lptr<const int16_t> norm, lpt
 }
 
 // FSE_readNCount + build (lane 0).  Returns bytes used, or -1.
-template <class S>
-__device__ inline int32_t fse_desc(lptr<uint32_t> T, Lds& L, const S& s, uint32_t base, uint32_t n, uint32_t max_al,
+template <class S, class LT>
+__device__ inline int32_t fse_desc(lptr<uint32_t> T, LT& L, const S& s, uint32_t base, uint32_t n, uint32_t max_al,
                                    uint32_t max_sym, uint32_t* al_out) {
   lptr<int16_t> norm = to_lds_ptr(L.norm);
   uint32_t bit = 0;
@@ -260,8 +260,8 @@ __constant__ uint8_t kMLBits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
 
 // Sequence table for mode m (lane 0): predefined / RLE / FSE / repeat.
 // Returns bytes used or -1.
-template <class S>
-__device__ inline int32_t seq_table(lptr<uint32_t> T, Lds& L, uint32_t mode, const int16_t* def, uint32_t ndef,
+template <class S, class LT>
+__device__ inline int32_t seq_table(lptr<uint32_t> T, LT& L, uint32_t mode, const int16_t* def, uint32_t ndef,
                                     uint32_t def_al, uint32_t max_al, uint32_t max_sym, const S& s, uint32_t base,
                                     uint32_t n, uint32_t* al, bool* have) {
   if (mode == 0) {
@@ -290,8 +290,8 @@ __device__ inline int32_t seq_table(lptr<uint32_t> T, Lds& L, uint32_t mode, con
 
 // Huffman tree description at s[base, base + n) -> L.huf (wave).  Returns bytes
 // used or -1 (uniform).
-template <class S>
-__device__ inline int32_t huf_read(Lds& L, const S& s, uint32_t base, uint32_t n, uint32_t* log_out) {
+template <class S, class LT>
+__device__ inline int32_t huf_read(LT& L, const S& s, uint32_t base, uint32_t n, uint32_t* log_out) {
   const uint32_t lane = lane_id();
   if (n < 1) return -1;
   const uint32_t hb = s[base];
