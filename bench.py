@@ -307,10 +307,10 @@ def main():
         block_fmt = np.empty(nb, np.uint8)
         block_fmt[0::2], block_fmt[1::2] = N.PBL_FMT_ROW, N.PBL_FMT_COL_CRDB1
         n_kv = rn + cn
-        # (the sequential mixed path: split + colblk size pass + row pipeline +
-        # colblk pipeline, timed together as one decode)
+        # (the sequential mixed path: split + colblk size pass + the row
+        # staging-pool kernel over the row ids + colblk pipeline, timed together)
         kernel = ("mixed_decode_kernel" if a.kernel == "single" else
-                  "mixed_col_size_kernel+mixed_row_kernel+mixed_col_kernel")
+                  "mixed_col_size_kernel+rowblk_pool_kernel+mixed_col_kernel")
         wl = (f"config4 shard: {nb} x {a.block_size // 1024} KiB blocks per GPU, even ids row-format "
               f"(config-2 shape), odd ids colblk crdb1 (config-3 shape)")
     gen_s = time.time() - t0

@@ -1081,10 +1081,10 @@ int launch_row_pool(const pbl::Args& a, hipStream_t st, bool values) {
   hipLaunchKernelGGL(pbl::row::pipe::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
   if (hide)
     hipLaunchKernelGGL(pbl::row::pool::rowblk_pool_kernel<true>, dim3(uint32_t(grid)), dim3(pbl::row::pool::kTPBP), 0,
-                       st, a);
+                       st, a, static_cast<const uint32_t*>(nullptr));
   else
     hipLaunchKernelGGL(pbl::row::pool::rowblk_pool_kernel<false>, dim3(uint32_t(grid)), dim3(pbl::row::pool::kTPBP),
-                       0, st, a);
+                       0, st, a, static_cast<const uint32_t*>(nullptr));
   if (values) hipLaunchKernelGGL(pbl::row::pipe::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }
@@ -1097,6 +1097,9 @@ bool hide_row(const pbl_block_batch* b) {
          b->format == PBL_FMT_ROW;
 }
 
+#ifndef PBL_MIXED_POOL
+#define PBL_MIXED_POOL 1  // mixed batches' row blocks on the staging-pool kernel (0: the row pipeline)
+#endif
 // Mixed batches: PBL_KERNEL_SINGLE keeps the one-block-per-workgroup kernel
 // (A/B); the default splits the ids by format and runs the mixed pipeline,
 // with the big row blocks' size / value passes around it.
@@ -1124,7 +1127,19 @@ int launch_mixed(const pbl_block_batch* batch, const pbl::Args& a, hipStream_t s
   const uint32_t* cids = static_cast<const uint32_t*>(ids);
   hipLaunchKernelGGL(pbl::row::pipe::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
   hipLaunchKernelGGL(pbl::row::mixed_col_size_kernel, dim3(g_cs), dim3(pbl::kWave), 0, st, a, cids);
+#if PBL_MIXED_POOL
+  // the row blocks on the staging-pool kernel, over the row id list
+  const uint64_t g_p = pbl::persistent_grid(st, pbl::kKRowPool,
+                                            reinterpret_cast<const void*>(pbl::row::pool::rowblk_pool_kernel<false>),
+                                            (uint64_t(nb) + pbl::row::pool::kNW - 1) / pbl::row::pool::kNW, &cus,
+                                            pbl::row::pool::kTPBP);
+  if (!g_p) return PBL_DEVICE_ERROR;
+  (void)g_r;
+  hipLaunchKernelGGL(pbl::row::pool::rowblk_pool_kernel<false>, dim3(uint32_t(g_p)), dim3(pbl::row::pool::kTPBP), 0,
+                     st, a, cids);
+#else
   hipLaunchKernelGGL(pbl::row::mixed_row_kernel, dim3(uint32_t(g_r)), dim3(pbl::row::pipe::kPTPB), 0, st, a, cids);
+#endif
   hipLaunchKernelGGL(pbl::row::mixed_col_kernel, dim3(uint32_t(g_c)), dim3(pbl::kTPB), 0, st, a, cids);
   if (values)
     hipLaunchKernelGGL(pbl::row::pipe::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);

@@ -51,7 +51,7 @@ namespace pool {
 #define PBL_POOL_STAGES 3
 #endif
 #ifndef PBL_POOL_DEPTH
-#define PBL_POOL_DEPTH 2  // blocks in flight per wave (slots per wave): 1 or 2
+#define PBL_POOL_DEPTH 1  // blocks in flight per wave (slots per wave): 1 or 2
 #endif
 #ifndef PBL_POOL_SLEEP
 #define PBL_POOL_SLEEP 8  // s_sleep units (64 cycles) between polls of the stage mask
@@ -965,14 +965,20 @@ __device__ __forceinline__ void block_emit(const Pend& P, const Slot<kHide>& W, 
 // stage, publishes the block's aggregate before it lets the stage go, and
 // waits (in the look-back) only on smaller tickets, each held by a wave that
 // holds a stage or has published.
+// `ids` (mixed batches): the ascending ids of the batch's row blocks, their
+// count at workspace header word kWsRowCount; the colblk blocks' aggregates are
+// published before this launch (mixed_col_size_kernel), so the look-back walks
+// through them and still waits only on smaller tickets.  Null: every block.
 template <bool kHide>
-__global__ void __launch_bounds__(kTPBP, 1) rowblk_pool_kernel(Args A) {
+__global__ void __launch_bounds__(kTPBP, 1) rowblk_pool_kernel(Args A, const uint32_t* ids) {
   __shared__ PoolLds<kHide> L;
   if (threadIdx.x == 0) L.free_mask = (1u << kNS) - 1u;
   __syncthreads();
   Slot<kHide>* W = L.sl + kDepth * wave_id();
   const uint32_t nb = A.in.n_blocks;
   uint32_t* tick = reinterpret_cast<uint32_t*>(A.out.workspace);
+  const uint32_t nt = ids ? __hip_atomic_load(to_glb(tick) + kWsRowCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                          : nb;
   Pend P;
   P.live = false;
   uint32_t cur = 0;
@@ -984,10 +990,11 @@ __global__ void __launch_bounds__(kTPBP, 1) rowblk_pool_kernel(Args A) {
     uint32_t t0 = 0;
     if (lane_id() == 0) t0 = g_atomic_add(tick, 1u);
     t0 = __builtin_amdgcn_readfirstlane(__shfl(t0, 0, kWave));
-    if (t0 >= nb) {
+    if (t0 >= nt) {
       release(L, s);
       break;
     }
+    if (ids) t0 = __builtin_amdgcn_readfirstlane(to_glb(ids)[t0]);
     PSTAMP(A, t0, 0, lane_id() == 0);
 #ifdef PBL_STAMPS
     if (lane_id() == 0)

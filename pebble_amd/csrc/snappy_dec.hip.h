@@ -377,22 +377,77 @@ __device__ __forceinline__ uint32_t sn_scan(uint32_t v) {  // inclusive, over th
 #define SN_LDS_OR(p, v) __hip_atomic_fetch_or((p), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
 #endif
 
+// One lane's read window over a block's input: the 64 bytes at [wb, wb + 64)
+// (wb a 16-B aligned address) in eight u64 registers, slid 16 bytes at a time;
+// the granule a slide loads is first read two slides later, so the walk reads
+// from registers while its loads run ~32 bytes (~10 text elements) ahead,
+// instead of one dependent global load per element.  Granules past the last
+// readable byte (the indicator at p[n]) read as zeros; the first may start up
+// to 15 bytes before p, inside p's own 16-B granule.
+struct SnWin {
+  uint64_t lim;  // address of p[n]
+  uint64_t wb;
+  uint64_t w0, w1, w2, w3, w4, w5, w6, w7;
+  __device__ __forceinline__ void ld(uint64_t a, uint64_t& x, uint64_t& y) const {
+    if (a <= lim) {
+      const u32x4 v = *(gptr<const u32x4>)(reinterpret_cast<const u32x4*>(a));
+      x = uint64_t(v[0]) | uint64_t(v[1]) << 32;
+      y = uint64_t(v[2]) | uint64_t(v[3]) << 32;
+    } else {
+      x = y = 0;
+    }
+  }
+  __device__ __forceinline__ void reset(uint64_t a) {
+    wb = a & ~uint64_t(15);
+    ld(wb, w0, w1);
+    ld(wb + 16, w2, w3);
+    ld(wb + 32, w4, w5);
+    ld(wb + 48, w6, w7);
+  }
+  __device__ __forceinline__ uint64_t sel(uint32_t k) const {  // word k of 8, selects only
+    const uint64_t a = (k & 1) ? w1 : w0, b = (k & 1) ? w3 : w2, c = (k & 1) ? w5 : w4, d = (k & 1) ? w7 : w6;
+    const uint64_t e = (k & 2) ? b : a, f = (k & 2) ? d : c;
+    return (k & 4) ? f : e;
+  }
+  // bytes [a, a + 8) (a - wb <= 56)
+  __device__ __forceinline__ uint64_t get8(uint64_t a) const {
+    const uint32_t o = uint32_t(a - wb), k = o >> 3, sh = 8 * (o & 7);
+    const uint64_t lo = sel(k);
+    if (!sh) return lo;
+    return (lo >> sh) | (sel(k + 1) << (64 - sh));
+  }
+  // make [a, a + 8) readable: slide while a is 16 or more bytes in (a load per
+  // slide), jump when it is past the window
+  __device__ __forceinline__ void seek(uint64_t a) {
+    if (a - wb >= 64) {
+      reset(a);
+      return;
+    }
+    while (a - wb >= 16) {
+      w0 = w2; w1 = w3; w2 = w4; w3 = w5; w4 = w6; w5 = w7;
+      wb += 16;
+      ld(wb + 48, w6, w7);
+    }
+  }
+};
+
 // One lane: the walk of a block (n input bytes from `used` on, D output bytes).
 __device__ __forceinline__ void sn4_walk(gptr<const uint8_t> p, uint32_t n, uint32_t used, uint32_t D,
                                          gptr<uint8_t> out) {
   const gptr<uint8_t> bm = out + 16;
   const uint32_t nw = (n + 31) / 32;
   uint32_t s = used, d = 0, cnt = 0, ok = 1, cw = 0, acc = 0;
-  uint64_t w = s < n ? sn_load8c(p, s, n) : 0ull;
+  const uint64_t pa = reinterpret_cast<uint64_t>(p);
+  SnWin W;
+  W.lim = pa + n;
+  W.reset(pa + s);
   while (s < n) {
-    const SnElem e = sn_elem(w);
+    const SnElem e = sn_elem(W.get8(pa + s));
     if (!sn_elem_ok(e, s, n, d, D)) { ok = 0; break; }
     const uint32_t s0 = s;
     s += e.h + (e.lit ? e.len : 0u);
     d += e.len;
-    // the next tag's load before this element's stores: loads and stores
-    // retire in order, so the next step waits for the load alone
-    if (s < n) w = sn_load8c(p, s, n);
+    if (s < n) W.seek(pa + s);
     for (; cw < (s0 >> 5); cw++, acc = 0) *(gptr<sn_u32_u>)(bm + 4 * cw) = acc;
     acc |= 1u << (s0 & 31);
     cnt++;
