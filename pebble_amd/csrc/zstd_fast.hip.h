@@ -41,8 +41,11 @@ namespace zstd {
 
 constexpr uint32_t kFastWin = kOut;   // decoded bytes per block on this path (LDS window)
 constexpr uint32_t kHdrWin = 1024;    // staged header bytes per window
-constexpr uint32_t kTblBytes = 14336; // per-block table slot: Huffman 2048 x u16, LL 512 / OF 256 / ML 512 x u64
-constexpr uint32_t kSeqPerBlock = 3072;  // sequence words of workspace per block (shared by a bump counter)
+constexpr uint32_t kTblBytes = 6656;  // per-block table slot: Huffman 2048 x u16, LL 512 / OF 256 / ML 512 x u16
+// sequence words of workspace per block, shared through a bump counter (text
+// at level 3 runs ~4.7 K sequences per 32 KiB block; a block that finds the
+// area full is left to zstd_kernel)
+constexpr uint32_t kSeqPerBlock = 8192;
 
 struct FDesc {
   uint32_t fast, D, regen, ltype;
@@ -81,15 +84,20 @@ struct FastWs {
     return W;
   }
   __device__ uint16_t* huf(uint32_t b) const { return reinterpret_cast<uint16_t*>(tbl + uint64_t(b) * kTblBytes); }
-  __device__ uint64_t* ll(uint32_t b) const { return reinterpret_cast<uint64_t*>(tbl + uint64_t(b) * kTblBytes + 4096); }
-  __device__ uint64_t* of(uint32_t b) const { return ll(b) + 512; }
-  __device__ uint64_t* ml(uint32_t b) const { return ll(b) + 768; }
+  __device__ uint16_t* ll(uint32_t b) const { return reinterpret_cast<uint16_t*>(tbl + uint64_t(b) * kTblBytes + 4096); }
+  __device__ uint16_t* of(uint32_t b) const { return ll(b) + 512; }
+  __device__ uint16_t* ml(uint32_t b) const { return ll(b) + 768; }
 };
 
-// Sequence-table entry (u64): next-state base (16) | state bits (8) | extra
-// bits (8) | baseline value (32).
-__device__ __forceinline__ uint64_t seq_entry(uint32_t e, uint32_t extra, uint32_t value) {
-  return uint64_t(e >> 16) | uint64_t((e >> 8) & 0xff) << 16 | uint64_t(extra) << 24 | uint64_t(value) << 32;
+// Sequence-table entry (u16): the state's occurrence counter x (10 bits: the
+// FSE build's next[s]++, in [count, 2 count)) | symbol << 10.  A decoder gets
+// nb = al - highbit(x) and the next-state base (x << nb) - 2^al from it
+// (RFC 8878 §4.1.1), and the symbol's baseline and extra bits from the
+// symbol; 2.5 KB of tables per block keeps a batch's tables inside the
+// Infinity Cache.  From the LDS build's entries (sym | nb << 8 | base << 16).
+__device__ __forceinline__ uint16_t seq_entry(uint32_t e, uint32_t al) {
+  const uint32_t nb = (e >> 8) & 0xff, x = ((e >> 16) + (1u << al)) >> nb;
+  return uint16_t(x | (e & 0xff) << 10);
 }
 
 // Bytes [lo, lo + len) of the block staged in LDS; reads outside read 0 (the
@@ -300,18 +308,9 @@ __global__ void __launch_bounds__(kWave) zstd_prep_kernel(const pbl_phys_batch B
         if (fast) {
           q += uint32_t(u);
           // the tables, baselines folded in (RFC 8878 §3.1.1.3.2.1.1)
-          for (uint32_t i = lane; i < (1u << al_ll); i += kWave) {
-            const uint32_t e = L.fse[0][i], s = e & 0xff;
-            to_glb(W.ll(b))[i] = seq_entry(e, kLLBits[s], kLLBase[s]);
-          }
-          for (uint32_t i = lane; i < (1u << al_of); i += kWave) {
-            const uint32_t e = L.fse[1][i], s = e & 0xff;
-            to_glb(W.of(b))[i] = seq_entry(e, s, 1u << (s & 31));
-          }
-          for (uint32_t i = lane; i < (1u << al_ml); i += kWave) {
-            const uint32_t e = L.fse[2][i], s = e & 0xff;
-            to_glb(W.ml(b))[i] = seq_entry(e, kMLBits[s], kMLBase[s]);
-          }
+          for (uint32_t i = lane; i < (1u << al_ll); i += kWave) to_glb(W.ll(b))[i] = seq_entry(L.fse[0][i], al_ll);
+          for (uint32_t i = lane; i < (1u << al_of); i += kWave) to_glb(W.of(b))[i] = seq_entry(L.fse[1][i], al_of);
+          for (uint32_t i = lane; i < (1u << al_ml); i += kWave) to_glb(W.ml(b))[i] = seq_entry(L.fse[2][i], al_ml);
         }
       } else if (fast && q != end) {
         fast = false;
@@ -352,33 +351,71 @@ __global__ void __launch_bounds__(kWave) zstd_prep_kernel(const pbl_phys_batch B
   }
 }
 
-// ---- lane-per-stream / lane-per-block bit readers ------------------------------
+// ---- lane-per-stream / lane-per-block bit reader ------------------------------
 // Backward bitstream over global bytes [0, n) of p (RFC 8878 §4.1): unread bits
-// [0, pos); the container holds bits [cb, cb + 64), refilled by one unaligned
-// 8-B load that never ends past byte n (byte loads for streams under 8 bytes).
-struct GBits {
-  gptr<const uint8_t> p;
+// [0, pos); the container c holds bits [cb, cb + 64), refilled from a register
+// window: stream bytes [wb, wb + 64) of p in eight u64 (wb a 16-B aligned
+// address), slid 16 bytes down whenever a refill reaches the window's lowest 16
+// bytes, so the granule a slide loads is first needed ~16 bytes of stream later
+// (a few symbols or sequences): refills read registers, not memory.  Granules
+// below p's own granule or past its last byte read as 0.
+struct GBitsW {
+  uint64_t pa, lo_a, hi_a;  // p; lowest and highest loadable granule addresses
   uint32_t n;
   int32_t pos, cb;
-  uint64_t c;
+  uint64_t c, wb;
+  uint64_t w0, w1, w2, w3, w4, w5, w6, w7;
+  __device__ __forceinline__ void ld(uint64_t a, uint64_t& x, uint64_t& y) const {
+    if (a >= lo_a && a <= hi_a) {
+      const u32x4 v = *(gptr<const u32x4>)(reinterpret_cast<const u32x4*>(a));
+      x = uint64_t(v[0]) | uint64_t(v[1]) << 32;
+      y = uint64_t(v[2]) | uint64_t(v[3]) << 32;
+    } else {
+      x = y = 0;
+    }
+  }
+  __device__ __forceinline__ uint64_t sel(uint32_t k) const {
+    const uint64_t a = (k & 1) ? w1 : w0, b = (k & 1) ? w3 : w2, cc = (k & 1) ? w5 : w4, d = (k & 1) ? w7 : w6;
+    const uint64_t e = (k & 2) ? b : a, f = (k & 2) ? d : cc;
+    return (k & 4) ? f : e;
+  }
   __device__ __forceinline__ void refill() {
     int32_t b = (pos - 57) >> 3;
     if (b < 0) b = 0;
     cb = 8 * b;
-    if (uint32_t(b) + 8 <= n) {
-      c = *(gptr<const uint64_t __attribute__((aligned(1)))>)(p + b);
+    const uint64_t a = pa + uint32_t(b);
+    if (a < wb || a - wb > 56) {  // (only after a corrupt jump)
+      wb = (a & ~uint64_t(15)) - 32;
+      ld(wb, w0, w1);
+      ld(wb + 16, w2, w3);
+      ld(wb + 32, w4, w5);
+      ld(wb + 48, w6, w7);
     } else {
-      c = 0;
-      for (uint32_t i = uint32_t(b); i < n; i++) c |= uint64_t(p[i]) << (8 * (i - b));
+      while (a < wb + 16 && wb > lo_a) {
+        w7 = w5; w6 = w4; w5 = w3; w4 = w2; w3 = w1; w2 = w0;
+        wb -= 16;
+        ld(wb, w0, w1);
+      }
     }
+    const uint32_t o = uint32_t(a - wb), k = o >> 3, sh = 8 * (o & 7);
+    const uint64_t lo = sel(k);
+    c = sh ? (lo >> sh) | (sel(k + 1) << (64 - sh)) : lo;
+    if (uint32_t(b) + 8 > n) c &= (~0ull >> (8 * (uint32_t(b) + 8 - n)));  // (bytes past the stream)
   }
   __device__ __forceinline__ bool init(gptr<const uint8_t> src, uint32_t len) {
-    p = src;
+    pa = reinterpret_cast<uint64_t>(src);
     n = len;
     if (len == 0) return false;
-    const uint32_t last = p[len - 1];
+    lo_a = pa & ~uint64_t(15);
+    hi_a = (pa + len - 1) & ~uint64_t(15);
+    const uint32_t last = src[len - 1];
     if (last == 0) return false;
     pos = int32_t(8 * len) - 8 + highbit(last);
+    wb = hi_a - 48;
+    ld(wb, w0, w1);
+    ld(wb + 16, w2, w3);
+    ld(wb + 32, w4, w5);
+    ld(wb + 48, w6, w7);
     refill();
     return true;
   }
@@ -415,7 +452,7 @@ __global__ void __launch_bounds__(256) zstd_lit_kernel(const pbl_phys_batch B, u
   const gptr<const uint8_t> src = to_glb(B.bytes + to_glb(B.block_off)[b]);
   const gptr<uint8_t> o = to_glb(out + to_glb(out_off)[b] + (D - regen) + s * seg);
   const gptr<const uint16_t> H = to_glb(static_cast<const uint16_t*>(W.huf(b)));
-  GBits br;
+  GBitsW br;
   bool bad = !br.init(src + g->s_off[s], g->s_len[s]);
   if (!bad) {
     // bytes until o is 4-B aligned, then whole words, then the tail
@@ -453,7 +490,26 @@ __device__ __forceinline__ uint64_t seq_pack(uint32_t ll, uint32_t ml, uint32_t 
   return uint64_t(min(ll, 0x1FFFFFu)) | uint64_t(min(ml, 0x1FFFFFu)) << 21 | uint64_t(min(off, 0x3FFFFFu)) << 42;
 }
 
+// A sequence-table entry's symbol and next-state fields.
+struct SeqSym {
+  uint32_t sym, nb, base;
+};
+__device__ __forceinline__ SeqSym seq_sym(uint32_t e, uint32_t al) {
+  const uint32_t x = e & 0x3ff;
+  SeqSym r;
+  r.sym = e >> 10;
+  r.nb = al - uint32_t(highbit(x));
+  r.base = (x << r.nb) - (1u << al);
+  return r;
+}
+
 __global__ void __launch_bounds__(256) zstd_seq_kernel(const pbl_phys_batch B, void* ws) {
+  // baselines and extra bits of the literal-length codes past 15 and the
+  // match-length codes past 31 (below them: the code itself, and code + 3)
+  __shared__ uint32_t xl[36], xm[53];
+  if (threadIdx.x < 36) xl[threadIdx.x] = kLLBase[threadIdx.x] | uint32_t(kLLBits[threadIdx.x]) << 24;
+  if (threadIdx.x < 53) xm[threadIdx.x] = kMLBase[threadIdx.x] | uint32_t(kMLBits[threadIdx.x]) << 24;
+  __syncthreads();
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B.n_blocks) return;
   const FastWs W = FastWs::at(ws, B.n_blocks);
@@ -461,26 +517,29 @@ __global__ void __launch_bounds__(256) zstd_seq_kernel(const pbl_phys_batch B, v
   if (!g->fast) return;
   const uint32_t nseq = g->nseq;
   if (nseq == 0) return;
-  const uint32_t al = g->al;
+  const uint32_t al = g->al, all = al & 0xff, alo = (al >> 8) & 0xff, alm = (al >> 16) & 0xff;
   const gptr<const uint8_t> src = to_glb(B.bytes + to_glb(B.block_off)[b]);
-  const gptr<const uint64_t> TL = to_glb(static_cast<const uint64_t*>(W.ll(b)));
-  const gptr<const uint64_t> TO = to_glb(static_cast<const uint64_t*>(W.of(b)));
-  const gptr<const uint64_t> TM = to_glb(static_cast<const uint64_t*>(W.ml(b)));
+  const gptr<const uint16_t> TL = to_glb(static_cast<const uint16_t*>(W.ll(b)));
+  const gptr<const uint16_t> TO = to_glb(static_cast<const uint16_t*>(W.of(b)));
+  const gptr<const uint16_t> TM = to_glb(static_cast<const uint16_t*>(W.ml(b)));
+  const lptr<const uint32_t> XL = to_lds_ptr(static_cast<const uint32_t*>(xl));
+  const lptr<const uint32_t> XM = to_lds_ptr(static_cast<const uint32_t*>(xm));
   const gptr<uint64_t> S = to_glb(W.seq + g->seq_base);
-  GBits br;
+  GBitsW br;
   bool bad = !br.init(src + g->q_off, g->q_len);
   if (!bad) {
-    uint32_t stl = br.read(al & 0xff), sto = br.read((al >> 8) & 0xff), stm = br.read((al >> 16) & 0xff);
+    uint32_t stl = br.read(all), sto = br.read(alo), stm = br.read(alm);
     uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
     for (uint32_t i = 0; i < nseq; i++) {
-      const uint64_t el = TL[stl], eo = TO[sto], em = TM[stm];
-      const uint32_t ofv = uint32_t(eo >> 32) + br.read(uint32_t(eo >> 24) & 0xff);
-      const uint32_t ml = uint32_t(em >> 32) + br.read(uint32_t(em >> 24) & 0xff);
-      const uint32_t ll = uint32_t(el >> 32) + br.read(uint32_t(el >> 24) & 0xff);
+      const SeqSym el = seq_sym(TL[stl], all), eo = seq_sym(TO[sto], alo), em = seq_sym(TM[stm], alm);
+      const uint32_t xlv = el.sym < 16 ? el.sym : XL[el.sym], xmv = em.sym < 32 ? em.sym + 3 : XM[em.sym];
+      const uint32_t ofv = (1u << eo.sym) + br.read(eo.sym);
+      const uint32_t ml = (xmv & 0xffffff) + br.read(xmv >> 24);
+      const uint32_t ll = (xlv & 0xffffff) + br.read(xlv >> 24);
       if (i + 1 < nseq) {
-        stl = uint32_t(el & 0xffff) + br.read(uint32_t(el >> 16) & 0xff);
-        stm = uint32_t(em & 0xffff) + br.read(uint32_t(em >> 16) & 0xff);
-        sto = uint32_t(eo & 0xffff) + br.read(uint32_t(eo >> 16) & 0xff);
+        stl = el.base + br.read(el.nb);
+        stm = em.base + br.read(em.nb);
+        sto = eo.base + br.read(eo.nb);
       }
       uint32_t off;
       if (ofv > 3) {
@@ -527,15 +586,41 @@ __device__ __forceinline__ void lds_put(lptr<uint8_t> wv, uint32_t at, const u32
     if (k < n) wv[at + k] = uint8_t(w[k >> 2] >> (8 * (k & 3)));
 }
 
+// Exclusive wave scan by DPP row shifts and row broadcasts (no LDS round trip).
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
   uint32_t x = v;
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, kWave);
-    if (lane_id() >= d) x += y;
-  }
-  *total = __shfl(x, kWave - 1, kWave);
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  *total = __builtin_amdgcn_readlane(x, kWave - 1);
   return x - v;
+}
+
+// One batch of up to 64 sequences (lane = sequence): lengths, offset, literal
+// source / literal destination / match destination from two wave scans (lp,
+// pos: literals consumed and bytes written before the batch), the batch's
+// totals, whether the lane's sequence is out of bounds, and the first 16
+// literal bytes (the load issued here, consumed a batch later).
+struct XBatch {
+  uint32_t ll, ml, off, lsrc, ldst, mdst, tll, tout;
+  bool bad;
+  u32x4 lit;
+};
+__device__ __forceinline__ void x_plan(XBatch& X, uint64_t sw, bool live, uint32_t lp, uint32_t pos,
+                                       gptr<const uint8_t> lits, uint32_t regen, uint32_t D) {
+  X.ll = uint32_t(sw & 0x1FFFFF);
+  X.ml = uint32_t((sw >> 21) & 0x1FFFFF);
+  X.off = uint32_t(sw >> 42);
+  const uint32_t lpx = wave_excl_scan(X.ll, &X.tll);
+  const uint32_t opx = wave_excl_scan(X.ll + X.ml, &X.tout);
+  X.lsrc = lp + lpx;
+  X.ldst = pos + opx;
+  X.mdst = X.ldst + X.ll;
+  X.bad = live && (X.lsrc + X.ll > regen || X.mdst + X.ml > D || X.off == 0 || X.off > X.mdst);
+  X.lit = (X.ll && !X.bad && X.lsrc < regen) ? ld16_lim(lits, X.lsrc, regen) : u32x4{0, 0, 0, 0};
 }
 
 __global__ void __launch_bounds__(kWave) zstd_exec_kernel(const pbl_phys_batch B, uint8_t* out, const uint64_t* out_off,
@@ -553,27 +638,34 @@ __global__ void __launch_bounds__(kWave) zstd_exec_kernel(const pbl_phys_batch B
     const gptr<const uint64_t> S = to_glb(static_cast<const uint64_t*>(W.seq + g->seq_base));
     bool ok = g->flags == 0;
     uint32_t pos = 0, lp = 0;
+    // Batch k + 1 is planned (scans, checks, its first literal chunk's load)
+    // before batch k's matches run, and its sequence words are loaded a batch
+    // earlier still: the loads run under the previous batch's LDS work.
+    uint64_t sw_n = kWave + lane < nseq ? S[kWave + lane] : 0ull;
+    XBatch X;
+    if (nseq) x_plan(X, lane < nseq ? S[lane] : 0ull, lane < nseq, 0, 0, lits, regen, D);
     for (uint32_t r0 = 0; ok && r0 < nseq; r0 += kWave) {
       const uint32_t i = r0 + lane;
-      const uint64_t sw = i < nseq ? S[i] : 0ull;
-      const uint32_t ll = uint32_t(sw & 0x1FFFFF), ml = uint32_t((sw >> 21) & 0x1FFFFF), off = uint32_t(sw >> 42);
-      uint32_t tll, tout;
-      const uint32_t lpx = wave_excl_scan(ll, &tll);
-      const uint32_t opx = wave_excl_scan(ll + ml, &tout);
-      const uint32_t lsrc = lp + lpx, ldst = pos + opx, mdst = ldst + ll;
-      const bool bad = i < nseq && (lsrc + ll > regen || mdst + ml > D || off == 0 || off > mdst);
-      if (__ballot(bad) || lp + tll > regen || pos + tout > D) { ok = false; break; }
+      const XBatch C = X;
+      if (__ballot(C.bad) || lp + C.tll > regen || pos + C.tout > D) { ok = false; break; }
       // literal runs, lane per sequence (the literal region is never written here)
-      for (uint32_t c = 0; c < ll; c += 16) {
-        const uint32_t k = min(16u, ll - c);
-        lds_put(win, ldst + c, ld16_lim(lits, lsrc + c, regen), k);
-      }
+      if (C.ll) lds_put(win, C.ldst, C.lit, min(16u, C.ll));
+      for (uint32_t c = 16; c < C.ll; c += 16) lds_put(win, C.ldst + c, ld16_lim(lits, C.lsrc + c, regen), min(16u, C.ll - c));
       wave_sync();
+      lp += C.tll;
+      pos += C.tout;
+      if (r0 + kWave < nseq) {
+        const uint64_t sw = sw_n;
+        sw_n = i + 2 * kWave < nseq ? S[i + 2 * kWave] : 0ull;
+        x_plan(X, sw, i + kWave < nseq, lp, pos, lits, regen, D);
+      }
+      const uint32_t ml = C.ml, off = C.off, mdst = C.mdst;
       // matches: groups whose sources lie below the group's first output
       uint64_t pend = __ballot(i < nseq && ml > 0);
       while (pend) {
         const int gl = __builtin_ctzll(pend);
-        const uint32_t gstart = __shfl(mdst, gl, kWave), gml = __shfl(ml, gl, kWave), goff = __shfl(off, gl, kWave);
+        const uint32_t gstart = __builtin_amdgcn_readlane(mdst, gl), gml = __builtin_amdgcn_readlane(ml, gl),
+                       goff = __builtin_amdgcn_readlane(off, gl);
         if (gml > kWave) {
           // a long match: the whole wave, 64-byte rounds (period goff when it overlaps)
           for (uint32_t j0 = 0; j0 < gml; j0 += kWave) {
@@ -590,13 +682,23 @@ __global__ void __launch_bounds__(kWave) zstd_exec_kernel(const pbl_phys_batch B
           continue;
         }
         const bool mine = ((pend >> lane) & 1) && ml <= kWave && (int(lane) == gl || mdst - off + ml <= gstart);
-        if (mine)
-          for (uint32_t j = 0; j < ml; j++) win[mdst + j] = win[mdst - off + j];
+        if (mine) {
+          // chunks of min(off, 16) bytes: a chunk's reads never see its own writes,
+          // so its byte reads are independent (one LDS latency per chunk)
+          const uint32_t ck = off < 16 ? off : 16u;
+          for (uint32_t j = 0; j < ml; j += ck) {
+            uint8_t t[16];
+#pragma unroll
+            for (uint32_t k = 0; k < 16; k++)
+              if (k < ck && j + k < ml) t[k] = win[mdst - off + j + k];
+#pragma unroll
+            for (uint32_t k = 0; k < 16; k++)
+              if (k < ck && j + k < ml) win[mdst + j + k] = t[k];
+          }
+        }
         wave_sync();
         pend &= ~__ballot(mine);
       }
-      pos += tout;
-      lp += tll;
     }
     if (ok) {
       const uint32_t rest = regen - lp;

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Profiling driver: the text-like zstd corpus of bench_physical.py (level 3,
-ratio ~2.66, distinct blocks) decompressed `iters` times (for rocprofv3)."""
+"""Profiling driver: a text-like corpus (bench_physical.py's kind, 512 distinct
+blocks cycled) compressed with zstd level 3 (ratio ~2.66) or, with
+CODEC=snappy, snappy (~1.95), decompressed `iters` times (for rocprofv3)."""
 import os
 import sys
 
@@ -19,7 +20,8 @@ level = int(os.environ.get("ZSTD_LEVEL", "3"))
 rng = np.random.default_rng(5)
 alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789", np.uint8)
 words = [bytes(alpha[rng.integers(0, len(alpha), int(k))]) + b" " for k in rng.integers(2, 9, 512)]
-c = pa.Codec("zstd", compression_level=level)
+codec = os.environ.get("CODEC", "zstd")
+c = pa.Codec("zstd", compression_level=level) if codec == "zstd" else pa.Codec("snappy")
 
 
 def uvarint(n):
@@ -32,7 +34,7 @@ def uvarint(n):
 
 
 raw = [b"".join(words[i] for i in rng.integers(0, 512, 8000))[:32768] for _ in range(512)]
-comp = [uvarint(len(b)) + c.compress(b, asbytes=True) for b in raw]
+comp = [(uvarint(len(b)) if codec == "zstd" else b"") + c.compress(b, asbytes=True) for b in raw]
 cl = np.array([len(comp[i % len(comp)]) for i in range(nb)], np.uint32)
 coff = np.zeros(nb, np.uint64)
 coff[1:] = np.cumsum((cl.astype(np.uint64) + 5 + 7) // 8 * 8)[:-1]
@@ -40,7 +42,7 @@ cbuf = np.zeros(int(coff[-1]) + int(cl[-1]) + 32, np.uint8)
 for i in range(nb):
     x = comp[i % len(comp)]
     cbuf[int(coff[i]):int(coff[i]) + len(x)] = np.frombuffer(x, np.uint8)
-    cbuf[int(coff[i]) + len(x)] = 7
+    cbuf[int(coff[i]) + len(x)] = 7 if codec == "zstd" else 1
 pb = PhysBatch.from_host(cbuf, coff, cl)
 for _ in range(iters):
     bb, st = decompress(pb)
