@@ -284,7 +284,7 @@ __device__ bool sn_decode(Snap2Lds& S, uint32_t ib, uint32_t n, uint32_t used, u
       const int first = __builtin_ctzll(cm);
       const uint32_t o = uint32_t(e) & 0xffffu, len = uint32_t(e >> 16) & 0xffffu,
                      off = uint32_t(e >> 32) & 0x7fffffffu;
-      const uint32_t d0 = __shfl(o, first, kWave);
+      const uint32_t d0 = __builtin_amdgcn_readlane(o, first);
       // final bytes at [P, P + len) (an overlapping copy: its period [o - off, o))
       const bool ovl = off < len;
       const uint32_t P = ovl ? o - off : (isc ? R[j] & kSnPos : 0u);
@@ -365,7 +365,19 @@ __device__ __forceinline__ uint4 sn_load16c(gptr<const uint8_t> p, uint32_t s, u
   const uint64_t lo = sn_load8c(p, s, n), hi = s + 8 < n ? sn_load8c(p, s + 8, n) : 0ull;
   return make_uint4(uint32_t(lo), uint32_t(lo >> 32), uint32_t(hi), uint32_t(hi >> 32));
 }
-__device__ __forceinline__ uint32_t sn_scan(uint32_t v) {  // inclusive, over the wave
+#ifndef SN_EMU_SCAN
+// inclusive, over the wave: DPP row shifts and row broadcasts (no LDS round trip)
+__device__ __forceinline__ uint32_t sn_scan(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+#else  // (the host emulator: the same scan by exchanges)
+__device__ __forceinline__ uint32_t sn_scan(uint32_t v) {
   const uint32_t lane = lane_id();
   for (uint32_t o = 1; o < uint32_t(kWave); o <<= 1) {
     const uint32_t t = __shfl(v, lane >= o ? int(lane - o) : int(lane), kWave);
@@ -373,6 +385,7 @@ __device__ __forceinline__ uint32_t sn_scan(uint32_t v) {  // inclusive, over th
   }
   return v;
 }
+#endif
 #ifndef SN_LDS_OR
 #define SN_LDS_OR(p, v) __hip_atomic_fetch_or((p), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
 #endif
@@ -565,7 +578,7 @@ __device__ bool sn4_decode(Snap4Lds& S, gptr<const uint8_t> src, uint32_t n, uin
         for (uint32_t b = bits; b; b &= b - 1) Q[k++] = 32 * w + uint32_t(__builtin_ctz(b));
       }
       const uint32_t na = uint32_t(__builtin_popcountll(tm));
-      if (na) qc += __shfl(incl, int(na - 1), kWave);
+      if (na) qc += __builtin_amdgcn_readlane(incl, int(na - 1));
       wc += na;
       if (na < uint32_t(kWave)) break;
     }
@@ -593,7 +606,7 @@ __device__ bool sn4_decode(Snap4Lds& S, gptr<const uint8_t> src, uint32_t n, uin
         Q[i] = sn_qent(e, pos, o);
         SN_LDS_OR(OB + ((o - dr) >> 5), 1u << ((o - dr) & 31));
       }
-      d += __shfl(incl, kWave - 1, kWave);
+      d += __builtin_amdgcn_readlane(incl, kWave - 1);
     }
     wave_sync();
     // element starts before each 64-bit word of OB (8 words a lane)
@@ -648,7 +661,8 @@ __device__ bool sn4_decode(Snap4Lds& S, gptr<const uint8_t> src, uint32_t n, uin
         for (uint32_t c = 0; c < len; c += 16) sn_store_n(dst + o + c, sn_load16c(src, x + c, n), len - c < 16 ? len - c : 16u);
       for (uint64_t m = __ballot(len > 256); m; m &= m - 1) {
         const int sl = __builtin_ctzll(m);
-        const uint32_t lo = __shfl(o, sl, kWave), ls = __shfl(x, sl, kWave), ll = __shfl(len, sl, kWave);
+        const uint32_t lo = __builtin_amdgcn_readlane(o, sl), ls = __builtin_amdgcn_readlane(x, sl),
+                       ll = __builtin_amdgcn_readlane(len, sl);
         for (uint32_t c = 16 * lane; c < ll; c += 16 * kWave)
           sn_store_n(dst + lo + c, sn_load16c(src, ls + c, n), ll - c < 16 ? ll - c : 16u);
       }
@@ -674,7 +688,7 @@ __device__ bool sn4_decode(Snap4Lds& S, gptr<const uint8_t> src, uint32_t n, uin
       const int first = __builtin_ctzll(cm);
       const uint64_t e = isc ? QR[j] : 0ull;
       const uint32_t o = sn_dst(e), len = sn_len(e), off = sn_src(e);
-      const uint32_t d0 = __shfl(o, first, kWave);
+      const uint32_t d0 = __builtin_amdgcn_readlane(o, first);
       const bool ovl = off < len;
       const uint32_t P = ovl ? o - off : (ri & kSnPos);
       const bool indep = isc && (ovl ? o <= d0 : P + len <= d0);

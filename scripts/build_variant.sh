@@ -7,7 +7,7 @@ wt=$(mktemp -d /tmp/pbl_wt.XXXX)
 if [ "$rev" = "." ]; then cp -r "$root/pebble_amd" "$root/include" "$wt/"; else git -C "$root" worktree add -q --detach "$wt" "$rev"; fi
 mkdir -p "$root/exp"
 (cd "$wt/pebble_amd/csrc" && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -pthread "$@" \
-  rowblk_decode.hip colblk_decode.hip $(ls transforms.hip physical.hip sstable.hip 2>/dev/null) rowblk_writer.cpp colblk_writer.cpp zipf_gen.cpp \
+  $(ls *.hip) $(ls *.cpp) \
   -o "$root/exp/$name.so")
 if [ "$rev" = "." ]; then rm -rf "$wt"; else git -C "$root" worktree remove --force "$wt"; fi
 echo "$root/exp/$name.so"

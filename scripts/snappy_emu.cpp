@@ -54,6 +54,8 @@ static uint32_t emu_alignbyte(uint32_t hi, uint32_t lo, uint32_t r) {
   return uint32_t(((uint64_t(hi) << 32) | lo) >> (8 * (r & 3)));
 }
 #define __builtin_amdgcn_readfirstlane(x) emu_readfirstlane(x)
+#define __builtin_amdgcn_readlane(x, l) exch((x), (l))
+#define SN_EMU_SCAN 1
 #define __builtin_amdgcn_alignbyte(a, b, c) emu_alignbyte(a, b, c)
 #define __builtin_amdgcn_fence(a, b) ((void)0)
 #define __builtin_amdgcn_wave_barrier() g_bar->arrive_and_wait()
