@@ -293,6 +293,9 @@ int pbl_decompressed_lengths(const pbl_phys_batch* batch, uint32_t* out_len, uin
  * must decode to exactly that length; a frame naming a dictionary is
  * PBL_UNSUPPORTED) are decoded on the device.  The outputs form a pbl_block_batch {out,
  * out_off, out_len} for pbl_decode_batch (keep out_off 8-B aligned for colblk).
+ * zstd's batch path takes a stream-ordered workspace (hipMallocAsync on `stream`,
+ * ~72 KB per block, freed on the stream after its last launch); when that
+ * allocation fails every zstd block takes the one-wave-per-block decoder instead.
  */
 int pbl_decompress_blocks(const pbl_phys_batch* batch, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                           uint32_t* out_len, uint32_t* status, void* stream);

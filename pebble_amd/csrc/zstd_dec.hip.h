@@ -166,6 +166,9 @@ __device__ inline uint32_t fwd(const S& s, uint32_t base, uint32_t n, uint32_t b
 }
 
 // FSE decoding table from norm[0, nsym) (lane 0).  T entries: sym | nb << 8 | base << 16.
+// kSpread: stop after the symbol spread (T[u] = sym, next[] = the counts): the
+// batch path finishes the table with the whole wave (zstd_fast.hip.h).
+template <bool kSpread = false>
 __device__ inline bool fse_build(lptr<uint32_t> T, lptr<const int16_t> norm, lptr<uint16_t> next, uint32_t nsym,
                                  uint32_t al) {
   const uint32_t size = 1u << al;
@@ -187,6 +190,7 @@ __device__ inline bool fse_build(lptr<uint32_t> T, lptr<const int16_t> norm, lpt
       while (int32_t(pos) > high);
     }
   if (pos != 0) return false;
+  if (kSpread) return true;
   for (uint32_t u = 0; u < size; u++) {
     const uint32_t s = T[u] & 0xff;
     const uint32_t x = next[s]++;
@@ -197,7 +201,7 @@ __device__ inline bool fse_build(lptr<uint32_t> T, lptr<const int16_t> norm, lpt
 }
 
 // FSE_readNCount + build (lane 0).  Returns bytes used, or -1.
-template <class S, class LT>
+template <bool kSpread = false, class S, class LT>
 __device__ inline int32_t fse_desc(lptr<uint32_t> T, LT& L, const S& s, uint32_t base, uint32_t n, uint32_t max_al,
                                    uint32_t max_sym, uint32_t* al_out) {
   lptr<int16_t> norm = to_lds_ptr(L.norm);
@@ -236,7 +240,7 @@ __device__ inline int32_t fse_desc(lptr<uint32_t> T, LT& L, const S& s, uint32_t
     }
   }
   if (remaining != 1 || bit > 8 * n || sym > max_sym + 1) return -1;
-  if (!fse_build(T, norm, to_lds_ptr(L.aux), sym, al)) return -1;
+  if (!fse_build<kSpread>(T, norm, to_lds_ptr(L.aux), sym, al)) return -1;
   *al_out = al;
   return int32_t((bit + 7) / 8);
 }
@@ -260,14 +264,14 @@ __constant__ uint8_t kMLBits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
 
 // Sequence table for mode m (lane 0): predefined / RLE / FSE / repeat.
 // Returns bytes used or -1.
-template <class S, class LT>
+template <bool kSpread = false, class S, class LT>
 __device__ inline int32_t seq_table(lptr<uint32_t> T, LT& L, uint32_t mode, const int16_t* def, uint32_t ndef,
                                     uint32_t def_al, uint32_t max_al, uint32_t max_sym, const S& s, uint32_t base,
                                     uint32_t n, uint32_t* al, bool* have) {
   if (mode == 0) {
     lptr<int16_t> norm = to_lds_ptr(L.norm);
     for (uint32_t i = 0; i < ndef; i++) norm[i] = def[i];
-    fse_build(T, norm, to_lds_ptr(L.aux), ndef, def_al);
+    fse_build<kSpread>(T, norm, to_lds_ptr(L.aux), ndef, def_al);
     *al = def_al;
     *have = true;
     return 0;
@@ -280,7 +284,7 @@ __device__ inline int32_t seq_table(lptr<uint32_t> T, LT& L, uint32_t mode, cons
     return 1;
   }
   if (mode == 2) {
-    const int32_t d = fse_desc(T, L, s, base, n, max_al, max_sym, al);
+    const int32_t d = fse_desc<kSpread>(T, L, s, base, n, max_al, max_sym, al);
     if (d < 0) return -1;
     *have = true;
     return d;

@@ -133,6 +133,38 @@ __device__ inline WinIn stage_win(uint8_t* win, const uint8_t* blk, uint32_t a, 
   return W;
 }
 
+// The last step of an FSE table build (fse_build after its spread) by the
+// whole wave: entry u of symbol s gets x = next[s]++ in u order, i.e. next[s]
+// plus the number of entries of s before u.  Lanes take 64 entries at a time;
+// a lane's rank among the chunk's lanes with its symbol comes from one ballot
+// per distinct symbol in the chunk.
+__device__ inline void fse_finish_wave(lptr<uint32_t> T, lptr<uint16_t> next, uint32_t al) {
+  const uint32_t lane = lane_id(), size = 1u << al;
+  for (uint32_t c = 0; c < size; c += kWave) {
+    const uint32_t u = c + lane;
+    const bool valid = u < size;
+    const uint32_t s = valid ? (T[u] & 0xff) : 0xffffu;
+    uint32_t rank = 0, cnt = 0;
+    for (uint64_t rem = __ballot(valid); rem;) {
+      const uint32_t sl = __builtin_amdgcn_readlane(s, __builtin_ctzll(rem));
+      const uint64_t m = __ballot(valid && s == sl);
+      if (valid && s == sl) {
+        rank = uint32_t(__builtin_popcountll(m & ((1ull << lane) - 1)));
+        cnt = uint32_t(__builtin_popcountll(m));
+      }
+      rem &= ~m;
+    }
+    const uint32_t x = (valid ? uint32_t(next[s]) : 0u) + rank;
+    wave_sync();  // (every lane has read next[] before any lane bumps it)
+    if (valid && rank + 1 == cnt) next[s] = uint16_t(x + 1);
+    if (valid) {
+      const uint32_t nb = al - uint32_t(highbit(x));
+      T[u] = s | nb << 8 | ((x << nb) - size) << 16;
+    }
+    wave_sync();
+  }
+}
+
 // ---- plan --------------------------------------------------------------------
 __global__ void __launch_bounds__(kWave) zstd_prep_kernel(const pbl_phys_batch B, uint8_t* out, const uint64_t* out_off,
                                                           const uint32_t* out_cap, void* ws) {
@@ -286,24 +318,36 @@ __global__ void __launch_bounds__(kWave) zstd_prep_kernel(const pbl_phys_batch B
         q++;
         // no repeat mode in a frame's first block (zstd_kernel reports it)
         fast = fast && !(modes & 3) && (modes >> 6) != 3 && ((modes >> 4) & 3) != 3 && ((modes >> 2) & 3) != 3;
+        // each table: lane 0 reads its description and spreads its symbols,
+        // the wave finishes it (modes 0 and 2; an RLE table is one entry)
+        const uint32_t lim = e1 > q ? e1 - q : 0u;
+        const uint32_t mode[3] = {modes >> 6, (modes >> 4) & 3, (modes >> 2) & 3};
         int32_t u = 0;
-        if (fast && lane == 0) {
-          bool hl = false, ho = false, hm = false;
-          const uint32_t lim = e1 > q ? e1 - q : 0u;
-          u = seq_table(to_lds_ptr(L.fse[0]), L, modes >> 6, kLLDef, 36, 6, 9, 35, w1, q, lim, &al_ll, &hl);
-          const int32_t u2 = u < 0 ? -1
-                                   : seq_table(to_lds_ptr(L.fse[1]), L, (modes >> 4) & 3, kOFDef, 29, 5, 8, 31, w1, q + u,
-                                               lim - u, &al_of, &ho);
-          const int32_t u3 = u2 < 0 ? -1
-                                    : seq_table(to_lds_ptr(L.fse[2]), L, (modes >> 2) & 3, kMLDef, 53, 6, 9, 52, w1,
-                                                q + u + u2, lim - u - u2, &al_ml, &hm);
-          u = u3 < 0 ? -1 : u + u2 + u3;
+        uint32_t al3[3] = {0, 0, 0};
+        for (int t = 0; t < 3 && fast; t++) {
+          int32_t ut = 0;
+          uint32_t alt = 0;
+          if (lane == 0) {
+            bool have = false;
+            const uint32_t at = q + uint32_t(u), lt = lim - uint32_t(u);
+            ut = t == 0 ? seq_table<true>(to_lds_ptr(L.fse[0]), L, mode[0], kLLDef, 36, 6, 9, 35, w1, at, lt, &alt, &have)
+                 : t == 1 ? seq_table<true>(to_lds_ptr(L.fse[1]), L, mode[1], kOFDef, 29, 5, 8, 31, w1, at, lt, &alt, &have)
+                          : seq_table<true>(to_lds_ptr(L.fse[2]), L, mode[2], kMLDef, 53, 6, 9, 52, w1, at, lt, &alt, &have);
+          }
+          ut = __shfl(ut, 0, kWave);
+          alt = __shfl(alt, 0, kWave);
+          wave_sync();
+          if (ut < 0) {
+            u = -1;
+            break;
+          }
+          if (mode[t] != 1) fse_finish_wave(to_lds_ptr(L.fse[t]), to_lds_ptr(static_cast<uint16_t*>(L.aux)), alt);
+          al3[t] = alt;
+          u += ut;
         }
-        u = __shfl(u, 0, kWave);
-        al_ll = __shfl(al_ll, 0, kWave);
-        al_of = __shfl(al_of, 0, kWave);
-        al_ml = __shfl(al_ml, 0, kWave);
-        wave_sync();
+        al_ll = al3[0];
+        al_of = al3[1];
+        al_ml = al3[2];
         fast = fast && u >= 0 && q + uint32_t(u) < end;
         if (fast) {
           q += uint32_t(u);
