@@ -1186,13 +1186,10 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
     const void* fn = single ? reinterpret_cast<const void*>(pbl::row::rowblk_decode_kernel)
                             : reinterpret_cast<const void*>(pbl::row::pipe::rowblk_pipe_kernel);
     int cus = 0;
-    uint64_t grid = pbl::persistent_grid(st, single ? pbl::kKRowSingle : pbl::kKRowPipe, fn,
+    const uint64_t grid = pbl::persistent_grid(st, single ? pbl::kKRowSingle : pbl::kKRowPipe, fn,
                                          batch->n_blocks, &cus,
                                          single ? pbl::kTPB : pbl::row::pipe::kPTPB);
     if (!grid) return PBL_DEVICE_ERROR;
-#ifdef PBL_EXP_ROW_WG_PER_CU  // experiment: cap the resident workgroups per CU
-    grid = std::min<uint64_t>(grid, uint64_t(cus) * PBL_EXP_ROW_WG_PER_CU);
-#endif
     if (single)
       hipLaunchKernelGGL(pbl::row::rowblk_decode_kernel, dim3(uint32_t(grid)), dim3(pbl::kTPB), 0, st, a);
     else {

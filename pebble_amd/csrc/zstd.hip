@@ -52,10 +52,6 @@ __device__ inline bool uvarint32(gptr<const uint8_t> p, uint32_t n, uint32_t* v,
   return false;
 }
 
-#ifdef PBL_ZSTD_STAMPS
-__device__ unsigned long long g_zstd_prof[8];  // diagnostic build only
-#endif
-
 }  // namespace zstd
 }  // namespace pbl
 #include "zstd_fast.hip.h"
@@ -69,12 +65,7 @@ __global__ void __launch_bounds__(kWave) zstd_kernel(const pbl_phys_batch B, uin
                                                      const void* ws) {
   __shared__ Lds L;
   const uint32_t lane = lane_id();
-#ifdef PBL_ZSTD_STAMPS
-  if (lane < 8) L.prof[lane] = 0;
-  wave_sync();
-#endif
   for (uint32_t b = blockIdx.x; b < B.n_blocks; b += gridDim.x) {
-    ZT(k0);
     const uint32_t n = to_glb(B.block_len)[b];
     const uint64_t boff = to_glb(B.block_off)[b];
     const gptr<const uint8_t> src = to_glb(B.bytes + boff);
@@ -94,13 +85,10 @@ __global__ void __launch_bounds__(kWave) zstd_kernel(const pbl_phys_batch B, uin
         const uint32_t ssh = uint32_t(sa & 15), ng = (ssh + cn + 15) / 16;
         const gptr<const u32x4> sg = to_glb(reinterpret_cast<const u32x4*>(sa - ssh));
         lds_stage16(to_lds_ptr(reinterpret_cast<u32x4*>(L.in)), sg, ng);
-        ZT(k1);
-        ZADD(L, 5, k0, k1);
         const uint64_t da = reinterpret_cast<uint64_t>(dptr);
         const uint32_t dsh = uint32_t(da & 15);
         r = decode_frames(L, LIn{to_lds_ptr(static_cast<const uint8_t*>(L.in))}, ssh, cn,
                           LOut{to_lds_ptr(static_cast<uint8_t*>(L.out)) + dsh}, D);
-        ZT(k2);
         if (r == kOk) {
           const uint32_t nd = (dsh + D + 15) / 16;
           const gptr<u32x4> dg = to_glb(reinterpret_cast<u32x4*>(da - dsh));
@@ -119,8 +107,6 @@ __global__ void __launch_bounds__(kWave) zstd_kernel(const pbl_phys_batch B, uin
             }
           }
         }
-        ZT(k3);
-        ZADD(L, 6, k2, k3);
       } else {
         r = decode_frames(L, GIn{src}, used, cn, GOut{to_glb(dptr)}, D);
       }
@@ -131,13 +117,7 @@ __global__ void __launch_bounds__(kWave) zstd_kernel(const pbl_phys_batch B, uin
       to_glb(status)[b] = st;
     }
     wave_sync();
-    ZT(k4);
-    ZADD(L, 7, k0, k4);
   }
-#ifdef PBL_ZSTD_STAMPS
-  wave_sync();
-  if (lane < 8) atomicAdd(&g_zstd_prof[lane], (unsigned long long)L.prof[lane]);
-#endif
 }
 
 }  // namespace zstd
@@ -177,12 +157,3 @@ hipError_t launch_zstd(const pbl_phys_batch& batch, uint8_t* out, const uint64_t
 
 }  // namespace pbl
 
-#ifdef PBL_ZSTD_STAMPS
-// diagnostic build: read (and clear) the per-phase cycle sums
-extern "C" int pbl_diag_zstd_prof(unsigned long long* out8) {
-  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(pbl::zstd::g_zstd_prof), 8 * sizeof(unsigned long long)) != hipSuccess)
-    return -1;
-  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(pbl::zstd::g_zstd_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
-}
-#endif

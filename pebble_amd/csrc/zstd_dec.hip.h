@@ -24,21 +24,8 @@ struct Lds {
   uint8_t w[256];
   int16_t norm[256];
   uint16_t aux[256];
-#ifdef PBL_ZSTD_STAMPS
-  uint64_t prof[8];  // diagnostic build: cycles per phase, summed over the wave's blocks
-#endif
 };
 
-#ifdef PBL_ZSTD_STAMPS
-#define ZT(v) const uint64_t v = __builtin_amdgcn_s_memtime()
-#define ZADD(L_, k_, a_, b_) \
-  do {                        \
-    if (lane_id() == 0) (L_).prof[k_] += (b_) - (a_); \
-  } while (0)
-#else
-#define ZT(v) do {} while (0)
-#define ZADD(L_, k_, a_, b_) do {} while (0)
-#endif
 
 // ---- byte accessors ------------------------------------------------------------
 struct LIn {
@@ -407,7 +394,6 @@ __device__ uint32_t comp_block(Lds& L, ZState& Z, const S& s, uint32_t base, uin
                                uint32_t start, uint32_t* pos_io) {
   const uint32_t lane = lane_id();
   if (n < 1) return kCorrupt;
-  ZT(z0);
   const uint32_t b0 = s[base], ltype = b0 & 3, sf = (b0 >> 2) & 3;
   uint32_t h, regen, csize = 0, streams = 1;
   if (ltype < 2) {
@@ -502,8 +488,6 @@ __device__ uint32_t comp_block(Lds& L, ZState& Z, const S& s, uint32_t base, uin
     q += csize;
   }
   o.sync();
-  ZT(z1);
-  ZADD(L, 0, z0, z1);
   // sequences section
   const uint32_t end = base + n;
   if (q >= end) return kCorrupt;
@@ -545,8 +529,6 @@ __device__ uint32_t comp_block(Lds& L, ZState& Z, const S& s, uint32_t base, uin
     wave_sync();
     if (u < 0) return kCorrupt;
     q += u;
-    ZT(z2);
-    ZADD(L, 1, z1, z2);
     // lane 0's bit reader and states persist across rounds
     BitR<S> br;
     uint32_t stl = 0, sto = 0, stm = 0;
@@ -566,7 +548,6 @@ __device__ uint32_t comp_block(Lds& L, ZState& Z, const S& s, uint32_t base, uin
     for (uint32_t r0 = 0; r0 < nseq; r0 += kSeq) {
       const uint32_t m = min(kSeq, nseq - r0);
       bool bad = false;
-      ZT(z3);
       if (lane == 0) {
         for (uint32_t i = 0; i < m; i++) {
           const uint32_t el = TL[stl], eo = TO[sto], em = TM[stm];
@@ -608,8 +589,6 @@ __device__ uint32_t comp_block(Lds& L, ZState& Z, const S& s, uint32_t base, uin
       }
       if (__shfl(int(bad), 0, kWave)) return kCorrupt;
       wave_sync();
-      ZT(z4);
-      ZADD(L, 2, z3, z4);
       for (uint32_t i = 0; i < m; i++) {
         const uint32_t ll = L.s_ll[i], ml = L.s_ml[i], off = L.s_off[i];
         if (ll > regen - lp || ml > D - pos || ll > D - pos - ml) return kCorrupt;
@@ -629,8 +608,6 @@ __device__ uint32_t comp_block(Lds& L, ZState& Z, const S& s, uint32_t base, uin
         pos += ml;
         o.sync();
       }
-      ZT(z5);
-      ZADD(L, 3, z4, z5);
     }
     Z.rep0 = __shfl(Z.rep0, 0, kWave);
     Z.rep1 = __shfl(Z.rep1, 0, kWave);
