@@ -547,16 +547,9 @@ __device__ __forceinline__ SeqSym seq_sym(uint32_t e, uint32_t al) {
   return r;
 }
 
-__global__ void __launch_bounds__(256) zstd_seq_kernel(const pbl_phys_batch B, void* ws) {
-  // baselines and extra bits of the literal-length codes past 15 and the
-  // match-length codes past 31 (below them: the code itself, and code + 3)
-  __shared__ uint32_t xl[36], xm[53];
-  if (threadIdx.x < 36) xl[threadIdx.x] = kLLBase[threadIdx.x] | uint32_t(kLLBits[threadIdx.x]) << 24;
-  if (threadIdx.x < 53) xm[threadIdx.x] = kMLBase[threadIdx.x] | uint32_t(kMLBits[threadIdx.x]) << 24;
-  __syncthreads();
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B.n_blocks) return;
-  const FastWs W = FastWs::at(ws, B.n_blocks);
+// One block's sequences (a lane's chain).
+__device__ __forceinline__ void seq_block(const pbl_phys_batch& B, const FastWs& W, uint32_t b,
+                                          lptr<const uint32_t> XL, lptr<const uint32_t> XM) {
   const gptr<const FDesc> g = to_glb(static_cast<const FDesc*>(W.desc + b));
   if (!g->fast) return;
   const uint32_t nseq = g->nseq;
@@ -566,8 +559,6 @@ __global__ void __launch_bounds__(256) zstd_seq_kernel(const pbl_phys_batch B, v
   const gptr<const uint16_t> TL = to_glb(static_cast<const uint16_t*>(W.ll(b)));
   const gptr<const uint16_t> TO = to_glb(static_cast<const uint16_t*>(W.of(b)));
   const gptr<const uint16_t> TM = to_glb(static_cast<const uint16_t*>(W.ml(b)));
-  const lptr<const uint32_t> XL = to_lds_ptr(static_cast<const uint32_t*>(xl));
-  const lptr<const uint32_t> XM = to_lds_ptr(static_cast<const uint32_t*>(xm));
   const gptr<uint64_t> S = to_glb(W.seq + g->seq_base);
   GBitsW br;
   bool bad = !br.init(src + g->q_off, g->q_len);
@@ -607,6 +598,22 @@ __global__ void __launch_bounds__(256) zstd_seq_kernel(const pbl_phys_batch B, v
     bad = br.pos != 0;
   }
   if (bad) g_atomic_or(&W.desc[b].flags, 16u);
+}
+
+// Lanes stride over the batch (gridDim.x * 256 lanes at a time: the launch
+// picks how many blocks' tables are live at once).
+__global__ void __launch_bounds__(256) zstd_seq_kernel(const pbl_phys_batch B, void* ws) {
+  // baselines and extra bits of the literal-length codes past 15 and the
+  // match-length codes past 31 (below them: the code itself, and code + 3)
+  __shared__ uint32_t xl[36], xm[53];
+  if (threadIdx.x < 36) xl[threadIdx.x] = kLLBase[threadIdx.x] | uint32_t(kLLBits[threadIdx.x]) << 24;
+  if (threadIdx.x < 53) xm[threadIdx.x] = kMLBase[threadIdx.x] | uint32_t(kMLBits[threadIdx.x]) << 24;
+  __syncthreads();
+  const FastWs W = FastWs::at(ws, B.n_blocks);
+  const lptr<const uint32_t> XL = to_lds_ptr(static_cast<const uint32_t*>(xl));
+  const lptr<const uint32_t> XM = to_lds_ptr(static_cast<const uint32_t*>(xm));
+  for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < B.n_blocks; b += gridDim.x * blockDim.x)
+    seq_block(B, W, b, XL, XM);
 }
 
 // ---- execution: a wave per block ---------------------------------------------

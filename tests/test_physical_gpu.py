@@ -182,6 +182,51 @@ def test_zstd_mixed_with_snappy_and_raw():
         assert bytes(out[bo[i]: bo[i] + bl[i]]) == want, i
 
 
+def test_zstd_batch_path_and_fallback_in_one_batch():
+    """Blocks the batch path plans (one frame, one compressed block) next to
+    blocks it leaves to zstd_kernel (two frames, a skippable frame first, a
+    raw zstd block, more than 36 KiB decoded): every one decodes exactly."""
+    import pyarrow as pa
+    rng = random.Random(24)
+
+    def uv(n):
+        pre = bytearray()
+        while n >= 0x80:
+            pre.append(n & 0x7F | 0x80)
+            n >>= 7
+        pre.append(n)
+        return bytes(pre)
+
+    c = pa.Codec("zstd", compression_level=3)
+    raw, comp = [], []
+    for i in range(96):
+        k = i % 6
+        r = compressible(rng, rng.randrange(2000, 30_000))
+        if k == 1:  # two frames
+            a, b = r[: len(r) // 2], r[len(r) // 2:]
+            comp.append(uv(len(r)) + c.compress(a, asbytes=True) + c.compress(b, asbytes=True))
+        elif k == 2:  # a skippable frame, then the frame
+            skip = (0x184D2A50).to_bytes(4, "little") + (5).to_bytes(4, "little") + b"pebbl"
+            comp.append(uv(len(r)) + skip + c.compress(r, asbytes=True))
+        elif k == 3:  # incompressible: a raw zstd block
+            r = rng.randbytes(rng.randrange(100, 20_000))
+            comp.append(zstd_block(r, 3))
+        elif k == 4:  # past the batch path's 36 KiB window
+            r = compressible(rng, rng.randrange(36_865, 60_000))
+            comp.append(zstd_block(r, 3))
+        else:
+            comp.append(zstd_block(r, rng.choice([1, 3, 9])))
+        raw.append(r)
+    buf, off, lens = pack_phys(comp, lambda b: 0, rng, indicator=7)
+    bb, st = decompress(PhysBatch.from_host(buf, off, lens))
+    assert list(st) == [0] * len(comp)
+    out, bo, bl = bb.blocks.cpu().numpy(), bb.block_off.cpu().numpy(), bb.block_len.cpu().numpy()
+    for i, want in enumerate(raw):
+        assert bytes(out[bo[i]: bo[i] + bl[i]]) == want, i
+        if i < 12:
+            assert oracle.zstd_block(comp[i]) == want, i
+
+
 def test_zstd_corrupt_matches_oracle():
     rng = random.Random(23)
     blocks = []
