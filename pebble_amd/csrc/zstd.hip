@@ -130,9 +130,7 @@ __global__ void __launch_bounds__(kWave) zstd_kernel(const pbl_phys_batch B, uin
 #ifndef PBL_ZSTD_FAST
 #define PBL_ZSTD_FAST 1
 #endif
-#ifndef PBL_ZSTD_SEQ_WG
-#define PBL_ZSTD_SEQ_WG 1u << 20  // sequence workgroups (x 256 lanes) live at once
-#endif
+
 hipError_t launch_zstd(const pbl_phys_batch& batch, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                        uint32_t* out_len, uint32_t* status, hipStream_t st) {
   const uint32_t n = batch.n_blocks;
@@ -146,8 +144,7 @@ hipError_t launch_zstd(const pbl_phys_batch& batch, uint8_t* out, const uint64_t
     hipLaunchKernelGGL(zstd::zstd_prep_kernel, dim3(std::min<uint32_t>(n, 8192)), dim3(kWave), 0, st, batch, out, out_off,
                        out_cap, ws);
     hipLaunchKernelGGL(zstd::zstd_lit_kernel, dim3((4ull * n + 255) / 256), dim3(256), 0, st, batch, out, out_off, ws);
-    hipLaunchKernelGGL(zstd::zstd_seq_kernel, dim3(std::min<uint32_t>((n + 255) / 256, PBL_ZSTD_SEQ_WG)), dim3(256), 0,
-                       st, batch, ws);
+    hipLaunchKernelGGL(zstd::zstd_seq_kernel, dim3((n + 255) / 256), dim3(256), 0, st, batch, ws);
     hipLaunchKernelGGL(zstd::zstd_exec_kernel, dim3(std::min<uint32_t>(n, 4096)), dim3(kWave), 0, st, batch, out,
                        out_off, out_len, status, ws);
   }

@@ -600,8 +600,9 @@ __device__ __forceinline__ void seq_block(const pbl_phys_batch& B, const FastWs&
   if (bad) g_atomic_or(&W.desc[b].flags, 16u);
 }
 
-// Lanes stride over the batch (gridDim.x * 256 lanes at a time: the launch
-// picks how many blocks' tables are live at once).
+// A lane per block, every block's chain live at once: capping the live lanes
+// so the tables stay in L2 (12 K / 24 K / 48 K lanes) measured 71.8 / 37.2 /
+// 26.1 ms against 15.7 per 64 Ki text blocks: the chains are latency-bound.
 __global__ void __launch_bounds__(256) zstd_seq_kernel(const pbl_phys_batch B, void* ws) {
   // baselines and extra bits of the literal-length codes past 15 and the
   // match-length codes past 31 (below them: the code itself, and code + 3)
