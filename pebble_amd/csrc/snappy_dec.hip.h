@@ -138,7 +138,6 @@ constexpr uint32_t kSnWalkMin = 64;  // smaller blocks: sn_decode walks them its
 // benign: every value R[k] takes is a valid source of copy k's bytes.
 // Overlapping copies (off < len) keep o - off and repeat their period.
 constexpr uint32_t kSnRes = 1u << 31, kSnStop = 1u << 30, kSnPos = 0xffffu;
-constexpr uint32_t kSnDone = 1u << 29;  // snappy4: an unresolved copy already written (phase 5)
 __device__ __forceinline__ uint32_t sn_dst(uint64_t e) { return uint32_t(e) & 0xffffu; }
 __device__ __forceinline__ uint32_t sn_len(uint64_t e) { return uint32_t(e >> 16) & 0xffffu; }
 __device__ __forceinline__ uint32_t sn_src(uint64_t e) { return uint32_t(e >> 32) & 0x7fffffffu; }
@@ -671,65 +670,48 @@ __device__ bool sn4_decode(Snap4Lds& S, gptr<const uint8_t> src, uint32_t n, uin
     sn_fence();
     SN_ACC(2, t1b);
     SN_T(t2);
-    // 5. the unresolved copies, in passes over the round's list: a copy runs
-    // once no unresolved copy whose output its source reaches (below its own
-    // output) is pending; copies are marked done (kSnDone in R) only after the
-    // pass's fence, so a later reader sees their bytes.  The earliest pending
-    // copy is always ready (every copy before it is done), so each pass
-    // progresses; a pass costs one fence, against one per ordered group.
-    for (uint32_t pass = 0; pass < kS4Q; pass++) {
-      uint32_t ran = 0;  // bit c: this lane's copy of chunk c ran in this pass
-      bool more = false;
-      for (uint32_t g = 0, c = 0; g < cc; g += kWave, c++) {
-        const uint32_t gi = g + lane;
-        const uint32_t j = gi < cc ? uint32_t(CL[gi]) : 0u;
-        const uint32_t ri = gi < cc ? R[j] : kSnRes;
-        const bool pend = gi < cc && !(ri & (kSnRes | kSnDone));
-        if (!__ballot(pend)) continue;
-        bool ready = pend;
-        uint32_t o = 0, len = 0, off = 0, P = 0;
-        bool ovl = false;
-        if (pend) {
-          const uint64_t e = QR[j];
-          o = sn_dst(e);
-          len = sn_len(e);
-          off = sn_src(e);
-          ovl = off < len;
-          P = ovl ? o - off : (ri & kSnPos);
-          // the source bytes below the copy's own output that lie in this round
-          const uint32_t lo = P > dr ? P : dr, hi = P + len < o ? P + len : o;
-          if (hi > lo) {
-            const uint32_t k1 = sn4_find(OB, PF, lo - dr), k2 = sn4_find(OB, PF, hi - 1 - dr);
-            for (uint32_t k = k1; k <= k2 && ready; k++) {
-              const uint64_t ek = QR[k];
-              if ((ek >> 63) && !(R[k] & (kSnRes | kSnDone))) ready = false;
-            }
+    // 5. the other copies in output order, groups of independent ones (sn_decode's)
+    uint32_t g = 0;
+    while (g < cc) {
+      const uint32_t gi = g + lane;
+      uint32_t j = 0, ri = kSnRes;
+      if (gi < cc) {
+        j = CL[gi];
+        ri = R[j];
+      }
+      const bool isc = gi < cc && !(ri & kSnRes);
+      const uint64_t cm = __ballot(isc);
+      if (!cm) {
+        g += kWave;
+        continue;
+      }
+      const int first = __builtin_ctzll(cm);
+      const uint64_t e = isc ? QR[j] : 0ull;
+      const uint32_t o = sn_dst(e), len = sn_len(e), off = sn_src(e);
+      const uint32_t d0 = __builtin_amdgcn_readlane(o, first);
+      const bool ovl = off < len;
+      const uint32_t P = ovl ? o - off : (ri & kSnPos);
+      const bool indep = isc && (ovl ? o <= d0 : P + len <= d0);
+      const uint64_t stop = first == 63 ? 0ull : (__ballot(isc && !indep) & ~((2ull << first) - 1));
+      const uint32_t end = stop ? uint32_t(__builtin_ctzll(stop)) : uint32_t(kWave);
+      if (isc && uint32_t(lane) >= uint32_t(first) && uint32_t(lane) < end) {
+        const gptr<const uint8_t> sp = dst + P;
+        if (!ovl || off >= 16) {
+          for (uint32_t c = 0; c < len; c += 16) {
+            const u32x4 v = *(gptr<const sn_u32x4_u>)(sp + c);
+            sn_store_n(dst + o + c, make_uint4(v[0], v[1], v[2], v[3]), len - c < 16 ? len - c : 16u);
           }
+        } else {
+          uint8_t per[16];
+          for (uint32_t k = 0; k < off; k++) per[k] = sp[k];
+          for (uint32_t k = 0; k < len; k++) dst[o + k] = per[k % off];
         }
-        if (ready) {
-          const gptr<const uint8_t> sp = dst + P;
-          if (!ovl || off >= 16) {
-            for (uint32_t q = 0; q < len; q += 16) {
-              const u32x4 v = *(gptr<const sn_u32x4_u>)(sp + q);
-              sn_store_n(dst + o + q, make_uint4(v[0], v[1], v[2], v[3]), len - q < 16 ? len - q : 16u);
-            }
-          } else {
-            uint8_t per[16];
-            for (uint32_t k = 0; k < off; k++) per[k] = sp[k];
-            for (uint32_t k = 0; k < len; k++) dst[o + k] = per[k % off];
-          }
-          ran |= 1u << c;
-        }
-        more = more || (pend && !ready);
       }
       sn_fence();
-      for (uint32_t g = 0, c = 0; g < cc; g += kWave, c++)
-        if ((ran >> c) & 1u) R[CL[g + lane]] |= kSnDone;
-      wave_sync();
+      g += end;
 #ifdef PBL_SNAP_STAMPS
-      if (lane == 0 && g_sn_b < 65536) g_snap_stamps[8 * g_sn_b + 5] += 1;  // passes
+      if (lane == 0 && g_sn_b < 65536) g_snap_stamps[8 * g_sn_b + 5] += 1;  // groups
 #endif
-      if (!__ballot(more)) break;
     }
     SN_ACC(3, t2);
 #ifdef PBL_SNAP_STAMPS
