@@ -429,10 +429,18 @@ struct Args {
 
 // Store 16 bytes (w) covering global bytes [ga, ga+16) of which only [lo, hi)
 // belong to this block: one dwordx4 store when whole, byte stores at the edges.
+// PBL_STORE16_NT: whole granules as non-temporal stores (A/B).
+#ifndef PBL_STORE16_NT
+#define PBL_STORE16_NT 0
+#endif
 __device__ inline void store16(uint8_t* base_, uint64_t ga, uint64_t lo, uint64_t hi, uint4 w) {
   const gptr<uint8_t> base = to_glb(base_);
   if (ga >= lo && ga + 16 <= hi) {
+#if PBL_STORE16_NT
+    __builtin_nontemporal_store(u32x4{w.x, w.y, w.z, w.w}, (gptr<u32x4>)(base + ga));
+#else
     *(gptr<u32x4>)(base + ga) = u32x4{w.x, w.y, w.z, w.w};
+#endif
     return;
   }
 #pragma unroll

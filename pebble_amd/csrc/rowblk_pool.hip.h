@@ -131,32 +131,47 @@ __device__ __forceinline__ uint32_t dpp_incl_scan(uint32_t v) {
 }
 __device__ __forceinline__ uint32_t last_lane(uint32_t v) { return __builtin_amdgcn_readlane(v, kWave - 1); }
 
+// Output stores.  PBL_POOL_NT: non-temporal (streaming) stores, so the
+// outputs do not displace the staged blocks' lines that the emit re-reads
+// from L2 (A/B).
+#ifndef PBL_POOL_NT
+#define PBL_POOL_NT 1  // measured: config 2 1200 vs 1183, config 4 1073 vs 1062 GiB/s
+#endif
+template <class T>
+__device__ __forceinline__ void st_out(gptr<T> p, T v) {
+#if PBL_POOL_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 // Bytes [0, n) of w (n <= 16) to p, any alignment: one 16-B store when whole,
 // else the fewest 8/4/2/1-B stores (nothing past n: the next key belongs to
 // another lane).
 __device__ __forceinline__ void store_n(gptr<uint8_t> p, const uint4& w, uint32_t n) {
   if (n == 16) {
-    *(gptr<u32x4_ug>)p = u32x4{w.x, w.y, w.z, w.w};
+    st_out((gptr<u32x4_ug>)p, u32x4_ug{w.x, w.y, w.z, w.w});
     return;
   }
   uint64_t lo = uint64_t(w.x) | uint64_t(w.y) << 32, hi = uint64_t(w.z) | uint64_t(w.w) << 32;
   uint32_t o = 0;
   if (n & 8) {
-    *(gptr<u64_ug>)p = lo;
+    st_out((gptr<u64_ug>)p, u64_ug(lo));
     lo = hi;
     o = 8;
   }
   if (n & 4) {
-    *(gptr<u32_ug>)(p + o) = uint32_t(lo);
+    st_out((gptr<u32_ug>)(p + o), u32_ug(lo));
     lo >>= 32;
     o += 4;
   }
   if (n & 2) {
-    *(gptr<u16_ug>)(p + o) = uint16_t(lo);
+    st_out((gptr<u16_ug>)(p + o), u16_ug(lo));
     lo >>= 16;
     o += 2;
   }
-  if (n & 1) *(p + o) = uint8_t(lo);
+  if (n & 1) st_out(p + o, uint8_t(lo));
 }
 
 // 16 bytes of the block in global memory at block offset i (any alignment,
@@ -524,8 +539,8 @@ __device__ __forceinline__ void key_store(const Slot<kHide>& W, const GSrc& V, c
     const uint32_t ko = kcar + incl - ukl;
     kcar += last_lane(incl);
     if (j > nkv) continue;
-    to_glb(O.key_off)[kvb + b + j] = ko;
-    to_glb(O.val_off)[kvb + b + j] = W.vp[j] & 0xffffu;
+    st_out(to_glb(O.key_off) + (kvb + b + j), ko);
+    st_out(to_glb(O.val_off) + (kvb + b + j), uint32_t(W.vp[j] & 0xffffu));
     if (j == nkv) continue;
     const uint32_t kl = m_klen(m), sh = m_sh(m);
     uint64_t t;
@@ -555,9 +570,9 @@ __device__ __forceinline__ void key_store(const Slot<kHide>& W, const GSrc& V, c
         store_n(kbytes + ko, w, ukl);
       }
     }
-    to_glb(O.trailer)[kvb + j] = with_seq(t, A.in.synthetic_seq_num, flags);
-    if (O.kv_flags) to_glb(O.kv_flags)[kvb + j] = uint8_t(f);
-    if (O.entry_off) to_glb(O.entry_off)[kvb + j] = m_ksrc(m) - m_hl(m);
+    st_out(to_glb(O.trailer) + (kvb + j), uint64_t(with_seq(t, A.in.synthetic_seq_num, flags)));
+    if (O.kv_flags) st_out(to_glb(O.kv_flags) + (kvb + j), uint8_t(f));
+    if (O.entry_off) st_out(to_glb(O.entry_off) + (kvb + j), uint32_t(m_ksrc(m) - m_hl(m)));
   }
 }
 
@@ -614,11 +629,11 @@ __device__ __forceinline__ void val_store(const uint32_t* vp, uint32_t nkv, uint
 #pragma unroll
   for (int u = 0; u < kVG; u++) {
     const VSeg S = val_seg(vp, nkv, jl + 8 * u);
-    if (S.has) *(gptr<u32x4_ug>)(vbytes + S.vo + S.q) = B.x[u];
+    if (S.has) st_out((gptr<u32x4_ug>)(vbytes + S.vo + S.q), u32x4_ug(B.x[u]));
     if (S.vl > 128 && S.vl <= kWaveVal) {
       for (uint32_t o = 16 * c + 128; o < S.vl; o += 128) {
         const uint32_t q = o < S.vl - 16 ? o : S.vl - 16;
-        *(gptr<u32x4_ug>)(vbytes + S.vo + q) = *(gptr<const u32x4_ug>)(g + S.vs + q);
+        st_out((gptr<u32x4_ug>)(vbytes + S.vo + q), u32x4_ug(*(gptr<const u32x4_ug>)(g + S.vs + q)));
       }
     } else if (S.vl < 16) {
       for (uint32_t o = c; o < S.vl; o += 8) vbytes[S.vo + o] = g[S.vs + o];
@@ -661,7 +676,7 @@ __device__ __forceinline__ void copy_values_grp(const uint32_t* vp, gptr<const u
 #pragma unroll
         for (int k = 0; k < 4; k++) {
           const uint32_t o = o0 + 16u * kWave * k, q = o < ll - 16 ? o : ll - 16;
-          if (o < ll) *(gptr<u32x4_ug>)(vbytes + lo + q) = y[k];
+          if (o < ll) st_out((gptr<u32x4_ug>)(vbytes + lo + q), u32x4_ug(y[k]));
         }
       }
     }
