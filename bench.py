@@ -64,7 +64,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the host->device->host (PCIe-inclusive) pass")
     p.add_argument("--e2e-chunk", type=int, default=2048, help="blocks per PCIe pipeline chunk")
-    p.add_argument("--kernel", choices=["auto", "single", "pipe", "pool"], default="auto",
+    p.add_argument("--kernel", choices=["auto", "single", "pipe", "pool", "res"], default="auto",
                    help="A/B: PBL_KERNEL_SINGLE / PBL_KERNEL_PIPE batch flags (auto = pool for row batches)")
     p.add_argument("--launch-check", action="store_true",
                    help="launcher self-test without a GPU: N gloo ranks report in, rank 0 prints one JSON line")
@@ -246,8 +246,8 @@ def main():
 
     nb = a.blocks or (131072 if a.workload == "mixed" else 65536)
     flags = N.PBL_ROW_VALUE_PREFIX if a.value_prefix else 0
-    flags |= {"auto": 0, "single": N.PBL_KERNEL_SINGLE, "pipe": N.PBL_KERNEL_PIPE, "pool": N.PBL_KERNEL_POOL}[a.kernel]
-    row_kernel = {"single": "rowblk_decode_kernel", "pipe": "rowblk_pipe_kernel"}.get(a.kernel, "rowblk_pool_kernel")
+    flags |= {"auto": 0, "single": N.PBL_KERNEL_SINGLE, "pipe": N.PBL_KERNEL_PIPE, "pool": N.PBL_KERNEL_POOL, "res": N.PBL_KERNEL_RES}[a.kernel]
+    row_kernel = {"single": "rowblk_decode_kernel", "pipe": "rowblk_pipe_kernel", "res": "rowblk_res_kernel"}.get(a.kernel, "rowblk_pool_kernel")
     seed = a.seed + 7919 * rank
     t0 = time.time()
     block_fmt = None

@@ -83,9 +83,12 @@ enum {
                                      the obsolete bit (row) or whose isObsolete bit
                                      is set (colblk) are not emitted; every count and
                                      offset covers the visible KVs only, restart
-                                     words are kept.  Ignored with PBL_ROW_RAW_KEYS.
-                                     (The name is historical: it applies to colblk
-                                     batches too.)                                  */
+                                     words are kept.  Row blocks ignore it with
+                                     PBL_ROW_RAW_KEYS (a raw key has no trailer);
+                                     colblk blocks always honour it.  Single-format
+                                     and mixed (block_format) batches alike.  (The
+                                     name is historical: it applies to colblk
+                                     blocks too.)                                   */
 #define PBL_BATCH_VARLEN 0x100u   /* scheduling hint, no effect on results: block
                                      lengths vary widely (e.g. Zipf value sizes), so a
                                      colblk batch takes the one-block-per-workgroup
@@ -103,6 +106,9 @@ enum {
                                      even with PBL_BATCH_VARLEN                    */
 /* 0x800u, 0x1000u, 0x2000u: retired A/B kernels (one-wave-per-block flat, run-
    major, HBM-walking row kernels; removed, the bits are ignored)               */
+#define PBL_KERNEL_RES 0x8000u    /* A/B measurement, no effect on results: row
+                                     batches on the block-resident kernel
+                                     (rowblk_res.hip.h)                            */
 #define PBL_KERNEL_POOL 0x4000u   /* row batches on the staging-pool kernel
                                      (rowblk_pool.hip.h): the default; the bit is
                                      accepted for older callers                    */
@@ -257,8 +263,15 @@ typedef struct pbl_phys_batch {
   const uint64_t* block_off; /* [n_blocks] DEVICE offset of each block in `bytes`        */
   const uint32_t* block_len; /* [n_blocks] DEVICE block.Handle.Length (trailer excluded) */
   uint32_t n_blocks;
-  uint32_t reserved;
+  uint32_t flags;            /* PBL_PHYS_* (0: the defaults)                           */
 } pbl_phys_batch;
+/* MinLZ blocks in the MinLZ form (first byte 0, internal/compression/minlz.go:
+   52-72) are decoded on the device only with this flag: the format is restated
+   without bytes from the real encoder to pin it (github.com/minio/minlz is an
+   absent dependency), so by default such blocks report
+   PBL_UNSUPPORTED and the caller decodes them on the host.  MinLZ blocks in
+   the Snappy form (minlz_test.go:31-36) are always decoded.                    */
+#define PBL_PHYS_MINLZ_NATIVE 0x1u
 enum { /* block.ChecksumType (block.go:106-114) */
   PBL_CHECKSUM_NONE = 0, PBL_CHECKSUM_CRC32C = 1, PBL_CHECKSUM_XXHASH = 2, PBL_CHECKSUM_XXHASH64 = 3
 };
@@ -294,7 +307,7 @@ int pbl_decompressed_lengths(const pbl_phys_batch* batch, uint32_t* out_len, uin
  * PBL_UNSUPPORTED) are decoded on the device.  The outputs form a pbl_block_batch {out,
  * out_off, out_len} for pbl_decode_batch (keep out_off 8-B aligned for colblk).
  * zstd's batch path takes a stream-ordered workspace (hipMallocAsync on `stream`,
- * ~72 KB per block, freed on the stream after its last launch); when that
+ * ~40 KB per block, freed on the stream after its last launch); when that
  * allocation fails every zstd block takes the one-wave-per-block decoder instead.
  */
 int pbl_decompress_blocks(const pbl_phys_batch* batch, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,

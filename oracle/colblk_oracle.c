@@ -387,7 +387,59 @@ uint64_t orc_colblk_scan_checksum(const uint8_t* blk, uint64_t len, uint32_t sch
   return h;
 }
 
+/* DataBlockIter under blockiter.Transforms{HideObsoletePoints}
+ * (sstable/colblk/data_block.go:1680-1697): rows whose isObsolete bit is set
+ * (data_block.go:519) are skipped; the block is checked and decoded whole
+ * first, so a block that fails without the transform fails with it. */
+static int colblk_decode_hide(const uint8_t* blk, uint64_t len, uint32_t fmt, orc_block_out* o) {
+  orc_block_out t;
+  memset(&t, 0, sizeof(t));
+  int st = orc_colblk_decode(blk, len, fmt, &t);
+  if (st != OK) {
+    o->n_kv = o->key_bytes = o->val_bytes = o->n_restarts = 0;
+    return st;
+  }
+  const uint64_t n = t.n_kv;
+  uint64_t* tr = calloc(n + 1, 8);
+  uint8_t* fl = calloc(n + 1, 1);
+  uint32_t* eo = calloc(n + 1, 4);
+  uint32_t* ko = calloc(n + 1, 4);
+  uint32_t* vo = calloc(n + 1, 4);
+  uint8_t* kb = calloc(t.key_bytes + 1, 1);
+  uint8_t* vb = calloc(t.val_bytes + 1, 1);
+  orc_block_out f = {0, 0, 0, 0, tr, fl, eo, ko, vo, kb, vb, NULL};
+  st = orc_colblk_decode(blk, len, fmt, &f);
+  uint64_t m = 0, kn = 0, vn = 0;
+  for (uint64_t i = 0; st == OK && i < n; i++) {
+    if (fl[i] & KV_OBSOLETE) continue;
+    const uint32_t kl = ko[i + 1] - ko[i], vl = vo[i + 1] - vo[i];
+    if (o->trailer) {
+      o->trailer[m] = tr[i];
+      if (o->kv_flags) o->kv_flags[m] = fl[i];
+      if (o->entry_off) o->entry_off[m] = eo[i];
+      o->key_off[m] = (uint32_t)kn;
+      o->val_off[m] = (uint32_t)vn;
+      memcpy(o->keys + kn, kb + ko[i], kl);
+      memcpy(o->vals + vn, vb + vo[i], vl);
+    }
+    m++;
+    kn += kl;
+    vn += vl;
+  }
+  if (o->trailer && st == OK) {
+    o->key_off[m] = (uint32_t)kn;
+    o->val_off[m] = (uint32_t)vn;
+  }
+  free(tr); free(fl); free(eo); free(ko); free(vo); free(kb); free(vb);
+  o->n_kv = st == OK ? m : 0;
+  o->key_bytes = st == OK ? kn : 0;
+  o->val_bytes = st == OK ? vn : 0;
+  o->n_restarts = 0;
+  return st;
+}
+
 static int decode_block(const uint8_t* blk, uint64_t len, uint32_t fmt, uint32_t flags, orc_block_out* o) {
+  if (fmt != FMT_ROW && (flags & FLAG_HIDE_OBSOLETE)) return colblk_decode_hide(blk, len, fmt, o);
   if (fmt == FMT_ROW && (flags & FLAG_HIDE_OBSOLETE) && !(flags & FLAG_RAW_KEYS)) {
     /* HideObsoletePoints: rowblk.Iter under blockiter.Transforms{HideObsoletePoints} */
     const orc_transforms t = {0, 1, 0, NULL, 0, NULL, 0};

@@ -56,6 +56,8 @@ PBL_ROW_HIDE_OBSOLETE = 0x8
 PBL_KERNEL_SINGLE = 0x200
 PBL_KERNEL_PIPE = 0x400
 PBL_KERNEL_POOL = 0x4000
+PBL_KERNEL_RES = 0x8000
+PBL_PHYS_MINLZ_NATIVE = 0x1
 
 PBL_KV_RESTART = 0x01
 PBL_KV_RESTART_SAMEPFX = 0x02
@@ -122,7 +124,7 @@ PBL_SPLIT_WHOLE, PBL_SPLIT_TESTKEYS, PBL_SPLIT_CRDB = 0, 1, 2
 
 class PhysBatchC(ctypes.Structure):
     _fields_ = [("bytes", _vp), ("block_off", _vp), ("block_len", _vp), ("n_blocks", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("flags", ctypes.c_uint32)]
 
 
 class FooterC(ctypes.Structure):

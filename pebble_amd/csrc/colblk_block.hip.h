@@ -756,6 +756,15 @@ __device__ __forceinline__ void col_rows(Lds& s, const Args& A, uint32_t b, uint
 // published, then written chunk by chunk at the places a block scan of
 // (visible, key length, value length) gives them: keys straight to global
 // memory, values row by row.
+// Row r's isObsolete bit (data_block.go:519; HideObsoletePoints skips such
+// rows, :1680-1697) and the values column's offset r.
+__device__ __forceinline__ bool row_obsolete(const Src& S, const Desc& d, uint32_t r) {
+  return d.obs_at && ((S.le(d.obs_at + 8 * (r >> 6), 8) >> (r & 63)) & 1);
+}
+__device__ __forceinline__ uint32_t row_voff(const Src& S, const Desc& d, uint32_t r) {
+  return d.v_off.w ? uint32_t(S.le(d.v_off.at + r * d.v_off.w, d.v_off.w)) : 0u;
+}
+
 template <bool F>
 __device__ __forceinline__ void col_rows_hide(Lds& s, const Args& A, uint32_t b, uint32_t schema, const Src& S) {
   const int t = threadIdx.x;
@@ -766,11 +775,8 @@ __device__ __forceinline__ void col_rows_hide(Lds& s, const Args& A, uint32_t b,
   const Desc& d = s.d;
   const uint32_t rows = s.status == PBL_OK ? d.rows : 0;
   const uint32_t nch = (rows + kChunk - 1) / kChunk;
-  const UCol& vo = d.v_off;
-  const auto obsolete = [&](uint32_t r) {
-    return d.obs_at && ((S.le(d.obs_at + 8 * (r >> 6), 8) >> (r & 63)) & 1);
-  };
-  const auto voff = [&](uint32_t r) { return vo.w ? uint32_t(S.le(vo.at + r * vo.w, vo.w)) : 0u; };
+  const auto obsolete = [&](uint32_t r) { return row_obsolete(S, d, r); };
+  const auto voff = [&](uint32_t r) { return row_voff(S, d, r); };
 
   // ---- pass 1: every row checked, the visible ones counted ---------------------
   uint64_t my_n = 0, my_kb = 0, my_vb = 0;

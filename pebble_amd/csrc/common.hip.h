@@ -494,7 +494,7 @@ __device__ inline bool overflows(const pbl_decode_out& O, const uint64_t excl[kN
 // immutable once written; racing first calls store the same values).
 enum PersistentKernel {
   kKRowPipe = 0, kKRowSingle = 1, kKColPipe = 2, kKMixedColSize = 3, kKMixedRow = 4, kKMixedCol = 5,
-  kKRowPool = 6, kKNum = 7
+  kKRowPool = 6, kKRowRes = 7, kKNum = 8
 };
 
 // Resident grid for `fn` on the stream's device (never more than n_units, at

@@ -149,6 +149,13 @@ __global__ void __launch_bounds__(kWave) minlz_kernel(const pbl_phys_batch B, ui
     const uint64_t boff = to_glb(B.block_off)[b];
     const gptr<const uint8_t> src = to_glb(B.bytes + boff);
     if (src[n] != PBL_COMPRESSION_MINLZ || snappy_form(PBL_COMPRESSION_MINLZ, src, n)) continue;
+    if (!(B.flags & PBL_PHYS_MINLZ_NATIVE)) {  // the MinLZ form is opt-in (parity unpinned)
+      if (lane == 0) {
+        to_glb(out_len)[b] = 0;
+        to_glb(status)[b] = PBL_UNSUPPORTED;
+      }
+      continue;
+    }
     gptr<uint8_t> dst = to_glb(out + to_glb(out_off)[b]);
     const uint32_t cap = to_glb(out_cap)[b];
     uint32_t st = PBL_OK, dl = 0, hdr = 0;

@@ -800,6 +800,7 @@ __global__ void __launch_bounds__(kTPB, 3) rowblk_decode_kernel(Args A) {
 
 #include "rowblk_pipe.hip.h"
 #include "rowblk_pool.hip.h"
+#include "rowblk_res.hip.h"
 
 // Mixed row + colblk batch (config 4): per-block format from block_format[];
 // both paths share the ticket order and the look-back state.
@@ -935,6 +936,9 @@ constexpr int kWsColTick2 = 4;  // header u32 [4]: the colblk queue of launch (3
 #ifndef PBL_COL_SIZE_WAVES
 #define PBL_COL_SIZE_WAVES 8  // waves per SIMD (64 VGPRs): config 4 951 at 4 (101 VGPRs), 975 at 8
 #endif
+// kHide (PBL_ROW_HIDE_OBSOLETE): the aggregate counts the visible rows, as
+// col_rows_hide publishes it again in (3).
+template <bool kHide>
 __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PBL_COL_SIZE_WAVES)))
 mixed_col_size_kernel(Args A, const uint32_t* ids) {
   __shared__ col::Desc d;
@@ -950,21 +954,34 @@ mixed_col_size_kernel(Args A, const uint32_t* ids) {
     const col::Src S{nullptr, nullptr, (col::glb_cu8)(A.in.blocks + to_glb(A.in.block_off)[b]), 0u, 0xffffffffu, blen};
     uint32_t st = col::parse_block_wave(S, schema, &d);
     const uint32_t rows = st == PBL_OK ? d.rows : 0;
-    uint64_t kb = 0;
+    uint64_t kb = 0, nv = 0, vb = 0;
     bool bad = false;
     // (not unrolled: 4 rows per lane in flight measured 0.89 against 0.47 ms)
     for (uint32_t r = lane_id(); r < rows; r += kWave) {
       const col::RowParts p = col::row_parts<false>(S, d, schema, r);
       bad |= !p.ok || !col::value_ok(S, d, r);
-      kb += p.klen;
+      if (!kHide || !col::row_obsolete(S, d, r)) {
+        kb += p.klen;
+        if (kHide) {
+          nv++;
+          vb += col::row_voff(S, d, r + 1) - col::row_voff(S, d, r);
+        }
+      }
     }
     kb = wave_sum(kb);
+    if (kHide) {
+      nv = wave_sum(nv);
+      vb = wave_sum(vb);
+    } else {
+      nv = rows;
+      vb = uint64_t(d.v_hi - d.v_lo);
+    }
     if (st == PBL_OK) {
       if (__ballot(bad)) st = PBL_CORRUPT_BOUNDS;
-      else if (kb > 0xffffffffull || uint64_t(d.v_hi - d.v_lo) > 0xffffffffull) st = PBL_UNSUPPORTED;
+      else if (kb > 0xffffffffull || vb > 0xffffffffull) st = PBL_UNSUPPORTED;
     }
     const bool ok = st == PBL_OK;
-    const uint64_t agg[kNumComp] = {ok ? rows : 0u, ok ? kb : 0ull, ok ? uint64_t(d.v_hi - d.v_lo) : 0ull, 0ull};
+    const uint64_t agg[kNumComp] = {ok ? nv : 0u, ok ? kb : 0ull, ok ? vb : 0ull, 0ull};
     lb_publish(lb_state, nb, b, agg);
     wave_sync();  // (d is rewritten by the next block's parse)
   }
@@ -986,6 +1003,26 @@ __global__ void __launch_bounds__(kTPB, PBL_COL_PIPE_WG) mixed_col_kernel(Args A
   uint32_t* hdr = reinterpret_cast<uint32_t*>(A.out.workspace);
   const uint32_t n_row = __hip_atomic_load(to_glb(hdr) + kWsRowCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   col::cpipe::col_pipe_body(L, A, ListQueue{hdr + kWsColTick2, ids + n_row, nb - n_row, nb});
+}
+
+// (3) with HideObsoletePoints fused: the one-block-per-workgroup colblk form
+// (col_rows_hide) over the colblk list, in ticket order; every row block has
+// its inclusive prefix by now.
+__global__ void __launch_bounds__(kTPB) mixed_col_hide_kernel(Args A, const uint32_t* ids) {
+  __shared__ col::Lds s;
+  __shared__ uint32_t tk;
+  const uint32_t nb = A.in.n_blocks;
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(A.out.workspace);
+  const uint32_t n_row = __hip_atomic_load(to_glb(hdr) + kWsRowCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    if (threadIdx.x == 0) tk = g_atomic_add(hdr + kWsColTick2, 1u);
+    __syncthreads();
+    const uint32_t t = tk;
+    if (t >= nb - n_row) break;
+    const uint32_t b = to_glb(ids)[n_row + t];
+    col::col_block<true>(s, A, b, to_glb(A.in.block_format)[b]);
+    __syncthreads();  // (the LDS and tk are the next block's)
+  }
 }
 
 // Size pass epilogue: a block that decoded reports PBL_OK, not the forced
@@ -1089,6 +1126,30 @@ int launch_row_pool(const pbl::Args& a, hipStream_t st, bool values) {
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }
 
+// Row batches on the block-resident kernel (rowblk_res.hip.h), with the same
+// big-block passes around it.
+int launch_row_res(const pbl::Args& a, hipStream_t st, bool values) {
+  const uint32_t nb = a.in.n_blocks;
+  const bool hide = (a.in.flags & PBL_ROW_HIDE_OBSOLETE) && !(a.in.flags & PBL_ROW_RAW_KEYS);
+  const void* fn = hide ? reinterpret_cast<const void*>(pbl::row::res::rowblk_res_kernel<true>)
+                        : reinterpret_cast<const void*>(pbl::row::res::rowblk_res_kernel<false>);
+  int cus = 0;
+  const uint64_t grid = pbl::persistent_grid(st, pbl::kKRowRes, fn,
+                                             (uint64_t(nb) + pbl::row::res::kNW - 1) / pbl::row::res::kNW, &cus,
+                                             pbl::row::res::kTPBR);
+  if (!grid) return PBL_DEVICE_ERROR;
+  const uint32_t small = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4));
+  hipLaunchKernelGGL(pbl::row::pipe::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+  if (hide)
+    hipLaunchKernelGGL(pbl::row::res::rowblk_res_kernel<true>, dim3(uint32_t(grid)), dim3(pbl::row::res::kTPBR), 0,
+                       st, a, static_cast<const uint32_t*>(nullptr));
+  else
+    hipLaunchKernelGGL(pbl::row::res::rowblk_res_kernel<false>, dim3(uint32_t(grid)), dim3(pbl::row::res::kTPBR), 0,
+                       st, a, static_cast<const uint32_t*>(nullptr));
+  if (values) hipLaunchKernelGGL(pbl::row::pipe::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+  return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
+}
+
 // HideObsoletePoints fused into the decode: the row staging-pool kernel (and
 // the general walk it hands blocks to) and the colblk kernels implement it;
 // other row kernels are A/B forms only, so such batches always take the pool.
@@ -1104,7 +1165,11 @@ bool hide_row(const pbl_block_batch* b) {
 // (A/B); the default splits the ids by format and runs the mixed pipeline,
 // with the big row blocks' size / value passes around it.
 int launch_mixed(const pbl_block_batch* batch, const pbl::Args& a, hipStream_t st, bool single, bool values) {
-  if (single) {
+  // HideObsoletePoints: colblk rows by their isObsolete bit, row entries by
+  // their trailer's obsolete bit unless the keys are raw
+  const bool hide = (batch->flags & PBL_ROW_HIDE_OBSOLETE) != 0;
+  const bool hide_rows = hide && !(batch->flags & PBL_ROW_RAW_KEYS);
+  if (single && !hide) {
     hipLaunchKernelGGL(pbl::row::mixed_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
     return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
   }
@@ -1126,21 +1191,33 @@ int launch_mixed(const pbl_block_batch* batch, const pbl::Args& a, hipStream_t s
   const uint32_t small = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4));
   const uint32_t* cids = static_cast<const uint32_t*>(ids);
   hipLaunchKernelGGL(pbl::row::pipe::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
-  hipLaunchKernelGGL(pbl::row::mixed_col_size_kernel, dim3(g_cs), dim3(pbl::kWave), 0, st, a, cids);
+  if (hide)
+    hipLaunchKernelGGL(pbl::row::mixed_col_size_kernel<true>, dim3(g_cs), dim3(pbl::kWave), 0, st, a, cids);
+  else
+    hipLaunchKernelGGL(pbl::row::mixed_col_size_kernel<false>, dim3(g_cs), dim3(pbl::kWave), 0, st, a, cids);
 #if PBL_MIXED_POOL
   // the row blocks on the staging-pool kernel, over the row id list
-  const uint64_t g_p = pbl::persistent_grid(st, pbl::kKRowPool,
-                                            reinterpret_cast<const void*>(pbl::row::pool::rowblk_pool_kernel<false>),
+  const void* pfn = hide_rows ? reinterpret_cast<const void*>(pbl::row::pool::rowblk_pool_kernel<true>)
+                              : reinterpret_cast<const void*>(pbl::row::pool::rowblk_pool_kernel<false>);
+  const uint64_t g_p = pbl::persistent_grid(st, pbl::kKRowPool, pfn,
                                             (uint64_t(nb) + pbl::row::pool::kNW - 1) / pbl::row::pool::kNW, &cus,
                                             pbl::row::pool::kTPBP);
   if (!g_p) return PBL_DEVICE_ERROR;
   (void)g_r;
-  hipLaunchKernelGGL(pbl::row::pool::rowblk_pool_kernel<false>, dim3(uint32_t(g_p)), dim3(pbl::row::pool::kTPBP), 0,
-                     st, a, cids);
+  if (hide_rows)
+    hipLaunchKernelGGL(pbl::row::pool::rowblk_pool_kernel<true>, dim3(uint32_t(g_p)), dim3(pbl::row::pool::kTPBP), 0,
+                       st, a, cids);
+  else
+    hipLaunchKernelGGL(pbl::row::pool::rowblk_pool_kernel<false>, dim3(uint32_t(g_p)), dim3(pbl::row::pool::kTPBP), 0,
+                       st, a, cids);
 #else
   hipLaunchKernelGGL(pbl::row::mixed_row_kernel, dim3(uint32_t(g_r)), dim3(pbl::row::pipe::kPTPB), 0, st, a, cids);
 #endif
-  hipLaunchKernelGGL(pbl::row::mixed_col_kernel, dim3(uint32_t(g_c)), dim3(pbl::kTPB), 0, st, a, cids);
+  if (hide)  // (workgroups loop over the colblk list's tickets; 21 KB of LDS each)
+    hipLaunchKernelGGL(pbl::row::mixed_col_hide_kernel, dim3(uint32_t(std::min<uint64_t>(nb, uint64_t(cus) * 7))),
+                       dim3(pbl::kTPB), 0, st, a, cids);
+  else
+    hipLaunchKernelGGL(pbl::row::mixed_col_kernel, dim3(uint32_t(g_c)), dim3(pbl::kTPB), 0, st, a, cids);
   if (values)
     hipLaunchKernelGGL(pbl::row::pipe::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
@@ -1173,7 +1250,6 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
   a.in = *batch;
   a.out = *out;
   if (batch->block_format) {
-    if ((batch->flags & PBL_ROW_HIDE_OBSOLETE) && !(batch->flags & PBL_ROW_RAW_KEYS)) return PBL_UNSUPPORTED;
     const int rc = launch_mixed(batch, a, st, batch->flags & PBL_KERNEL_SINGLE, true);
     if (rc != PBL_OK) return rc;
   } else {
@@ -1182,6 +1258,7 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
     // fused).  PBL_KERNEL_SINGLE / PBL_KERNEL_PIPE keep the one-block-per-
     // workgroup kernel and the two-stage pipeline for A/B measurement.
     const bool single = (batch->flags & PBL_KERNEL_SINGLE) != 0;
+    if (batch->flags & PBL_KERNEL_RES) return launch_row_res(a, st, true);
     if (hide_row(batch) || !(batch->flags & (PBL_KERNEL_SINGLE | PBL_KERNEL_PIPE))) return launch_row_pool(a, st, true);
     const void* fn = single ? reinterpret_cast<const void*>(pbl::row::rowblk_decode_kernel)
                             : reinterpret_cast<const void*>(pbl::row::pipe::rowblk_pipe_kernel);
@@ -1215,8 +1292,6 @@ int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stre
   if (!batch->blocks || !batch->block_off || !batch->block_len || !out->workspace ||
       out->workspace_bytes < pbl::ws_alloc_bytes(batch->n_blocks))
     return PBL_INVALID_ARG;
-  if (batch->block_format && (batch->flags & PBL_ROW_HIDE_OBSOLETE) && !(batch->flags & PBL_ROW_RAW_KEYS))
-    return PBL_UNSUPPORTED;
   // the decode with every per-KV pointer NULL and zero capacities: each block
   // takes its overflow branch (sizes computed and published, nothing written);
   // the fixup then reports the statuses the decode would have had
@@ -1243,6 +1318,9 @@ int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stre
     // pointers), minus the big-block value pass
     if (batch->block_format) {
       rc = launch_mixed(batch, a, st, batch->flags & PBL_KERNEL_SINGLE, false);
+      if (rc != PBL_OK) return rc;
+    } else if (batch->flags & PBL_KERNEL_RES) {
+      rc = launch_row_res(a, st, false);
       if (rc != PBL_OK) return rc;
     } else if (hide_row(batch) || !(batch->flags & PBL_KERNEL_PIPE)) {
       rc = launch_row_pool(a, st, false);

@@ -422,13 +422,15 @@ struct GSrc {
 };
 
 // byte p of the internal key of entry j (source = max{i <= j : shared_i <= p})
-__device__ __forceinline__ uint32_t key_byte(const uint64_t* M0, const GSrc& V, int j, uint32_t p) {
+template <class Src>
+__device__ __forceinline__ uint32_t key_byte(const uint64_t* M0, const Src& V, int j, uint32_t p) {
   uint64_t m = M0[j];
   while (p < m_sh(m)) m = M0[--j];
   return V.byte(m_ksrc(m) + p - m_sh(m));
 }
 
-__device__ __forceinline__ uint64_t trailer_of(const uint64_t* M0, const GSrc& V, int j, uint64_t m, uint32_t* fl,
+template <class Src>
+__device__ __forceinline__ uint64_t trailer_of(const uint64_t* M0, const Src& V, int j, uint64_t m, uint32_t* fl,
                                                uint32_t flags) {
   if (flags & PBL_ROW_RAW_KEYS) return 0;
   const uint32_t kl = m_klen(m);
@@ -448,7 +450,8 @@ __device__ __forceinline__ uint64_t trailer_of(const uint64_t* M0, const GSrc& V
 // Key bytes [c, c + n) of KV m (n <= 16) merged from the segments of its prefix
 // chain: each a 16-B read that starts where the chunk's first byte would sit in
 // that entry (at most 15 bytes before the block).
-__device__ __forceinline__ uint4 key_chunk(const uint64_t* M0, const GSrc& V, uint64_t m, uint32_t c, uint32_t n) {
+template <class Src>
+__device__ __forceinline__ uint4 key_chunk(const uint64_t* M0, const Src& V, uint64_t m, uint32_t c, uint32_t n) {
   const uint32_t ce = c + n;
   uint32_t cur = ce;
   uint4 w = make_uint4(0, 0, 0, 0);
@@ -496,8 +499,8 @@ __device__ __forceinline__ bool key_fast(uint64_t m, uint64_t mp, bool raw) {
   return ukl_of(m, raw) <= 16 && (sh == 0 || m_sh(mp) == 0) && (raw || kl < 8 || kl - 8 >= sh);
 }
 
-template <bool kHide>
-__device__ __forceinline__ void key_load(const Slot<kHide>& W, const GSrc& V, bool raw, uint32_t j0, uint32_t nkv,
+template <bool kHide, class Src>
+__device__ __forceinline__ void key_load(const Slot<kHide>& W, const Src& V, bool raw, uint32_t j0, uint32_t nkv,
                                          KBatch& K) {
   const int l = lane_id();
 #pragma unroll
@@ -522,8 +525,8 @@ __device__ __forceinline__ void key_load(const Slot<kHide>& W, const GSrc& V, bo
 
 // The batch's stores.  Key output offsets: an exclusive wave scan of the user-
 // key lengths per u, `kcar` carrying the running total (KV nkv gets the total).
-template <bool kHide>
-__device__ __forceinline__ void key_store(const Slot<kHide>& W, const GSrc& V, const Args& A, uint32_t b, uint32_t j0,
+template <bool kHide, class Src>
+__device__ __forceinline__ void key_store(const Slot<kHide>& W, const Src& V, const Args& A, uint32_t b, uint32_t j0,
                                           uint32_t nkv, uint64_t kvb, uint64_t kbb, const KBatch& K, uint32_t& kcar) {
   const int l = lane_id();
   const uint32_t flags = A.in.flags;
@@ -613,13 +616,15 @@ __device__ __forceinline__ VSeg val_seg(const uint32_t* vp, uint32_t nkv, uint32
 }
 
 // The step's first chunks from the block (every lane loads, from the block's
-// first bytes when it has no chunk: no conditionally defined registers).
+// first 16-B aligned granule when it has no chunk: no conditionally defined
+// registers, and no read past the block's last granule however short it is).
 __device__ __forceinline__ void val_load(const uint32_t* vp, gptr<const uint8_t> g, uint32_t nkv, uint32_t j0, VBatch& B) {
   const uint32_t jl = j0 + (uint32_t(lane_id()) >> 3);
+  const uint32_t ph = uint32_t(reinterpret_cast<uintptr_t>(g) & 15u);
 #pragma unroll
   for (int u = 0; u < kVG; u++) {
     const VSeg S = val_seg(vp, nkv, jl + 8 * u);
-    B.x[u] = *(gptr<const u32x4_ug>)(g + (S.has ? S.vs + S.q : 0u));
+    B.x[u] = *(gptr<const u32x4_ug>)(g + (S.has ? int32_t(S.vs + S.q) : -int32_t(ph)));
   }
 }
 
@@ -935,7 +940,7 @@ __device__ __forceinline__ void block_emit(const Pend& P, const Slot<kHide>& W, 
   uint32_t rs0 = 0;
   const bool ok0 = P.status == PBL_OK;
   if (ok0) {
-    key_load<kHide>(W, KS, raw, 0, nkv, K);
+    key_load<kHide, GSrc>(W, KS, raw, 0, nkv, K);
     val_load(W.vp, gb, nkv, 0, VB);
     if (O.restarts && uint32_t(l) < nres) rs0 = KS.le32(P.roff + 4 * l);
   }
@@ -958,11 +963,11 @@ __device__ __forceinline__ void block_emit(const Pend& P, const Slot<kHide>& W, 
   const uint64_t kvb = excl[0], kbb = excl[1], vbb = excl[2], rbb = excl[3];
   if (O.restarts && uint32_t(l) < nres) to_glb(O.restarts)[rbb + l] = rs0;
   uint32_t kcar = 0;
-  key_store<kHide>(W, KS, A, b, 0, nkv, kvb, kbb, K, kcar);
+  key_store<kHide, GSrc>(W, KS, A, b, 0, nkv, kvb, kbb, K, kcar);
   for (uint32_t j0 = kWave * kKU; j0 <= nkv; j0 += kWave * kKU) {
     KBatch N;
-    key_load<kHide>(W, KS, raw, j0, nkv, N);
-    key_store<kHide>(W, KS, A, b, j0, nkv, kvb, kbb, N, kcar);
+    key_load<kHide, GSrc>(W, KS, raw, j0, nkv, N);
+    key_store<kHide, GSrc>(W, KS, A, b, j0, nkv, kvb, kbb, N, kcar);
   }
   if (O.restarts)
     for (uint32_t r = kWave + l; r < nres; r += kWave) to_glb(O.restarts)[rbb + r] = KS.le32(P.roff + 4 * r);

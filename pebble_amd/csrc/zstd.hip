@@ -140,7 +140,11 @@ hipError_t launch_zstd(const pbl_phys_batch& batch, uint8_t* out, const uint64_t
     ws = nullptr;
   }
   if (ws) {
-    if (hipMemsetAsync(ws, 0, sizeof(zstd::WsHdr), st) != hipSuccess) return hipGetLastError();
+    if (hipMemsetAsync(ws, 0, sizeof(zstd::WsHdr), st) != hipSuccess) {
+      const hipError_t e = hipGetLastError();
+      (void)hipFreeAsync(ws, st);
+      return e;
+    }
     hipLaunchKernelGGL(zstd::zstd_prep_kernel, dim3(std::min<uint32_t>(n, 8192)), dim3(kWave), 0, st, batch, out, out_off,
                        out_cap, ws);
     hipLaunchKernelGGL(zstd::zstd_lit_kernel, dim3((4ull * n + 255) / 256), dim3(256), 0, st, batch, out, out_off, ws);

@@ -45,7 +45,11 @@ constexpr uint32_t kTblBytes = 6656;  // per-block table slot: Huffman 2048 x u1
 // sequence words of workspace per block, shared through a bump counter (text
 // at level 3 runs ~4.7 K sequences per 32 KiB block; a block that finds the
 // area full is left to zstd_kernel)
-constexpr uint32_t kSeqPerBlock = 8192;
+// Sequence words reserved per block ON AVERAGE: the area is one bump
+// allocation (seq_ctr) over the whole batch, so a long block borrows from short
+// ones; a batch that runs out sends the rest of its blocks to zstd_kernel.  A
+// 32 KiB text block at ratio 2.66 holds ~3-4 K sequences.
+constexpr uint32_t kSeqPerBlock = 4096;
 
 struct FDesc {
   uint32_t fast, D, regen, ltype;
@@ -80,7 +84,7 @@ struct FastWs {
     W.desc = reinterpret_cast<FDesc*>(p + sizeof(WsHdr));
     W.tbl = p + sizeof(WsHdr) + uint64_t(n) * sizeof(FDesc);
     W.seq = reinterpret_cast<uint64_t*>(W.tbl + uint64_t(n) * kTblBytes);
-    W.seq_cap = n * kSeqPerBlock;
+    W.seq_cap = uint32_t(std::min<uint64_t>(uint64_t(n) * kSeqPerBlock, 0xffffffffull));
     return W;
   }
   __device__ uint16_t* huf(uint32_t b) const { return reinterpret_cast<uint16_t*>(tbl + uint64_t(b) * kTblBytes); }

@@ -25,22 +25,23 @@ class PhysBatch:
     bytes: torch.Tensor      # uint8, the file bytes holding the blocks
     block_off: torch.Tensor  # int64 [n]: offset of each block
     block_len: torch.Tensor  # int32 [n]: block.Handle.Length (the trailer follows)
+    flags: int = 0           # PBL_PHYS_* (PBL_PHYS_MINLZ_NATIVE: decode the MinLZ form)
 
     @property
     def n_blocks(self) -> int:
         return int(self.block_off.numel())
 
     @classmethod
-    def from_host(cls, blob: np.ndarray, off, lens, device="cuda") -> "PhysBatch":
+    def from_host(cls, blob: np.ndarray, off, lens, device="cuda", flags: int = 0) -> "PhysBatch":
         b = np.zeros(len(blob) + 16, np.uint8)
         b[: len(blob)] = np.frombuffer(bytes(blob), np.uint8) if isinstance(blob, (bytes, bytearray)) else blob
         return cls(torch.from_numpy(b).to(device),
                    torch.from_numpy(np.ascontiguousarray(off, np.uint64).view(np.int64)).to(device),
-                   torch.from_numpy(np.ascontiguousarray(lens, np.uint32).view(np.int32)).to(device))
+                   torch.from_numpy(np.ascontiguousarray(lens, np.uint32).view(np.int32)).to(device), flags)
 
     def c_struct(self) -> N.PhysBatchC:
         return N.PhysBatchC(self.bytes.data_ptr(), self.block_off.data_ptr(), self.block_len.data_ptr(),
-                            self.n_blocks, 0)
+                            self.n_blocks, self.flags)
 
 
 def verify_checksums(pb: PhysBatch, checksum_type: int, stream=None):

@@ -14,7 +14,7 @@ import pytest
 
 import oracle
 from pebble_amd import _native as N
-from pebble_amd.batch import BlockBatch, DecodeError, decode
+from pebble_amd.batch import BlockBatch, decode
 from pebble_amd.rowblk import gen_row_blocks
 from colutil import build_block, random_rows
 from pebble_amd.colblk import SCHEMA_CRDB1, SCHEMA_DEFAULT
@@ -105,11 +105,44 @@ def test_colblk_config3_shaped():
     assert_same(g, o, "config-3 shaped")
 
 
-def test_not_fused_for_mixed():
-    rng = random.Random(71)
-    rows = random_rows(rng, SCHEMA_CRDB1, 20)
-    blocks = [build_block(SCHEMA_CRDB1, rows, 16)[0], random_block(rng)[0]]
+@pytest.mark.parametrize("flags", [0, N.PBL_ROW_VALUE_PREFIX])
+def test_mixed_batches(flags):
+    """Mixed row + colblk batches under the flag (config 4's shape): colblk rows
+    by their isObsolete bit, row entries by their trailer's obsolete bit, every
+    block placed by one look-back over the batch order; against the oracle's
+    fused decode (pinned by test_oracle_hide.py), and the size pass agrees."""
+    from pebble_amd.batch import size_batch
+    rng = random.Random(71 + flags)
+    blocks, fmts = [], []
+    for i in range(300):
+        k = rng.randrange(4)
+        if k == 0:
+            blocks.append(mvcc_block(rng, rng.randint(1, 300), rng.choice([1, 2, 16, 33]), rng.random() < 0.5,
+                                     rng.random() < 0.7))
+            fmts.append(N.PBL_FMT_ROW)
+        elif k == 1:
+            blocks.append(random_block(rng)[0])
+            fmts.append(N.PBL_FMT_ROW)
+        else:
+            schema = SCHEMA_DEFAULT if k == 2 else SCHEMA_CRDB1
+            rows = random_rows(rng, schema, rng.choice([1, 5, 17, 100, 300]), shared=rng.choice([0, 3]),
+                               val_len=(0, rng.choice([3, 50, 400])))
+            blocks.append(build_block(schema, rows, rng.choice([1, 4, 16]))[0])
+            fmts.append(schema)
+    blocks.append(mvcc_block(rng, 2500, 16))  # past the 32 KiB stage
+    fmts.append(N.PBL_FMT_ROW)
+    for i in range(0, len(blocks), 37):  # a few corrupt blocks stay failed
+        b = bytearray(blocks[i])
+        b[rng.randrange(len(b))] ^= 0x5A
+        blocks[i] = bytes(b)
     buf, off, lens = pack(blocks)
-    with pytest.raises(DecodeError, match="UNSUPPORTED"):
-        decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, HIDE,
-                                    block_format=np.array([SCHEMA_CRDB1, N.PBL_FMT_ROW], np.uint8)))
+    bf = np.array(fmts, np.uint8)
+    o = oracle.decode_batch(buf, off, lens, 0, bf, flags | HIDE)
+    plain = oracle.decode_batch(buf, off, lens, 0, bf, flags)
+    bb = BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, flags | HIDE, block_format=bf)
+    g = decode(bb).to_host()
+    assert_same(g, o, f"mixed hide flags={flags}")
+    assert 0 < g["n_kv"] < plain["n_kv"]
+    t = size_batch(bb).read_totals()
+    assert int(t.n_kv) == int(o["n_kv"]) and int(t.key_bytes) == int(o["key_bytes_total"])
+    assert int(t.val_bytes) == int(o["val_bytes_total"])

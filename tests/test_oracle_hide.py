@@ -62,3 +62,50 @@ def test_hidden_point_with_empty_set_value_iterates():
     assert oracle.decode_batch(buf, off, lens, 0, None, N.PBL_ROW_VALUE_PREFIX)["blk_status"][0] != 0
     r = oracle.decode_batch(buf, off, lens, 0, None, N.PBL_ROW_VALUE_PREFIX | HIDE)
     assert r["blk_status"][0] == 0 and r["n_kv"] == 2
+
+
+def test_fused_hide_colblk_and_mixed_match_transform_restatement():
+    """Colblk blocks under the flag (DataBlockIter, data_block.go:1680-1697:
+    isObsolete rows skipped) and mixed row + colblk batches: the oracle's fused
+    decode equals the transform restatement over its plain decode, array for
+    array (the mixed GPU test checks the device against the fused form)."""
+    from colutil import build_block, random_rows
+    from pebble_amd.colblk import SCHEMA_CRDB1, SCHEMA_DEFAULT
+    rng = random.Random(7)
+    blocks, fmts = [], []
+    for i in range(120):
+        if i % 3 == 2:
+            blocks.append(mvcc_block(rng, rng.randint(1, 200), rng.choice([1, 4, 16]), rng.random() < 0.5,
+                                     rng.random() < 0.7))
+            fmts.append(N.PBL_FMT_ROW)
+        else:
+            schema = SCHEMA_DEFAULT if i % 3 == 0 else SCHEMA_CRDB1
+            rows = random_rows(rng, schema, rng.choice([1, 5, 17, 100, 300]), shared=rng.choice([0, 3]),
+                               val_len=(0, rng.choice([3, 50, 400])))
+            blocks.append(build_block(schema, rows, rng.choice([1, 4, 16]))[0])
+            fmts.append(schema)
+    for i in range(0, 120, 29):  # a few corrupt blocks stay failed
+        b = bytearray(blocks[i])
+        b[rng.randrange(len(b))] ^= 0x5A
+        blocks[i] = bytes(b)
+    buf, off, lens = pack(blocks)
+    bf = np.array(fmts, np.uint8)
+    for flags in (0, N.PBL_ROW_VALUE_PREFIX):
+        plain = oracle.decode_batch(buf, off, lens, 0, bf, flags)
+        fused = oracle.decode_batch(buf, off, lens, 0, bf, flags | HIDE)
+        tf = oracle.transform_batch(plain, 0, True, src=(buf, off, lens, 0, bf, flags))
+        assert list(fused["blk_status"]) == list(tf["blk_status"])
+        hidden = 0
+        for b in range(len(blocks)):
+            if fused["blk_status"][b] == 0:
+                assert per_block(fused, b) == per_block(tf, b), (flags, b)
+                hidden += len(per_block(plain, b)) - len(per_block(fused, b))
+        assert hidden > 0
+    # a colblk-only batch as well (the single-format colblk path's contract)
+    cb = [blk for blk, f in zip(blocks, fmts) if f == SCHEMA_CRDB1]
+    buf, off, lens = pack(cb)
+    plain = oracle.decode_batch(buf, off, lens, SCHEMA_CRDB1, None, 0)
+    fused = oracle.decode_batch(buf, off, lens, SCHEMA_CRDB1, None, HIDE)
+    tf = oracle.transform_batch(plain, 0, True)
+    for k in KEYS + ("blk_kv_base", "blk_key_base", "blk_val_base", "blk_status"):
+        assert np.array_equal(fused[k], tf[k]), k

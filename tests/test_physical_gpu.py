@@ -347,7 +347,7 @@ def test_minlz_random_blocks_lds_and_global_paths():
     comp += [snappy(r) for r in raw[:30]]  # the Snappy form under indicator 8
     want = raw + raw[:30]
     buf, off, lens = pack_phys(comp, lambda b: 0, rng, indicator=N.PBL_COMPRESSION_MINLZ)
-    bb, st = decompress(PhysBatch.from_host(buf, off, lens))
+    bb, st = decompress(PhysBatch.from_host(buf, off, lens, flags=N.PBL_PHYS_MINLZ_NATIVE))
     assert list(st) == [0] * len(comp)
     out, bo, bl = bb.blocks.cpu().numpy(), bb.block_off.cpu().numpy(), bb.block_len.cpu().numpy()
     for i, w in enumerate(want):
@@ -376,7 +376,7 @@ def test_minlz_corrupt_matches_oracle():
         blocks.append(bytes(b))
     blocks += [b"", b"\x00", b"\x00\x00", b"\x00\x00abc", b"\x00\x01\x08ab"]
     buf, off, lens = pack_phys(blocks, lambda b: 0, rng, indicator=N.PBL_COMPRESSION_MINLZ)
-    bb, st = decompress(PhysBatch.from_host(buf, off, lens))
+    bb, st = decompress(PhysBatch.from_host(buf, off, lens, flags=N.PBL_PHYS_MINLZ_NATIVE))
     out, bo, bl = bb.blocks.cpu().numpy(), bb.block_off.cpu().numpy(), bb.block_len.cpu().numpy()
     for i, b in enumerate(blocks):
         want = oracle.minlz_decode(b)
@@ -396,8 +396,17 @@ def test_minlz_mixed_with_other_codecs():
         inds.append(7 if k == 0 else 1 if k == 1 else 8 if k == 2 else 0)
     it = iter(inds)
     buf, off, lens = pack_phys(blocks, lambda b: 0, rng, indicator=lambda b: next(it))
-    bb, st = decompress(PhysBatch.from_host(buf, off, lens))
+    bb, st = decompress(PhysBatch.from_host(buf, off, lens, flags=N.PBL_PHYS_MINLZ_NATIVE))
     assert list(st) == [0] * len(blocks)
+    # without the opt-in flag the MinLZ-form blocks are left to the host
+    # (PBL_UNSUPPORTED); every other block decodes the same
+    bb0, st0 = decompress(PhysBatch.from_host(buf, off, lens))
+    out0, bo0, bl0 = bb0.blocks.cpu().numpy(), bb0.block_off.cpu().numpy(), bb0.block_len.cpu().numpy()
+    for i, want in enumerate(raw):
+        if inds[i] == 8:
+            assert st0[i] == N.PBL_UNSUPPORTED, i
+        else:
+            assert st0[i] == 0 and bytes(out0[bo0[i]: bo0[i] + bl0[i]]) == want, i
     out, bo, bl = bb.blocks.cpu().numpy(), bb.block_off.cpu().numpy(), bb.block_len.cpu().numpy()
     for i, want in enumerate(raw):
         assert bytes(out[bo[i]: bo[i] + bl[i]]) == want, i
