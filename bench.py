@@ -65,7 +65,8 @@ def parse():
     p.add_argument("--no-e2e", action="store_true", help="skip the host->device->host (PCIe-inclusive) pass")
     p.add_argument("--e2e-chunk", type=int, default=2048, help="blocks per PCIe pipeline chunk")
     p.add_argument("--kernel", choices=["auto", "single", "pipe", "pool", "res"], default="auto",
-                   help="A/B: PBL_KERNEL_SINGLE / PBL_KERNEL_PIPE batch flags (auto = pool for row batches)")
+                   help="A/B: row batches pool / res (PBL_KERNEL_RES); colblk batches single / pipe "
+                        "(PBL_KERNEL_SINGLE / PBL_KERNEL_PIPE)")
     p.add_argument("--launch-check", action="store_true",
                    help="launcher self-test without a GPU: N gloo ranks report in, rank 0 prints one JSON line")
     p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
@@ -247,7 +248,7 @@ def main():
     nb = a.blocks or (131072 if a.workload == "mixed" else 65536)
     flags = N.PBL_ROW_VALUE_PREFIX if a.value_prefix else 0
     flags |= {"auto": 0, "single": N.PBL_KERNEL_SINGLE, "pipe": N.PBL_KERNEL_PIPE, "pool": N.PBL_KERNEL_POOL, "res": N.PBL_KERNEL_RES}[a.kernel]
-    row_kernel = {"single": "rowblk_decode_kernel", "pipe": "rowblk_pipe_kernel", "res": "rowblk_res_kernel"}.get(a.kernel, "rowblk_pool_kernel")
+    row_kernel = {"res": "rowblk_res_kernel"}.get(a.kernel, "rowblk_pool_kernel")
     seed = a.seed + 7919 * rank
     t0 = time.time()
     block_fmt = None
@@ -309,8 +310,7 @@ def main():
         n_kv = rn + cn
         # (the sequential mixed path: split + colblk size pass + the row
         # staging-pool kernel over the row ids + colblk pipeline, timed together)
-        kernel = ("mixed_decode_kernel" if a.kernel == "single" else
-                  "mixed_col_size_kernel+rowblk_pool_kernel+mixed_col_kernel")
+        kernel = "mixed_col_size_kernel+rowblk_pool_kernel+mixed_col_kernel"
         wl = (f"config4 shard: {nb} x {a.block_size // 1024} KiB blocks per GPU, even ids row-format "
               f"(config-2 shape), odd ids colblk crdb1 (config-3 shape)")
     gen_s = time.time() - t0

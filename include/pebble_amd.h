@@ -97,13 +97,12 @@ enum {
                                      kernel picks a path per block.  The caller knows
                                      the lengths on the host (block handles carry
                                      them).                                        */
-#define PBL_KERNEL_SINGLE 0x200u  /* A/B measurement, no effect on results: the
-                                     one-block-per-workgroup kernels instead of the
-                                     persistent ones                               */
-#define PBL_KERNEL_PIPE 0x400u    /* A/B measurement, no effect on results: row
-                                     batches on the two-stage pipeline
-                                     (rowblk_pipe.hip.h), colblk batches on theirs
-                                     even with PBL_BATCH_VARLEN                    */
+#define PBL_KERNEL_SINGLE 0x200u  /* A/B measurement, no effect on results: colblk
+                                     batches on the one-block-per-workgroup kernel
+                                     (row batches ignore it)                       */
+#define PBL_KERNEL_PIPE 0x400u    /* A/B measurement, no effect on results: colblk
+                                     batches on the pipeline even with
+                                     PBL_BATCH_VARLEN (row batches ignore it)      */
 /* 0x800u, 0x1000u, 0x2000u: retired A/B kernels (one-wave-per-block flat, run-
    major, HBM-walking row kernels; removed, the bits are ignored)               */
 #define PBL_KERNEL_RES 0x8000u    /* A/B measurement, no effect on results: row

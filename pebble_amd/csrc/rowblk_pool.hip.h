@@ -239,7 +239,7 @@ __device__ __forceinline__ void count_span(const View& V, uint32_t pos, uint32_t
                                            bool& bad, bool& vbad) {
   while (pos < e0) {
     uint32_t sh, un, vl, h;
-    const bool hok = pipe::hdr2(V.ld8(pos), &sh, &un, &vl, &h);
+    const bool hok = rowc::hdr2(V.ld8(pos), &sh, &un, &vl, &h);
     const uint32_t np = pos + h + un + vl;  // < 2^23: no overflow
     if (!hok || (k == 0 && sh != 0) || np > e0) { ok = false; return; }
     bad = bad || (k > 0 && sh > prev_kl);
@@ -290,7 +290,7 @@ __device__ __forceinline__ void run_walk(const View& V, uint32_t r, uint32_t nre
   for (int k = 0; k < kRunBuf; k++) {
     if (go && pos < e0) {
       uint32_t sh, un, vl, h;
-      const bool hok = pipe::hdr2(V.ld8(pos), &sh, &un, &vl, &h);
+      const bool hok = rowc::hdr2(V.ld8(pos), &sh, &un, &vl, &h);
       const uint32_t np = pos + h + un + vl;
       bool hidden = false, setv = false;
       if (!hok || (k == 0 && sh != 0) || np > e0) {
@@ -399,7 +399,7 @@ __device__ __forceinline__ void span_meta(Slot<kHide>& W, const View& V, uint32_
                                           bool vprefix, MState& M) {
   while (pos < e0) {
     uint32_t sh, un, vl, h;
-    pipe::hdr2(V.ld8(pos), &sh, &un, &vl, &h);
+    rowc::hdr2(V.ld8(pos), &sh, &un, &vl, &h);
     const uint32_t kl = sh + un;
     bool hidden, setv;
     entry_class<kHide>(V, pos, h, sh, kl, k, prev_kl, prev_kind, flags, vprefix, hidden, setv);
@@ -838,7 +838,7 @@ __device__ __forceinline__ Pend block_front(PoolLds<kHide>& L, uint32_t s, uint3
   PSTAMP(A, b, 2, l == 0);
   const View V = lds_view(S.x, uint32_t(kPad + (boff & 15)));
   uint32_t roff, nres;
-  uint32_t status = pipe::init_checks(LdsRd{V}, blen, flags, &roff, &nres);
+  uint32_t status = rowc::init_checks(LdsRd{V}, blen, flags, &roff, &nres);
   bool slow = status == PBL_OK && nres > kKv;
   uint32_t nkv = 0, tkb = 0, tvb = 0;
   bool published = false;

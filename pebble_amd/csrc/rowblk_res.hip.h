@@ -245,7 +245,7 @@ __device__ __forceinline__ void block_res(Stage& S, Slot<kHide>& W, const Desc& 
   }
   const View V = lds_view(S.x, uint32_t(kPad + (boff & 15)));
   uint32_t roff, nres;
-  uint32_t status = pipe::init_checks(LdsRd{V}, blen, flags, &roff, &nres);
+  uint32_t status = rowc::init_checks(LdsRd{V}, blen, flags, &roff, &nres);
   bool slow = status == PBL_OK && nres > kKv;
   uint32_t nkv = 0, tkb = 0, tvb = 0;
   bool published = false;

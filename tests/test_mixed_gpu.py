@@ -1,8 +1,7 @@
-"""Mixed row + colblk batches (config 4, block_format[]): the pipelined mixed
-kernel (format split into two ascending id lists, row and colblk pipeline
-bodies in one persistent launch, one look-back over the batch order) and the
-one-block-per-workgroup kernel (PBL_KERNEL_SINGLE) against the oracle,
-bit-exact on every output array."""
+"""Mixed row + colblk batches (config 4, block_format[]): the format split into
+two ascending id lists, the colblk sizes, the row kernel over the row ids and
+the colblk pipeline over the colblk ids, one look-back over the batch order,
+against the oracle, bit-exact on every output array."""
 import random
 
 import numpy as np
@@ -16,7 +15,7 @@ from pebble_amd.rowblk import gen_row_blocks
 from test_rowblk_gpu import assert_same, pack
 
 pytestmark = pytest.mark.gpu
-KERNELS = {"pipe": 0, "single": N.PBL_KERNEL_SINGLE}
+KERNELS = {"default": 0}
 
 
 def gpu(buf, off, lens, bf, flags=0, cap=None, exact=False):
@@ -99,5 +98,5 @@ def test_mixed_overflow_retry_and_size_pass():
     rows, cols = pool(8, 20, 20)
     blocks = [x for p in zip(rows, cols) for x in p]
     fmts = [N.PBL_FMT_ROW, N.PBL_FMT_COL_CRDB1] * 20
-    check(blocks, fmts, "pipe", 8, "overflow", cap=Capacity(kv=10, key=10, val=10, rst=10))
-    check(blocks, fmts, "pipe", 8, "exact", exact=True)
+    check(blocks, fmts, "default", 8, "overflow", cap=Capacity(kv=10, key=10, val=10, rst=10))
+    check(blocks, fmts, "default", 8, "exact", exact=True)
