@@ -40,6 +40,15 @@ METRIC = "raw-block GiB/s decoded to KV arrays (device-resident), 1/2/4/8 MI355X
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
+
+def lib_sha16() -> str:
+    """sha256[:16] of the decoder library this process loads (PBL_LIB or the
+    in-tree build): a traffic file counts only for the build it measured."""
+    import hashlib
+    from pebble_amd import _native as N
+    with open(N.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -54,6 +63,9 @@ def parse():
     p.add_argument("--key-len", type=int, default=16)
     p.add_argument("--val-len", type=int, default=100)
     p.add_argument("--value-prefix", action="store_true")
+    p.add_argument("--hide", type=int, default=0,
+                   help="HideObsoletePoints fused (PBL_ROW_HIDE_OBSOLETE) on row / col batches whose every N-th "
+                        "KV per block is an obsolete point (0: off)"),
     p.add_argument("--zipf-format", choices=["row", "col"], default="row",
                    help="config 5 block format (col = colblk DefaultKeySchema)")
     p.add_argument("--seed", type=int, default=42)
@@ -64,8 +76,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the host->device->host (PCIe-inclusive) pass")
     p.add_argument("--e2e-chunk", type=int, default=2048, help="blocks per PCIe pipeline chunk")
-    p.add_argument("--kernel", choices=["auto", "single", "pipe", "pool", "res"], default="auto",
-                   help="A/B: row batches pool / res (PBL_KERNEL_RES); colblk batches single / pipe "
+    p.add_argument("--kernel", choices=["auto", "single", "pipe", "pool"], default="auto",
+                   help="A/B: colblk batches single / pipe "
                         "(PBL_KERNEL_SINGLE / PBL_KERNEL_PIPE)")
     p.add_argument("--launch-check", action="store_true",
                    help="launcher self-test without a GPU: N gloo ranks report in, rank 0 prints one JSON line")
@@ -247,21 +259,24 @@ def main():
 
     nb = a.blocks or (131072 if a.workload == "mixed" else 65536)
     flags = N.PBL_ROW_VALUE_PREFIX if a.value_prefix else 0
-    flags |= {"auto": 0, "single": N.PBL_KERNEL_SINGLE, "pipe": N.PBL_KERNEL_PIPE, "pool": N.PBL_KERNEL_POOL, "res": N.PBL_KERNEL_RES}[a.kernel]
-    row_kernel = {"res": "rowblk_res_kernel"}.get(a.kernel, "rowblk_pool_kernel")
+    if a.hide:
+        flags |= N.PBL_ROW_HIDE_OBSOLETE
+    flags |= {"auto": 0, "single": N.PBL_KERNEL_SINGLE, "pipe": N.PBL_KERNEL_PIPE, "pool": N.PBL_KERNEL_POOL}[a.kernel]
+    row_kernel = "rowblk_pool_kernel"
     seed = a.seed + 7919 * rank
     t0 = time.time()
     block_fmt = None
     if a.workload in ("row", "transform"):
         fmt = N.PBL_FMT_ROW
         buf, off, lens, n_kv = gen_row_blocks(seed, nb, a.block_size, a.restart_interval, a.key_len, a.val_len,
-                                              a.value_prefix, n_threads=16)
+                                              a.value_prefix, n_threads=16, obsolete_every=a.hide)
         kernel = row_kernel
         if a.workload == "transform":
             kernel = "tf_count_kernel+tf_scan_kernel+tf_scatter_kernel"
         wl = ("transform pass (SyntheticSeqNum, HideObsoletePoints, 12 B SyntheticPrefix) over " if a.workload ==
               "transform" else "") + (f"config2: {nb} x {a.block_size // 1024} KiB row-format blocks per GPU, restart interval "
-              f"{a.restart_interval}, {a.key_len} B keys / {a.val_len} B values" + (", value prefix" if a.value_prefix else ""))
+              f"{a.restart_interval}, {a.key_len} B keys / {a.val_len} B values" + (", value prefix" if a.value_prefix else "")
+              + (f", every {a.hide}th KV obsolete, HideObsoletePoints fused" if a.hide else ""))
     elif a.workload == "rowmix":
         from pebble_amd.batch import gen_row_mix
         fmt = N.PBL_FMT_ROW
@@ -272,10 +287,12 @@ def main():
                "every 8th a short table-tail block (2 / 4 / 8 KiB)"))
     elif a.workload == "col":
         fmt = N.PBL_FMT_COL_CRDB1
-        buf, off, lens, n_kv = gen_col_blocks(seed, nb, a.block_size, n_threads=16)
-        kernel = "colblk_decode_kernel" if a.kernel == "single" else "colblk_pipe_kernel"
+        buf, off, lens, n_kv = gen_col_blocks(seed, nb, a.block_size, n_threads=16, obsolete_every=a.hide)
+        kernel = ("colblk_decode_kernel" if a.kernel == "single" else
+                  "colblk_hide_kernel" if a.hide else "colblk_pipe_kernel")
         wl = (f"config3: {nb} x {a.block_size // 1024} KiB colblk blocks per GPU, cockroachkvs crdb1 schema "
-              f"(KeyGenConfig alphabet 26, RoachKeyLen 12, PrefixLenShared 4, 1 key/prefix), 128 B values")
+              f"(KeyGenConfig alphabet 26, RoachKeyLen 12, PrefixLenShared 4, 1 key/prefix), 128 B values"
+              + (f", every {a.hide}th row isObsolete, HideObsoletePoints fused" if a.hide else ""))
     elif a.workload == "zipf":
         from pebble_amd.batch import gen_zipf_blocks
         fmt = N.PBL_FMT_ROW if a.zipf_format == "row" else N.PBL_FMT_COL_DEFAULT
@@ -320,6 +337,9 @@ def main():
     # size the outputs exactly with one decode, then reuse them every step
     first = decode(batch)
     h = first.to_host()
+    if a.hide:  # the visible KVs only: fewer than were written
+        assert 0 < h["n_kv"] < n_kv and h["status_mask"] == 0, (h["n_kv"], n_kv, h["status_mask"])
+        n_kv = h["n_kv"]
     assert h["n_kv"] == n_kv and h["status_mask"] == 0, (h["n_kv"], n_kv, h["status_mask"])
     cap = Capacity(kv=h["n_kv"], key=h["key_bytes_total"], val=h["val_bytes_total"], rst=h["n_restarts"])
     stream = torch.cuda.current_stream(dev)
@@ -396,10 +416,10 @@ def main():
         ab = alg_bytes(h_in, nb, 0) + alg_bytes(hres, nb, 0) - 24 * nb
     achieved = ab / (kern_ms * 1e-3) / 1e9
     traffic = None
-    tname = ("pmc_traffic.json" if a.workload == "row" and a.kernel == "auto" else
-             f"pmc_traffic_{a.kernel}.json" if a.workload == "row" else
-             f"pmc_traffic_zipf_ri{a.restart_interval}.json" if a.workload == "zipf" and a.zipf_format == "row" else
-             f"pmc_traffic_{a.workload}.json")
+    tname = ("pmc_traffic" if a.workload == "row" and a.kernel == "auto" else
+             f"pmc_traffic_{a.kernel}" if a.workload == "row" else
+             f"pmc_traffic_zipf_ri{a.restart_interval}" if a.workload == "zipf" and a.zipf_format == "row" else
+             f"pmc_traffic_{a.workload}") + (f"_hide{a.hide}" if a.hide else "") + ".json"
     tp = os.path.join(ROOT, "profiles", tname)
     if os.path.exists(tp):
         try:
@@ -408,8 +428,11 @@ def main():
             same_zipf = a.workload != "zipf" or (pt.get("restart_interval") == a.restart_interval
                                                   and pt.get("zipf_format") == a.zipf_format)
             # the PMC of THIS decode's kernels only (a file names the kernel(s) it measured)
+            # ... and of THIS build of the library (the file records the sha256 of
+            # the .so it was measured on)
             if (pt.get("workload_blocks") == nb and pt.get("block_size") == a.block_size
-                    and pt.get("workload", "row") == a.workload and same_zipf and pt.get("kernel") == kernel):
+                    and pt.get("workload", "row") == a.workload and same_zipf and pt.get("kernel") == kernel
+                    and pt.get("lib_sha16") == lib_sha16()):
                 traffic = pt.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -425,6 +448,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "alg_bytes_per_launch": ab, "kernel_ms": round(kern_ms, 4),
+                     "lib_sha16": lib_sha16(), "traffic_source": f"profiles/{tname}" if traffic else None,
                      "input_GiB_per_s_kernel": round(input_bytes / (kern_ms * 1e-3) / 2**30, 1)},
     }
 

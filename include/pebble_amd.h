@@ -103,11 +103,9 @@ enum {
 #define PBL_KERNEL_PIPE 0x400u    /* A/B measurement, no effect on results: colblk
                                      batches on the pipeline even with
                                      PBL_BATCH_VARLEN (row batches ignore it)      */
-/* 0x800u, 0x1000u, 0x2000u: retired A/B kernels (one-wave-per-block flat, run-
-   major, HBM-walking row kernels; removed, the bits are ignored)               */
-#define PBL_KERNEL_RES 0x8000u    /* A/B measurement, no effect on results: row
-                                     batches on the block-resident kernel
-                                     (rowblk_res.hip.h)                            */
+/* 0x800u, 0x1000u, 0x2000u, 0x8000u: retired A/B kernels (one-wave-per-block
+   flat, run-major, HBM-walking and block-resident row kernels; removed, the
+   bits are ignored)                                                            */
 #define PBL_KERNEL_POOL 0x4000u   /* row batches on the staging-pool kernel
                                      (rowblk_pool.hip.h): the default; the bit is
                                      accepted for older callers                    */
@@ -512,6 +510,13 @@ uint64_t pbl_gen_row_blocks(uint64_t seed, uint32_t n_blocks, uint32_t block_siz
                             int restart_interval, uint32_t key_len, uint32_t val_len,
                             int value_prefix, uint8_t* dst, uint64_t* block_off,
                             uint32_t* block_len, int n_threads);
+/* The same with obsolete points (HideObsoletePoints measurements): key k of a
+ * block carries the trailer's obsolete bit when obsolete_every > 0 and
+ * k % obsolete_every == obsolete_every - 1 (rowblk_writer.go:30-42).        */
+uint64_t pbl_gen_row_blocks_obs(uint64_t seed, uint32_t n_blocks, uint32_t block_size,
+                                int restart_interval, uint32_t key_len, uint32_t val_len,
+                                int value_prefix, uint32_t obsolete_every, uint8_t* dst,
+                                uint64_t* block_off, uint32_t* block_len, int n_threads);
 
 /* ---- colblk.DataBlockEncoder (format producer; host memory) ------------------ */
 /*
@@ -549,6 +554,10 @@ typedef struct pbl_colgen_config {
   uint64_t base_wall_time;     /* BaseWallTime                             */
   uint32_t pct_logical;        /* PercentLogical                           */
   uint32_t value_len;
+  uint32_t obsolete_every;     /* 0, or: row k of a block has isObsolete set
+                                  when k % obsolete_every == obsolete_every-1
+                                  (HideObsoletePoints measurements)         */
+  uint32_t reserved;
 } pbl_colgen_config;
 
 /*

@@ -56,7 +56,6 @@ PBL_ROW_HIDE_OBSOLETE = 0x8
 PBL_KERNEL_SINGLE = 0x200
 PBL_KERNEL_PIPE = 0x400
 PBL_KERNEL_POOL = 0x4000
-PBL_KERNEL_RES = 0x8000
 PBL_PHYS_MINLZ_NATIVE = 0x1
 
 PBL_KV_RESTART = 0x01
@@ -86,6 +85,7 @@ class ColGenConfigC(ctypes.Structure):
         ("prefix_len_shared", ctypes.c_uint32), ("roach_key_len", ctypes.c_uint32),
         ("avg_keys_per_prefix", ctypes.c_uint32), ("base_wall_time", ctypes.c_uint64),
         ("pct_logical", ctypes.c_uint32), ("value_len", ctypes.c_uint32),
+        ("obsolete_every", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
     ]
 
 
@@ -231,6 +231,9 @@ SIGNATURES = {
     "pbl_gen_row_blocks": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                              ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                              _vp, _vp, _vp, ctypes.c_int]),
+    "pbl_gen_row_blocks_obs": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                                 ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                                 ctypes.c_uint32, _vp, _vp, _vp, ctypes.c_int]),
     "pbl_colblk_writer_new": (_vp, [ctypes.c_uint32, ctypes.c_int]),
     "pbl_colblk_writer_free": (None, [_vp]),
     "pbl_colblk_writer_reset": (None, [_vp]),

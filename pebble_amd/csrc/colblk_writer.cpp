@@ -675,7 +675,7 @@ extern "C" uint64_t pbl_gen_col_blocks(const pbl_colgen_config* cfgp, uint32_t s
       for (; k < keys.size(); k++) {
         for (auto& x : val) x = uint8_t(sm64(s));
         uint64_t seq = (uint64_t(b) << 20) + k;
-        bool obs = prev && *prev == keys[k];
+        bool obs = (prev && *prev == keys[k]) || (cfg.obsolete_every && k % cfg.obsolete_every == cfg.obsolete_every - 1);
         pbl_colblk_writer_add(&w, reinterpret_cast<const uint8_t*>(keys[k].data()), keys[k].size(), -1,
                               (seq << 8) | 1, val.data(), val.size(), 0, obs);
         prev = &keys[k];

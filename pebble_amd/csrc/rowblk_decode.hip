@@ -4,7 +4,6 @@
 //
 // Kernels:
 //   rowblk_pool_kernel   (rowblk_pool.hip.h) the staging-pool kernel
-//   rowblk_res_kernel    (rowblk_res.hip.h) the block-resident kernel
 //   big_block_*_kernel   (rowblk_big.hip.h) blocks past the 32 KiB LDS stage
 //   mixed_*              row + colblk batches (config 4): the ids split by
 //                        format, the colblk sizes, the row kernel over the row
@@ -151,7 +150,6 @@ struct GlbRd {  // unstaged block in global memory
 
 #include "rowblk_big.hip.h"
 #include "rowblk_pool.hip.h"
-#include "rowblk_res.hip.h"
 
 }  // namespace row
 }  // namespace pbl
@@ -431,30 +429,6 @@ int launch_row_pool(const pbl::Args& a, hipStream_t st, bool values) {
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }
 
-// Row batches on the block-resident kernel (rowblk_res.hip.h), with the same
-// big-block passes around it.
-int launch_row_res(const pbl::Args& a, hipStream_t st, bool values) {
-  const uint32_t nb = a.in.n_blocks;
-  const bool hide = (a.in.flags & PBL_ROW_HIDE_OBSOLETE) && !(a.in.flags & PBL_ROW_RAW_KEYS);
-  const void* fn = hide ? reinterpret_cast<const void*>(pbl::row::res::rowblk_res_kernel<true>)
-                        : reinterpret_cast<const void*>(pbl::row::res::rowblk_res_kernel<false>);
-  int cus = 0;
-  const uint64_t grid = pbl::persistent_grid(st, pbl::kKRowRes, fn,
-                                             (uint64_t(nb) + pbl::row::res::kNW - 1) / pbl::row::res::kNW, &cus,
-                                             pbl::row::res::kTPBR);
-  if (!grid) return PBL_DEVICE_ERROR;
-  const uint32_t small = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4));
-  hipLaunchKernelGGL(pbl::row::rowc::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
-  if (hide)
-    hipLaunchKernelGGL(pbl::row::res::rowblk_res_kernel<true>, dim3(uint32_t(grid)), dim3(pbl::row::res::kTPBR), 0,
-                       st, a, static_cast<const uint32_t*>(nullptr));
-  else
-    hipLaunchKernelGGL(pbl::row::res::rowblk_res_kernel<false>, dim3(uint32_t(grid)), dim3(pbl::row::res::kTPBR), 0,
-                       st, a, static_cast<const uint32_t*>(nullptr));
-  if (values) hipLaunchKernelGGL(pbl::row::rowc::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
-  return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
-}
-
 // Mixed batches: the ids split by format, the colblk sizes, the row kernel
 // over the row ids (with the big row blocks' size / value passes around it),
 // then the colblk blocks.
@@ -506,11 +480,8 @@ int launch_mixed(const pbl_block_batch* batch, const pbl::Args& a, hipStream_t s
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }
 
-// A single-format row batch: the block-resident kernel with PBL_KERNEL_RES,
-// else the staging-pool kernel.
-int launch_row(const pbl::Args& a, hipStream_t st, bool values) {
-  return (a.in.flags & PBL_KERNEL_RES) ? launch_row_res(a, st, values) : launch_row_pool(a, st, values);
-}
+// A single-format row batch: the staging-pool kernel.
+int launch_row(const pbl::Args& a, hipStream_t st, bool values) { return launch_row_pool(a, st, values); }
 }  // namespace
 
 extern "C" {

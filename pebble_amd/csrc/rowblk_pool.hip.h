@@ -22,11 +22,15 @@
 //             written from the registers into the slot; the stage is released
 //   -- the wave stages, walks and publishes its NEXT block here --
 //   resolve   the exclusive prefix (one round trip: every predecessor has long
-//             published), issued together with the first key batch's, the
-//             first value step's and the restart words' loads
-//   keys      lane per KV: offsets (a wave scan of the key lengths), trailer,
-//             flags, entry offset, the user key merged from its prefix chain
-//   values    8 lanes per KV, 16-B chunks, software-pipelined steps
+//             published), issued together with the first step's and the
+//             restart words' loads
+//   steps     64 KVs per step, keys and values together (a line of the block
+//             is fetched once for both), each step's loads issued before the
+//             previous step's stores:
+//               keys    lane per KV: offsets (a wave scan of the key lengths),
+//                       trailer, flags, entry offset, the user key merged from
+//                       its prefix chain
+//               values  8 lanes per KV, 16-B chunks
 //
 // LDS per CU: 3 stages x 32.8 KB + 16 slots x ~4 KB (8 waves x 2 blocks).
 //
@@ -482,7 +486,7 @@ __device__ __forceinline__ uint4 key_chunk(const uint64_t* M0, const Src& V, uin
 // key_chunk).  Only the loaded data and the words they were addressed by are
 // held between the loads and the stores.
 #ifndef PBL_POOL_KU
-#define PBL_POOL_KU 3
+#define PBL_POOL_KU 1
 #endif
 constexpr int kKU = PBL_POOL_KU;
 struct KBatch {
@@ -589,7 +593,7 @@ __device__ __forceinline__ void key_store(const Slot<kHide>& W, const Src& V, co
 // Values shorter than 16 B go byte by byte; values longer than kWaveVal are
 // copied by the whole wave, four 16-B chunks per lane in flight.
 #ifndef PBL_POOL_VG
-#define PBL_POOL_VG 4
+#define PBL_POOL_VG 8
 #endif
 constexpr int kVG = PBL_POOL_VG;
 constexpr uint32_t kWaveVal = 1024;
@@ -650,20 +654,59 @@ __device__ __forceinline__ void val_store(const uint32_t* vp, uint32_t nkv, uint
 // stores (vmcnt retires loads and stores in issue order, so a load issued
 // after a store would wait for that store's acknowledgement too).  B: step 0,
 // loaded by the caller.
+__device__ __forceinline__ void copy_long_values(const uint32_t* vp, gptr<const uint8_t> g, uint32_t nkv,
+                                                 gptr<uint8_t> vbytes);
+
+// PBL_POOL_VDEPTH 2: two steps in flight (B: step 0, B1: step 1, both loaded
+// by the caller), each step's loads issued two steps ahead of its stores.
+#ifndef PBL_POOL_VDEPTH
+#define PBL_POOL_VDEPTH 1
+#endif
+constexpr int kVDepth = PBL_POOL_VDEPTH;
+// PBL_POOL_UNI: the keys and the values of 64 KVs per step (one key batch, one
+// value step of 8 KVs per 8-lane group)
+#ifndef PBL_POOL_UNI
+#define PBL_POOL_UNI 1
+#endif
+constexpr bool kUni = PBL_POOL_UNI != 0;
+static_assert(!kUni || (kKU == 1 && 8 * kVG == kWave), "unified steps: one 64-KV key batch = one value step");
+static_assert(kVDepth == 1 || kVDepth == 2, "value steps in flight: 1 or 2");
 __device__ __forceinline__ void copy_values_grp(const uint32_t* vp, gptr<const uint8_t> g, uint32_t nkv,
-                                                gptr<uint8_t> vbytes, VBatch& B) {
+                                                gptr<uint8_t> vbytes, VBatch& B, VBatch& B1) {
   const int l = lane_id();
-  for (uint32_t j0 = 0; j0 < nkv; j0 += 8 * kVG) {
-    if (j0 + 8 * kVG < nkv) {
+  constexpr uint32_t S = 8 * kVG;  // KVs per step
+  if (kVDepth == 1) {
+    for (uint32_t j0 = 0; j0 < nkv; j0 += S) {
+      if (j0 + S < nkv) {
+        VBatch N;
+        val_load(vp, g, nkv, j0 + S, N);
+        val_store(vp, nkv, j0, B, g, vbytes);
+        B = N;
+      } else {
+        val_store(vp, nkv, j0, B, g, vbytes);
+      }
+    }
+  } else {
+    for (uint32_t j0 = 0; j0 < nkv; j0 += 2 * S) {
       VBatch N;
-      val_load(vp, g, nkv, j0 + 8 * kVG, N);
+      if (j0 + 2 * S < nkv) val_load(vp, g, nkv, j0 + 2 * S, N);
       val_store(vp, nkv, j0, B, g, vbytes);
+      if (j0 + S >= nkv) break;
+      VBatch N1;
+      if (j0 + 3 * S < nkv) val_load(vp, g, nkv, j0 + 3 * S, N1);
+      val_store(vp, nkv, j0 + S, B1, g, vbytes);
       B = N;
-    } else {
-      val_store(vp, nkv, j0, B, g, vbytes);
+      B1 = N1;
     }
   }
-  // long values: the whole wave, four 16-B chunks per lane in flight
+  copy_long_values(vp, g, nkv, vbytes);
+}
+
+// Values longer than kWaveVal: the whole wave, four 16-B chunks per lane in
+// flight.
+__device__ __forceinline__ void copy_long_values(const uint32_t* vp, gptr<const uint8_t> g, uint32_t nkv,
+                                                 gptr<uint8_t> vbytes) {
+  const int l = lane_id();
   for (uint32_t j0 = 0; j0 < nkv; j0 += kWave) {
     const uint32_t j = j0 + uint32_t(l);
     const uint32_t a = j < nkv ? vp[j] : 0u, z = j < nkv ? vp[j + 1] : 0u;
@@ -935,13 +978,15 @@ __device__ __forceinline__ void block_emit(const Pend& P, const Slot<kHide>& W, 
   // first restart words: all in one round trip
   LbWindows<kLbWin> G;
   if (b > 0) G.issue(LbPtrs(lb_state, nb), int64_t(b) - 1);
-  KBatch K;
-  VBatch VB;
+  KBatch K, K1;
+  VBatch VB, VB1;
   uint32_t rs0 = 0;
   const bool ok0 = P.status == PBL_OK;
   if (ok0) {
     key_load<kHide, GSrc>(W, KS, raw, 0, nkv, K);
     val_load(W.vp, gb, nkv, 0, VB);
+    if (kUni && kVDepth == 2) key_load<kHide, GSrc>(W, KS, raw, kWave, nkv, K1);
+    if (kVDepth == 2) val_load(W.vp, gb, nkv, 8 * kVG, VB1);
     if (O.restarts && uint32_t(l) < nres) rs0 = KS.le32(P.roff + 4 * l);
   }
   const uint64_t agg[kNumComp] = {nkv, P.tkb, P.tvb, nres};
@@ -963,6 +1008,54 @@ __device__ __forceinline__ void block_emit(const Pend& P, const Slot<kHide>& W, 
   const uint64_t kvb = excl[0], kbb = excl[1], vbb = excl[2], rbb = excl[3];
   if (O.restarts && uint32_t(l) < nres) to_glb(O.restarts)[rbb + l] = rs0;
   uint32_t kcar = 0;
+  const gptr<uint8_t> vbytes = to_glb(O.val_bytes) + vbb;
+  if (kUni) {
+    // keys and values of the same 64 KVs in one step: a line of the block is
+    // fetched once for both
+    if (kVDepth == 1) {
+      for (uint32_t j0 = 0; j0 <= nkv; j0 += kWave) {
+        KBatch KN;
+        VBatch VN;
+        const bool more = j0 + kWave <= nkv;
+        if (more) {
+          key_load<kHide, GSrc>(W, KS, raw, j0 + kWave, nkv, KN);
+          val_load(W.vp, gb, nkv, j0 + kWave, VN);
+        }
+        key_store<kHide, GSrc>(W, KS, A, b, j0, nkv, kvb, kbb, K, kcar);
+        val_store(W.vp, nkv, j0, VB, gb, vbytes);
+        K = KN;
+        VB = VN;
+      }
+    } else {
+      for (uint32_t j0 = 0; j0 <= nkv; j0 += 2 * kWave) {
+        KBatch KN, KN1;
+        VBatch VN, VN1;
+        if (j0 + 2 * kWave <= nkv) {
+          key_load<kHide, GSrc>(W, KS, raw, j0 + 2 * kWave, nkv, KN);
+          val_load(W.vp, gb, nkv, j0 + 2 * kWave, VN);
+        }
+        key_store<kHide, GSrc>(W, KS, A, b, j0, nkv, kvb, kbb, K, kcar);
+        val_store(W.vp, nkv, j0, VB, gb, vbytes);
+        if (j0 + kWave > nkv) break;
+        if (j0 + 3 * kWave <= nkv) {
+          key_load<kHide, GSrc>(W, KS, raw, j0 + 3 * kWave, nkv, KN1);
+          val_load(W.vp, gb, nkv, j0 + 3 * kWave, VN1);
+        }
+        key_store<kHide, GSrc>(W, KS, A, b, j0 + kWave, nkv, kvb, kbb, K1, kcar);
+        val_store(W.vp, nkv, j0 + kWave, VB1, gb, vbytes);
+        K = KN;
+        VB = VN;
+        K1 = KN1;
+        VB1 = VN1;
+      }
+    }
+    if (O.restarts)
+      for (uint32_t r = kWave + l; r < nres; r += kWave) to_glb(O.restarts)[rbb + r] = KS.le32(P.roff + 4 * r);
+    copy_long_values(W.vp, gb, nkv, vbytes);
+    PSTAMP(A, b, 6, l == 0);
+    PSTAMP(A, b, 7, l == 0);
+    return;
+  }
   key_store<kHide, GSrc>(W, KS, A, b, 0, nkv, kvb, kbb, K, kcar);
   for (uint32_t j0 = kWave * kKU; j0 <= nkv; j0 += kWave * kKU) {
     KBatch N;
@@ -974,7 +1067,7 @@ __device__ __forceinline__ void block_emit(const Pend& P, const Slot<kHide>& W, 
   PSTAMP(A, b, 6, l == 0);
 
   // ---- values, global -> global --------------------------------------------
-  if (P.tvb) copy_values_grp(W.vp, gb, nkv, to_glb(O.val_bytes) + vbb, VB);
+  if (P.tvb) copy_values_grp(W.vp, gb, nkv, vbytes, VB, VB1);
   PSTAMP(A, b, 7, l == 0);
 }
 

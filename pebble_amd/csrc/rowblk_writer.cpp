@@ -182,7 +182,7 @@ void fill_bytes(uint8_t* p, size_t n, uint64_t s) {
 }
 
 uint64_t gen_one_block(uint64_t seed, uint32_t b, uint32_t block_size, int ri, uint32_t key_len,
-                       uint32_t val_len, bool vprefix, uint8_t* dst, uint32_t* out_len) {
+                       uint32_t val_len, bool vprefix, uint32_t obsolete_every, uint8_t* dst, uint32_t* out_len) {
   pbl_rowblk_writer w;
   w.reset(ri);
   std::vector<uint8_t> ukey(key_len), ikey(key_len + 8), val(val_len);
@@ -203,7 +203,8 @@ uint64_t gen_one_block(uint64_t seed, uint32_t b, uint32_t block_size, int ri, u
     size_t grow = w.next_entry_growth(ikey.data(), key_len + 8, val_len, int64_t(key_len), vprefix);
     if (w.estimated_size() + grow > block_size) break;
     fill_bytes(val.data(), val_len, seed + r * 0x9E3779B97F4A7C15ull);
-    pbl_rowblk_writer_add(&w, ukey.data(), key_len, trailer, 0, val.data(), val_len,
+    const int obs = obsolete_every && (k % obsolete_every) == obsolete_every - 1;
+    pbl_rowblk_writer_add(&w, ukey.data(), key_len, trailer, obs, val.data(), val_len,
                           int64_t(key_len), vprefix ? 1 : 0, 0x00, 0);
   }
   size_t sz = w.finish(dst, block_size);
@@ -214,10 +215,10 @@ uint64_t gen_one_block(uint64_t seed, uint32_t b, uint32_t block_size, int ri, u
 
 }  // namespace
 
-extern "C" uint64_t pbl_gen_row_blocks(uint64_t seed, uint32_t n_blocks, uint32_t block_size,
-                                       int restart_interval, uint32_t key_len, uint32_t val_len,
-                                       int value_prefix, uint8_t* dst, uint64_t* block_off,
-                                       uint32_t* block_len, int n_threads) {
+extern "C" uint64_t pbl_gen_row_blocks_obs(uint64_t seed, uint32_t n_blocks, uint32_t block_size,
+                                           int restart_interval, uint32_t key_len, uint32_t val_len,
+                                           int value_prefix, uint32_t obsolete_every, uint8_t* dst,
+                                           uint64_t* block_off, uint32_t* block_len, int n_threads) {
   if (n_threads <= 0) n_threads = int(std::max(1u, std::thread::hardware_concurrency()));
   n_threads = std::min<int>(n_threads, 64);
   if (key_len < 8) key_len = 8;
@@ -227,7 +228,7 @@ extern "C" uint64_t pbl_gen_row_blocks(uint64_t seed, uint32_t n_blocks, uint32_
     for (uint32_t b = uint32_t(t); b < n_blocks; b += uint32_t(n_threads)) {
       block_off[b] = uint64_t(b) * block_size;
       c += gen_one_block(seed, b, block_size, restart_interval, key_len, val_len,
-                         value_prefix != 0, dst + uint64_t(b) * block_size, &block_len[b]);
+                         value_prefix != 0, obsolete_every, dst + uint64_t(b) * block_size, &block_len[b]);
     }
     counts[size_t(t)] = c;
   };
@@ -238,4 +239,12 @@ extern "C" uint64_t pbl_gen_row_blocks(uint64_t seed, uint32_t n_blocks, uint32_
   uint64_t total = 0;
   for (auto c : counts) total += c;
   return total;
+}
+
+extern "C" uint64_t pbl_gen_row_blocks(uint64_t seed, uint32_t n_blocks, uint32_t block_size,
+                                       int restart_interval, uint32_t key_len, uint32_t val_len,
+                                       int value_prefix, uint8_t* dst, uint64_t* block_off,
+                                       uint32_t* block_len, int n_threads) {
+  return pbl_gen_row_blocks_obs(seed, n_blocks, block_size, restart_interval, key_len, val_len, value_prefix, 0,
+                                dst, block_off, block_len, n_threads);
 }

@@ -5,7 +5,8 @@ are produced by the device itself (a first verify pass reports `computed`,
 which is written into the trailers; the timed passes then verify them all OK).
 Snappy: the same blocks compressed on the host (pyarrow), decompressed on the
 device; also a text-like corpus (~2x for snappy) and zstd (level 3, Pebble's
-uvarint length prefix) on both; every block distinct.  Prints one JSON line.
+uvarint length prefix) and MinLZ (indicator 8, Snappy form) on both; every
+block distinct.  Prints one JSON line.
 Usage: bench_physical.py [n_blocks] [reps] [codecs, e.g. snappy,zstd]"""
 import json
 import os
@@ -99,11 +100,15 @@ def codec_run(raw_blocks, codec, n):
     """Compress the distinct raw blocks (zstd with Pebble's uvarint prefix),
     lay out n physical blocks cycling through them, decompress on the device
     (checked), time pbl_decompress_blocks."""
-    ind = 1 if codec == "snappy" else 7
-    c = pa.Codec(codec) if codec == "snappy" else pa.Codec("zstd", compression_level=3)
+    # minlz: blocks with the MinLZ indicator (8) in the Snappy form, the form
+    # minlz.Decode is pinned for (internal/compression/minlz_test.go:31-36);
+    # the native MinLZ form is opt-in and unpinned (include/pebble_amd.h)
+    ind = {"snappy": 1, "minlz": 8, "zstd": 7}[codec]
+    snappy_like = codec in ("snappy", "minlz")
+    c = pa.Codec("snappy") if snappy_like else pa.Codec("zstd", compression_level=3)
     from concurrent.futures import ThreadPoolExecutor
     with ThreadPoolExecutor(16) as ex:
-        comp = list(ex.map(lambda b: c.compress(b, asbytes=True) if codec == "snappy"
+        comp = list(ex.map(lambda b: c.compress(b, asbytes=True) if snappy_like
                            else uvarint(len(b)) + c.compress(b, asbytes=True), raw_blocks))
     k = len(comp)
     cl = np.array([len(comp[i % k]) for i in range(n)], np.uint32)
@@ -137,7 +142,7 @@ def codec_run(raw_blocks, codec, n):
 
 
 cfg2 = [buf[int(o):int(o) + int(ln)].tobytes() for o, ln in zip(off, lens)]
-codecs = sys.argv[3].split(",") if len(sys.argv) > 3 else ["snappy", "zstd"]
+codecs = sys.argv[3].split(",") if len(sys.argv) > 3 else ["snappy", "minlz", "zstd"]
 words = words_blocks(nb)
 for codec in codecs:
     # config-2 blocks (random values: ratio ~1.0) and text-like blocks (ratio ~2-3), all distinct

@@ -1,6 +1,9 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 D=${PROF_OUT:-gpurun_out/prof}; mkdir -p $D
+# the library the profiled process loads (PBL_LIB or the in-tree build): the
+# summary records its hash, and bench.py quotes a traffic file only for it
+python3 -c "import hashlib,os; p=os.environ.get('PBL_LIB') or 'pebble_amd/libpebble_amd.so'; print(hashlib.sha256(open(p,'rb').read()).hexdigest()[:16])" > $D/lib_sha.txt
 R="rocprofv3 --output-format csv"
 P="python3 scripts/prof_decode.py ${PROF_BLOCKS:-65536} 5 ${PROF_WORKLOAD:-row}"
 timeout -k 10 300 rocprofv3 -L > $D/counters_list.txt 2>&1; \

@@ -13,11 +13,12 @@ from pebble_amd.rowblk import gen_row_blocks  # noqa: E402
 nb = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 workload = sys.argv[3] if len(sys.argv) > 3 else "row"
+hide = int(os.environ.get("PROF_HIDE", "0"))  # bench.py --hide N: every N-th KV obsolete, hidden
 if workload == "col":
     from pebble_amd import _native as N
     from pebble_amd.colblk import gen_col_blocks
-    buf, off, lens, n = gen_col_blocks(42, nb, 32768, n_threads=16)
-    b = BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_COL_CRDB1, 0)
+    buf, off, lens, n = gen_col_blocks(42, nb, 32768, n_threads=16, obsolete_every=hide)
+    b = BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_COL_CRDB1, N.PBL_ROW_HIDE_OBSOLETE if hide else 0)
 elif workload.startswith("zipf"):
     # config 5 (bench.py --workload zipf): "zipf" / "zipf:RI" row format at
     # restart interval RI (default 16), "zipf:col" colblk DefaultKeySchema
@@ -48,8 +49,9 @@ elif workload == "mixed":
     n = rn + cn
     b = BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, 0, block_format=bf)
 else:
-    buf, off, lens, n = gen_row_blocks(42, nb, 32768, 16, 16, 100, n_threads=16)
-    b = BlockBatch.from_host(buf, off, lens, "cuda")
+    from pebble_amd import _native as N
+    buf, off, lens, n = gen_row_blocks(42, nb, 32768, 16, 16, 100, n_threads=16, obsolete_every=hide)
+    b = BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, N.PBL_ROW_HIDE_OBSOLETE if hide else 0)
 b.flags |= int(os.environ.get("PROF_FLAGS", "0"), 0)  # e.g. PBL_KERNEL_PIPE (0x400) for A/B profiles
 if workload == "transform":
     # the config-2 batch decoded once, then transformed `iters` times

@@ -23,6 +23,8 @@ os.makedirs(dst, exist_ok=True)
 KERNEL = sys.argv[2] if len(sys.argv) > 2 else "rowblk_pipe_kernel"
 NB = int(sys.argv[3]) if len(sys.argv) > 3 else 65536
 WORKLOAD = sys.argv[4] if len(sys.argv) > 4 else "row"
+HIDE = int(sys.argv[5]) if len(sys.argv) > 5 else 0  # bench.py --hide N / PROF_HIDE=N
+LIB_SHA = open(os.path.join(src, "lib_sha.txt")).read().strip() if os.path.exists(os.path.join(src, "lib_sha.txt")) else None
 
 shutil.copy(os.path.join(src, "trace", "trace_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
 pmc = collections.defaultdict(list)
@@ -48,19 +50,22 @@ for r in csv.DictReader(open(os.path.join(src, "trace", "trace_kernel_stats.csv"
             stats["avg_ns"] += float(r["AverageNs"])
             stats["min_ns"] += float(r["MinNs"])
             stats["max_ns"] += float(r["MaxNs"])
-out = {"kernel": KERNEL, "workload_blocks": NB, "trace": stats, "pmc_per_dispatch_mean": means}
+out = {"kernel": KERNEL, "workload_blocks": NB, "lib_sha16": LIB_SHA, "hide": HIDE, "trace": stats,
+       "pmc_per_dispatch_mean": means}
 if "FETCH_SIZE" in means and "WRITE_SIZE" in means:
     fetch = means["FETCH_SIZE"] * 2 * 1024
     write = means["WRITE_SIZE"] * 1024
     out["hbm_bytes_per_launch"] = fetch + write
+    base = "pmc_traffic" if WORKLOAD == "row" else f"pmc_traffic_{WORKLOAD.replace(':', '_ri')}"
+    tname = base + (f"_hide{HIDE}" if HIDE else "") + ".json"
     json.dump({"kernel": KERNEL, "workload": WORKLOAD.split(":")[0], "workload_blocks": NB, "block_size": 32768,
+               "lib_sha16": LIB_SHA, "hide": HIDE,
                "fetch_bytes_corrected": fetch, "write_bytes": write,
                **({"restart_interval": int(WORKLOAD.split(":")[1]) if ":" in WORKLOAD else 16, "zipf_format": "row"}
                   if WORKLOAD.startswith("zipf") else {}),
                "hbm_bytes_per_launch": fetch + write,
                "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes; FETCH_SIZE(KiB)x2x1024 "
                          "(gfx950 16-B/lane streaming-read correction), WRITE_SIZE(KiB)x1024",
-               "source": f"profiles/{tag}_pmc.json"}, open(os.path.join(dst, "pmc_traffic.json" if WORKLOAD == "row" else
-                      f"pmc_traffic_{WORKLOAD.replace(':', '_ri')}.json"), "w"), indent=1)
+               "source": f"profiles/{tag}_pmc.json"}, open(os.path.join(dst, tname), "w"), indent=1)
 json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))

@@ -293,12 +293,12 @@ def test_kernel_ab_flags_same_results(fmt):
         (lambda: gen_col_blocks(8, 300))
     buf, off, lens, n = gen()
     a = gpu(buf, off, lens, fmt)
-    # row: the block-resident kernel (the retired SINGLE / PIPE bits are
-    # ignored for row batches); colblk: the one-block-per-workgroup kernel and
-    # the pipeline
+    # row: the retired A/B bits (SINGLE / PIPE and the removed kernels' 0x800,
+    # 0x1000, 0x2000, 0x8000) are ignored; colblk: the one-block-per-workgroup
+    # kernel and the pipeline
     if fmt == N.PBL_FMT_ROW:
-        assert_same(gpu(buf, off, lens, fmt, flags=N.PBL_KERNEL_RES), a, "res")
-        assert_same(gpu(buf, off, lens, fmt, flags=N.PBL_KERNEL_SINGLE | N.PBL_KERNEL_PIPE), a, "retired bits")
+        retired = N.PBL_KERNEL_SINGLE | N.PBL_KERNEL_PIPE | 0x800 | 0x1000 | 0x2000 | 0x8000
+        assert_same(gpu(buf, off, lens, fmt, flags=retired), a, "retired bits")
     else:
         assert_same(gpu(buf, off, lens, fmt, flags=N.PBL_KERNEL_SINGLE), a, "single")
         assert_same(gpu(buf, off, lens, fmt, flags=N.PBL_KERNEL_PIPE), a, "pipe")

@@ -44,7 +44,7 @@ def big_row_blocks(rng):
     return out
 
 
-@pytest.mark.parametrize("kernel", [0, N.PBL_KERNEL_RES])
+@pytest.mark.parametrize("kernel", [0])
 @pytest.mark.parametrize("seq", SEQS)
 def test_row_batches(kernel, seq):
     rng = random.Random(seq % 1000 + kernel)

@@ -1,6 +1,5 @@
-"""The row kernels -- the staging-pool kernel (rowblk_pool.hip.h, batch flag
-PBL_KERNEL_POOL) and the block-resident kernel (rowblk_res.hip.h,
-PBL_KERNEL_RES) -- against the oracle: bit-exact on every
+"""The row kernel -- the staging-pool kernel (rowblk_pool.hip.h, with its
+general walk and the big-block passes) -- against the oracle: bit-exact on every
 output array, over reference blocks, synthetic configs, random and fuzzed
 blocks, value prefixes, blocks past the LDS limits, the general-path fallbacks
 and batches whose block shapes vary."""
@@ -16,7 +15,7 @@ from pebble_amd.rowblk import Writer, gen_row_blocks
 from test_rowblk_gpu import GOLDEN, assert_same, pack, random_block
 
 pytestmark = pytest.mark.gpu
-KERNELS = {"pool": N.PBL_KERNEL_POOL, "res": N.PBL_KERNEL_RES}
+KERNELS = {"pool": N.PBL_KERNEL_POOL}
 
 
 @pytest.fixture(params=sorted(KERNELS))
@@ -89,21 +88,6 @@ def test_blocks_past_the_limit(bs, kern):
     rng = random.Random(bs)
     rng.shuffle(blocks)
     check(*pack(blocks), 0, f"bs={bs}", kern)
-
-
-def test_config2_full_size_sha_pool_vs_res():
-    """The full config-2 batch: the default (pool) and the pipeline agree on
-    every array (each is checked against the oracle at reduced size above and
-    in test_baseline_configs_gpu.py)."""
-    import hashlib
-    from pebble_amd.batch import BlockBatch, decode
-    buf, off, lens, n = gen_row_blocks(42, 65536, 32768, 16, 16, 100, n_threads=16)
-    gp = decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, N.PBL_KERNEL_RES)).to_host()
-    gf = decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, 0)).to_host()
-    for k in ("trailer", "kv_flags", "entry_off", "key_off", "val_off", "key_bytes", "val_bytes", "restarts",
-              "blk_kv_base", "blk_key_base", "blk_val_base", "blk_rst_base", "blk_status"):
-        assert hashlib.sha256(gp[k].tobytes()).digest() == hashlib.sha256(gf[k].tobytes()).digest(), k
-    assert gf["n_kv"] == n and int(gf["n_slow_blocks"]) == 0
 
 
 @pytest.mark.parametrize("mix", ["zipf10", "tail8"])

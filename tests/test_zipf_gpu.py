@@ -24,9 +24,9 @@ def test_zipf_row(ri, vp):
     if not vp:
         assert g["n_kv"] == n and g["status_mask"] == 0
         assert g["n_slow_blocks"] >= int((lens > 32768).sum())
-    # both row kernels must route every block past the 32 KiB stage to the
+    # the row kernel must route every block past the 32 KiB stage to the
     # big-block passes (the count may be larger: blocks on the general walk)
-    for kern in (N.PBL_KERNEL_POOL, N.PBL_KERNEL_RES):
+    for kern in (N.PBL_KERNEL_POOL,):
         g = row_check(buf, off, lens, (N.PBL_ROW_VALUE_PREFIX if vp else 0) | kern, f"zipf row ri={ri} vp={vp} k={kern:#x}")
         if not vp:
             assert g["n_slow_blocks"] >= int((lens > 32768).sum())
