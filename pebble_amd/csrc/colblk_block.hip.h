@@ -569,11 +569,7 @@ __device__ __forceinline__ uint64_t block_sum_u64(uint64_t v, uint64_t* red) {
 // Decode block b (format `schema`); the caller has taken ticket b.
 template <bool F>
 __device__ __forceinline__ void col_rows(Lds& s, const Args& A, uint32_t b, uint32_t schema, const Src& S);
-template <bool F>
-__device__ __forceinline__ void col_rows_hide(Lds& s, const Args& A, uint32_t b, uint32_t schema, const Src& S);
 
-// kHide: HideObsoletePoints fused into the decode (PBL_ROW_HIDE_OBSOLETE).
-template <bool kHide = false>
 __device__ __forceinline__ void col_block(Lds& s, const Args& A, uint32_t b, uint32_t schema) {
   const int t = threadIdx.x;
   const uint64_t boff = A.in.block_off[b];
@@ -595,13 +591,8 @@ __device__ __forceinline__ void col_block(Lds& s, const Args& A, uint32_t b, uin
     }
   }
   __syncthreads();
-  if constexpr (kHide) {
-    if (s.status == PBL_OK && s.d.key_end <= nhead) col_rows_hide<true>(s, A, b, schema, S);
-    else col_rows_hide<false>(s, A, b, schema, S);
-  } else {
-    if (s.status == PBL_OK && s.d.key_end <= nhead) col_rows<true>(s, A, b, schema, S);
-    else col_rows<false>(s, A, b, schema, S);
-  }
+  if (s.status == PBL_OK && s.d.key_end <= nhead) col_rows<true>(s, A, b, schema, S);
+  else col_rows<false>(s, A, b, schema, S);
 }
 
 template <bool F>
@@ -750,12 +741,6 @@ __device__ __forceinline__ void col_rows(Lds& s, const Args& A, uint32_t b, uint
   }
 }
 
-// HideObsoletePoints fused into the decode (data_block.go:1680-1697: a row
-// whose isObsolete bit is set is skipped).  Every row is still checked (a
-// block whose decode fails stays failed); the visible rows are counted,
-// published, then written chunk by chunk at the places a block scan of
-// (visible, key length, value length) gives them: keys straight to global
-// memory, values row by row.
 // Row r's isObsolete bit (data_block.go:519; HideObsoletePoints skips such
 // rows, :1680-1697) and the values column's offset r.
 __device__ __forceinline__ bool row_obsolete(const Src& S, const Desc& d, uint32_t r) {
@@ -763,114 +748,6 @@ __device__ __forceinline__ bool row_obsolete(const Src& S, const Desc& d, uint32
 }
 __device__ __forceinline__ uint32_t row_voff(const Src& S, const Desc& d, uint32_t r) {
   return d.v_off.w ? uint32_t(S.le(d.v_off.at + r * d.v_off.w, d.v_off.w)) : 0u;
-}
-
-template <bool F>
-__device__ __forceinline__ void col_rows_hide(Lds& s, const Args& A, uint32_t b, uint32_t schema, const Src& S) {
-  const int t = threadIdx.x;
-  const pbl_decode_out& O = A.out;
-  const uint32_t nb = A.in.n_blocks;
-  uint8_t* ws = reinterpret_cast<uint8_t*>(O.workspace);
-  uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
-  const Desc& d = s.d;
-  const uint32_t rows = s.status == PBL_OK ? d.rows : 0;
-  const uint32_t nch = (rows + kChunk - 1) / kChunk;
-  const auto obsolete = [&](uint32_t r) { return row_obsolete(S, d, r); };
-  const auto voff = [&](uint32_t r) { return row_voff(S, d, r); };
-
-  // ---- pass 1: every row checked, the visible ones counted ---------------------
-  uint64_t my_n = 0, my_kb = 0, my_vb = 0;
-  bool my_bad = false;
-  for (uint32_t c = 0; c < nch; c++) {
-    const uint32_t r = c * kChunk + t;
-    if (r < rows) {
-      const RowParts p = row_parts<F>(S, d, schema, r);
-      my_bad |= !p.ok || !value_ok(S, d, r);
-      if (!obsolete(r)) {
-        my_n++;
-        my_kb += p.klen;
-        my_vb += voff(r + 1) - voff(r);
-      }
-    }
-  }
-  if (my_bad) s.bad = 1;
-  const uint64_t n_tot = block_sum_u64(my_n, s.red);
-  const uint64_t kb_tot = block_sum_u64(my_kb, s.red);
-  const uint64_t vb_tot = block_sum_u64(my_vb, s.red);  // (syncs; also orders s.bad)
-  if (t == 0 && s.status == PBL_OK) {
-    if (s.bad) s.status = PBL_CORRUPT_BOUNDS;
-    else if (kb_tot > 0xffffffffull || vb_tot > 0xffffffffull) s.status = PBL_UNSUPPORTED;
-  }
-  __syncthreads();
-  const bool ok = s.status == PBL_OK;
-  const uint64_t agg[kNumComp] = {ok ? n_tot : 0ull, ok ? kb_tot : 0ull, ok ? vb_tot : 0ull, 0ull};
-  if (wave_id() == 0) {
-    // publish first (block 0's aggregate IS its inclusive prefix: without the
-    // publish its successors would wait for a prefix nobody stores)
-    uint64_t excl[kNumComp];
-    lookback(lb_state, nb, b, agg, excl, &O.totals->status_mask);
-    if (lane_id() == 0) {
-      uint32_t status = s.status;
-      if (ok && overflows(O, excl, agg)) status = PBL_OVERFLOW;
-      s.status = status;
-#pragma unroll
-      for (int c = 0; c < kNumComp; c++) s.bases[c] = excl[c];
-      if (status != PBL_OK && O.key_off && excl[0] + b < O.kv_cap + nb) {
-        O.key_off[excl[0] + b] = 0;
-        O.val_off[excl[0] + b] = 0;
-      }
-      write_block_meta(O, b, nb, status, excl, agg, !F);
-    }
-  }
-  __syncthreads();
-  if (s.status != PBL_OK) return;
-  const uint64_t kvb = s.bases[0], kbb = s.bases[1], vbb = s.bases[2];
-
-  // ---- pass 2: the visible rows, compacted --------------------------------------
-  uint32_t cn = 0, ck = 0, cv = 0;
-  for (uint32_t c = 0; c < nch; c++) {
-    const uint32_t r = c * kChunk + t;
-    const bool vis = r < rows && !obsolete(r);
-    RowParts p;
-    p.klen = 0;
-    uint32_t v0 = 0, v1 = 0;
-    if (vis) {
-      p = row_parts<F>(S, d, schema, r);
-      v0 = voff(r);
-      v1 = voff(r + 1);
-    }
-    uint32_t en, ek, ev, dz, tn, tk, tv, dt;
-    block_excl_scan2(vis ? 1u : 0u, vis ? p.klen : 0u, &en, &ek, s.scratch, &tn, &tk);
-    __syncthreads();
-    block_excl_scan2(v1 - v0, 0u, &ev, &dz, s.scratch, &tv, &dt);
-    __syncthreads();
-    if (vis) {
-      const uint64_t i = kvb + cn + en;
-      const uint32_t ko = ck + ek, vo_ = cv + ev;
-      O.key_off[i + b] = ko;
-      O.val_off[i + b] = vo_;
-      O.trailer[i] = with_seq(u_at<F>(S, d.trailers, r), A.in.synthetic_seq_num, 0u);
-      if (O.kv_flags) {
-        uint8_t fl = 0;
-        if (d.pc_at && ((S.le(d.pc_at + 8 * (r >> 6), 8) >> (r & 63)) & 1)) fl |= PBL_KV_PREFIX_CHANGED;
-        if (d.ext_at && ((S.le(d.ext_at + 8 * (r >> 6), 8) >> (r & 63)) & 1)) {
-          const bool vb = v1 > v0 && (S.byte(d.v_data + v0) & 0xC0) == 0x80;
-          fl |= vb ? PBL_KV_VALBLK_HANDLE : PBL_KV_BLOB_HANDLE;
-        }
-        O.kv_flags[i] = fl;
-      }
-      if (O.entry_off) O.entry_off[i] = r;
-      build_key_global<F>(S, d, schema, p, O.key_bytes + kbb + ko);
-      for (uint32_t k = v0; k < v1; k++) O.val_bytes[vbb + vo_ + (k - v0)] = uint8_t(S.byte(d.v_data + k));
-    }
-    cn += tn;
-    ck += tk;
-    cv += tv;
-  }
-  if (t == 0) {
-    O.key_off[kvb + b + cn] = ck;
-    O.val_off[kvb + b + cn] = cv;
-  }
 }
 
 }  // namespace col

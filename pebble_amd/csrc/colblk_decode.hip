@@ -21,17 +21,6 @@ colblk_decode_kernel(Args A) {
   col_block(s, A, ticket, A.in.format);
 }
 
-// The same with HideObsoletePoints fused (PBL_ROW_HIDE_OBSOLETE batches).
-__global__ void __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(PBL_COL_SINGLE_WAVES)))
-colblk_hide_kernel(Args A) {
-  __shared__ Lds s;
-  __shared__ uint32_t ticket;
-  uint32_t* ticket_ctr = reinterpret_cast<uint32_t*>(A.out.workspace);
-  if (threadIdx.x == 0) ticket = atomicAdd(ticket_ctr, 1u);
-  __syncthreads();
-  col_block<true>(s, A, ticket, A.in.format);
-}
-
 }  // namespace col
 }  // namespace pbl
 
@@ -50,17 +39,22 @@ extern "C" int pbl_decode_batch_colblk(const pbl_block_batch* batch, pbl_decode_
   // (config 5: 412 vs 245 GiB/s, the pipeline's one-iteration look-back lag
   // convoys behind long blocks).
   const uint32_t f = batch->flags;
-  const bool single = (f & PBL_KERNEL_SINGLE) || ((f & PBL_BATCH_VARLEN) && !(f & PBL_KERNEL_PIPE));
-  if (f & PBL_ROW_HIDE_OBSOLETE) {
-    hipLaunchKernelGGL(pbl::col::colblk_hide_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
-  } else if (single) {
+  // HideObsoletePoints (PBL_ROW_HIDE_OBSOLETE) is fused into the pipeline
+  // (colblk_pipe_kernel<true>) whatever the other flags say.
+  const bool hide = (f & PBL_ROW_HIDE_OBSOLETE) != 0;
+  const bool single = !hide && ((f & PBL_KERNEL_SINGLE) || ((f & PBL_BATCH_VARLEN) && !(f & PBL_KERNEL_PIPE)));
+  if (single) {
     hipLaunchKernelGGL(pbl::col::colblk_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
   } else {
-    const uint64_t grid = pbl::persistent_grid(st, pbl::kKColPipe,
-                                               reinterpret_cast<const void*>(pbl::col::cpipe::colblk_pipe_kernel),
-                                               batch->n_blocks, nullptr);
+    const void* fn = hide ? reinterpret_cast<const void*>(pbl::col::cpipe::colblk_pipe_kernel<true>)
+                          : reinterpret_cast<const void*>(pbl::col::cpipe::colblk_pipe_kernel<false>);
+    const uint64_t grid = pbl::persistent_grid(st, hide ? pbl::kKColPipeHide : pbl::kKColPipe, fn, batch->n_blocks,
+                                               nullptr);
     if (!grid) return PBL_DEVICE_ERROR;
-    hipLaunchKernelGGL(pbl::col::cpipe::colblk_pipe_kernel, dim3(uint32_t(grid)), dim3(pbl::kTPB), 0, st, a);
+    if (hide)
+      hipLaunchKernelGGL(pbl::col::cpipe::colblk_pipe_kernel<true>, dim3(uint32_t(grid)), dim3(pbl::kTPB), 0, st, a);
+    else
+      hipLaunchKernelGGL(pbl::col::cpipe::colblk_pipe_kernel<false>, dim3(uint32_t(grid)), dim3(pbl::kTPB), 0, st, a);
   }
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }

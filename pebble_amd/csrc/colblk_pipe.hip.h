@@ -54,6 +54,9 @@ struct Slot {
 struct CLds {
   Slot s[2];
   uint4 key4[(kKeyBuf + 2 * kKeyPad) / 16];
+  // HideObsoletePoints: a chunk's visible rows, compacted: value source offset
+  // (values column), output offset (from the chunk's value base), length
+  uint32_t rv0[kChunk], rvo[kChunk], rvl[kChunk];
   uint64_t red[4];
   uint64_t bases[kNumComp];
   uint32_t scratch[16];
@@ -157,7 +160,7 @@ __device__ __forceinline__ void col_resolve(CLds& L, const Slot& E, const Args& 
 }
 
 // ---- parse phase (whole workgroup) ------------------------------------------------
-template <bool F>
+template <bool F, bool kHide>
 __device__ __forceinline__ void col_parse_rows(CLds& L, Slot& P, const Args& A, uint32_t schema, const Src& S) {
   const int t = threadIdx.x;
   const uint32_t nb = A.in.n_blocks;
@@ -168,29 +171,41 @@ __device__ __forceinline__ void col_parse_rows(CLds& L, Slot& P, const Args& A, 
   const uint32_t rows = hdr_ok ? d.rows : 0;
   const uint32_t nch = (rows + kChunk - 1) / kChunk;
   uint32_t k0 = 0;
-  uint64_t my_kb = 0;
+  uint64_t my_kb = 0, my_n = 0, my_vb = 0;
   bool my_bad = false;
   for (uint32_t c = 0; c < nch; c++) {
     const uint32_t r = c * kChunk + t;
     if (r < rows) {
       const RowParts p = row_parts<F>(S, d, schema, r);
       my_bad |= !p.ok || !value_ok(S, d, r);
-      my_kb += p.klen;
+      // HideObsoletePoints (data_block.go:1680-1697): the visible rows only
+      if (!kHide || !row_obsolete(S, d, r)) {
+        my_kb += p.klen;
+        if (kHide) {
+          my_n++;
+          my_vb += row_voff(S, d, r + 1) - row_voff(S, d, r);
+        }
+      }
       if (c == 0) k0 = p.klen;
     }
   }
   if (my_bad) L.bad = 1;
   uint32_t excl0, tot0, de, dt;
   block_excl_scan2(k0, 0u, &excl0, &de, L.scratch, &tot0, &dt);
+  uint64_t n_tot = rows, vb_tot = uint64_t(d.v_hi - d.v_lo);
+  if (kHide) {
+    n_tot = block_sum_u64(my_n, L.red);
+    vb_tot = block_sum_u64(my_vb, L.red);
+  }
   const uint64_t kb_tot = block_sum_u64(my_kb, L.red);  // (syncs; also orders L.bad)
   (void)excl0;
   if (t == 0 && P.status == PBL_OK) {
     if (L.bad) P.status = PBL_CORRUPT_BOUNDS;
-    else if (kb_tot > 0xffffffffull || uint64_t(d.v_hi - d.v_lo) > 0xffffffffull) P.status = PBL_UNSUPPORTED;
+    else if (kb_tot > 0xffffffffull || vb_tot > 0xffffffffull) P.status = PBL_UNSUPPORTED;
   }
   __syncthreads();
   const bool ok = P.status == PBL_OK;
-  const uint64_t agg[kNumComp] = {ok ? rows : 0u, ok ? kb_tot : 0ull, ok ? uint64_t(d.v_hi - d.v_lo) : 0ull, 0ull};
+  const uint64_t agg[kNumComp] = {ok ? n_tot : 0ull, ok ? kb_tot : 0ull, ok ? vb_tot : 0ull, 0ull};
   if (wave_id() == 0) lb_publish(lb_state, nb, P.b, agg);
   if (t == 0) {
 #pragma unroll
@@ -200,7 +215,7 @@ __device__ __forceinline__ void col_parse_rows(CLds& L, Slot& P, const Args& A, 
   }
 }
 
-template <bool kSizeOnly = false>
+template <bool kSizeOnly = false, bool kHide = false>
 __device__ __forceinline__ void col_parse(CLds& L, Slot& P, const Slot& E, const Args& A, uint32_t schema) {
   const Src S = slot_src(P, A);
   CSTAMP(A, P.b, 0);
@@ -216,8 +231,8 @@ __device__ __forceinline__ void col_parse(CLds& L, Slot& P, const Slot& E, const
   if (P.b >= A.in.n_blocks) return;
   if (threadIdx.x == 0) P.fast = P.status == PBL_OK && P.d.key_end <= P.nhead;
   CSTAMP(A, P.b, 1);
-  if (P.status == PBL_OK && P.d.key_end <= P.nhead) col_parse_rows<true>(L, P, A, schema, S);
-  else col_parse_rows<false>(L, P, A, schema, S);
+  if (P.status == PBL_OK && P.d.key_end <= P.nhead) col_parse_rows<true, kHide>(L, P, A, schema, S);
+  else col_parse_rows<false, kHide>(L, P, A, schema, S);
   CSTAMP(A, P.b, 2);
 }
 
@@ -366,14 +381,119 @@ __device__ __forceinline__ void col_emit_rows(CLds& L, const Slot& E, const Args
   CSTAMP(A, b, 7);
 }
 
-// Emit (whole workgroup) of block E.b, whose prefix col_resolve left in L.
+// 16 bytes of block E at block offset j (any alignment, [j, j + 16) inside the
+// block): from the staged head or tail when they hold them, else global.
+__device__ __forceinline__ uint4 slot_ld16(const Slot& E, const Args& A, uint32_t j) {
+  if (j + 16 <= E.nhead) return lds_bytes16((lds_cu32)to_lds(E.head4), E.shift + j);
+  if (j >= E.tail_lo && j + 16 <= E.blen) return lds_bytes16((lds_cu32)to_lds(E.tail4), E.shift + j - E.tail_lo);
+  typedef u32x4 u32x4_ua __attribute__((aligned(1)));
+  const u32x4 v = *(gptr<const u32x4_ua>)(to_glb(A.in.blocks) + E.boff + j);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// HideObsoletePoints fused into the pipeline's emit (data_block.go:1680-1697):
+// chunk by chunk, a block scan of (visible, key length) and of the visible
+// value lengths places every visible row; keys are built in LDS and leave as
+// aligned 16-B granules, values are copied row by row (8 threads per row,
+// 16-B chunks, the last one ending at the value's end) from the staged head
+// and tail or from global memory.
 template <bool F>
+__device__ __forceinline__ void col_emit_rows_hide(CLds& L, const Slot& E, const Args& A, uint32_t schema,
+                                                   const Src& S) {
+  const int t = threadIdx.x;
+  const pbl_decode_out& O = A.out;
+  const uint32_t b = E.b;
+  const Desc& d = E.d;
+  const uint32_t rows = d.rows;
+  const uint32_t nch = (rows + kChunk - 1) / kChunk;
+  const uint64_t kvb = L.bases[0], kbb = L.bases[1], vbb = L.bases[2];
+  typedef u32x4 u32x4_ua __attribute__((aligned(1)));
+  lds_u8 kb8 = (lds_u8)to_lds(L.key4);
+  uint32_t cn = 0, ck = 0, cv = 0;
+  for (uint32_t c = 0; c < nch; c++) {
+    const uint32_t r = c * kChunk + t;
+    const bool vis = r < rows && !row_obsolete(S, d, r);
+    RowParts p;
+    p.klen = 0;
+    uint32_t v0 = 0, v1 = 0;
+    if (vis) {
+      p = row_parts<F>(S, d, schema, r);
+      v0 = row_voff(S, d, r);
+      v1 = row_voff(S, d, r + 1);
+    }
+    uint32_t en, ek, ev, dz, tn, tk, tv, dt;
+    block_excl_scan2(vis ? 1u : 0u, vis ? p.klen : 0u, &en, &ek, L.scratch, &tn, &tk);
+    __syncthreads();
+    block_excl_scan2(v1 - v0, 0u, &ev, &dz, L.scratch, &tv, &dt);
+    if (vis) {
+      const uint64_t i = kvb + cn + en;
+      to_glb(O.key_off)[i + b] = ck + ek;
+      to_glb(O.val_off)[i + b] = cv + ev;
+      to_glb(O.trailer)[i] = with_seq(u_at<F>(S, d.trailers, r), A.in.synthetic_seq_num, 0u);
+      if (O.kv_flags) {
+        uint8_t fl = 0;
+        if (d.pc_at && ((S.le(d.pc_at + 8 * (r >> 6), 8) >> (r & 63)) & 1)) fl |= PBL_KV_PREFIX_CHANGED;
+        if (d.ext_at && ((S.le(d.ext_at + 8 * (r >> 6), 8) >> (r & 63)) & 1)) {
+          const bool vb = v1 > v0 && (S.byte(d.v_data + v0) & 0xC0) == 0x80;
+          fl |= vb ? PBL_KV_VALBLK_HANDLE : PBL_KV_BLOB_HANDLE;
+        }
+        to_glb(O.kv_flags)[i] = fl;
+      }
+      if (O.entry_off) to_glb(O.entry_off)[i] = r;
+      L.rv0[en] = d.v_data + v0;
+      L.rvo[en] = ev;
+      L.rvl[en] = v1 - v0;
+    }
+    // keys
+    if (tk <= kKeyBuf) {
+      if (vis) build_key<F>(S, d, schema, p, kb8, kKeyPad + ek);
+      __syncthreads();
+      const uint64_t lo = kbb + ck, hi = lo + tk;
+      const lds_cu32 W = (lds_cu32)to_lds(L.key4);
+      for (uint64_t ga = (lo & ~uint64_t(15)) + 16ull * t; ga < hi; ga += 16ull * kTPB)
+        store16(O.key_bytes, ga, lo, hi, lds_bytes16(W, uint32_t(kKeyPad + ga - lo)));
+    } else {
+      if (vis) build_key_global<F>(S, d, schema, p, O.key_bytes + kbb + ck + ek);
+      __syncthreads();
+    }
+    // values: 8 threads per visible row
+    const gptr<uint8_t> vout = to_glb(O.val_bytes) + vbb + cv;
+    const uint32_t q8 = uint32_t(t) & 7u;
+    for (uint32_t q = uint32_t(t) >> 3; q < tn; q += kTPB / 8) {
+      const uint32_t src = L.rv0[q], o0 = L.rvo[q], len = L.rvl[q];
+      if (len >= 16) {
+        for (uint32_t o = 16 * q8; o < len; o += 128) {
+          const uint32_t qq = o < len - 16 ? o : len - 16;
+          const uint4 w = slot_ld16(E, A, src + qq);
+          __builtin_nontemporal_store(u32x4_ua{w.x, w.y, w.z, w.w}, (gptr<u32x4_ua>)(vout + o0 + qq));
+        }
+      } else {
+        for (uint32_t o = q8; o < len; o += 8) vout[o0 + o] = uint8_t(S.byte(src + o));
+      }
+    }
+    cn += tn;
+    ck += tk;
+    cv += tv;
+    __syncthreads();  // (the key buffer and the row arrays are the next chunk's)
+  }
+  if (t == 0) {
+    to_glb(O.key_off)[kvb + b + cn] = ck;
+    to_glb(O.val_off)[kvb + b + cn] = cv;
+  }
+}
+
+// Emit (whole workgroup) of block E.b, whose prefix col_resolve left in L.
+template <bool F, bool kHide>
 __device__ __forceinline__ void col_emit_t(CLds& L, const Slot& E, const Args& A, uint32_t schema) {
   const uint32_t b = E.b;
   const int t = threadIdx.x;
   const Src S = slot_src(E, A);
   CSTAMP(A, b, 3);
   if (L.st != PBL_OK) return;
+  if (kHide) {
+    col_emit_rows_hide<F>(L, E, A, schema, S);
+    return;
+  }
   // keys of a single-chunk block are built in LDS first (one scan + one barrier)
   const uint32_t rows = E.d.rows;
   const bool prebuilt = rows <= kChunk && E.tot0 <= kKeyBuf;
@@ -391,15 +511,16 @@ __device__ __forceinline__ void col_emit_t(CLds& L, const Slot& E, const Args& A
   col_emit_rows<F>(L, E, A, schema, S, prebuilt, ex, tot);
 }
 
+template <bool kHide>
 __device__ __forceinline__ void col_emit(CLds& L, const Slot& E, const Args& A, uint32_t schema) {
-  if (E.fast) col_emit_t<true>(L, E, A, schema);
-  else col_emit_t<false>(L, E, A, schema);
+  if (E.fast) col_emit_t<true, kHide>(L, E, A, schema);
+  else col_emit_t<false, kHide>(L, E, A, schema);
 }
 
 // ---- the persistent kernel ----------------------------------------------------------
 // kSizeOnly: parse and publish every block's aggregate, no resolve and no
-// outputs (the first pass of a sequential mixed batch, rowblk_decode.hip).
-template <class Q, bool kSizeOnly = false>
+// outputs.  kHide: HideObsoletePoints fused (PBL_ROW_HIDE_OBSOLETE).
+template <class Q, bool kSizeOnly = false, bool kHide = false>
 __device__ __forceinline__ void col_pipe_body(CLds& L, const Args& A, const Q& q) {
   const int t = threadIdx.x;
   const uint32_t nb = A.in.n_blocks;
@@ -434,7 +555,7 @@ __device__ __forceinline__ void col_pipe_body(CLds& L, const Args& A, const Q& q
     // held for one iteration only, which keeps the look-back distance short
     if (t == 0) L.nxt = cb < nb ? q.take() : nb;
     ColPf pf;
-    col_parse<kSizeOnly>(L, P, E, A, P.schema);  // (wave 1 first resolves E's prefix)
+    col_parse<kSizeOnly, kHide>(L, P, E, A, P.schema);  // (wave 1 first resolves E's prefix)
     __syncthreads();
     const uint32_t nx = L.nxt;
     uint64_t nx_off = 0;
@@ -445,7 +566,7 @@ __device__ __forceinline__ void col_pipe_body(CLds& L, const Args& A, const Q& q
     }
     const bool pf_on = nx < nb && (nx_off & 7) == 0;
     if (pf_on) pf.load(A.in.blocks, nx_off, nx_len);  // lands during the emit
-    if (!kSizeOnly && E.mode != kNone) col_emit(L, E, A, E.schema);
+    if (!kSizeOnly && E.mode != kNone) col_emit<kHide>(L, E, A, E.schema);
     __syncthreads();
     if (t == 0) slot_setup(E, nx < nb ? nx : nb, nx_off, nx_len, A);
     if (pf_on) pf.store(E, nx_off, nx_len);
@@ -456,9 +577,11 @@ __device__ __forceinline__ void col_pipe_body(CLds& L, const Args& A, const Q& q
 }
 
 #ifndef PBL_COL_PIPE_BODY_ONLY  // (rowblk_decode.hip uses the body in the mixed pipeline)
+template <bool kHide>
 __global__ void __launch_bounds__(kTPB, PBL_COL_PIPE_WG) colblk_pipe_kernel(Args A) {
   __shared__ CLds L;
-  col_pipe_body(L, A, TicketQueue{reinterpret_cast<uint32_t*>(A.out.workspace), A.in.n_blocks});
+  col_pipe_body<TicketQueue, false, kHide>(L, A, TicketQueue{reinterpret_cast<uint32_t*>(A.out.workspace),
+                                                              A.in.n_blocks});
 }
 #endif
 

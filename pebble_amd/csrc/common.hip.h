@@ -492,7 +492,7 @@ __device__ inline bool overflows(const pbl_decode_out& O, const uint64_t excl[kN
 // kernel's resident workgroups per CU are hardware properties of that device:
 // they are queried once and cached (the library's only process-wide state, and
 // immutable once written; racing first calls store the same values).
-enum PersistentKernel { kKColPipe = 0, kKMixedCol = 1, kKRowPool = 2, kKNum = 3 };
+enum PersistentKernel { kKColPipe = 0, kKMixedCol = 1, kKRowPool = 2, kKColPipeHide = 3, kKMixedColHide = 4, kKNum = 5 };
 
 // Resident grid for `fn` on the stream's device (never more than n_units, at
 // least 1); 0 on a runtime error.

@@ -233,7 +233,7 @@ __global__ void __launch_bounds__(kTPB) mixed_split_scatter_kernel(Args A, const
 // Mixed batches: persistent launches over the split id lists.  (1)
 // mixed_col_size_kernel parses every colblk block and publishes its aggregate;
 // (2) the row kernel runs over the row list, its look-back walking through the
-// colblk aggregates; (3) mixed_col_kernel (or mixed_col_hide_kernel) runs over
+// colblk aggregates; (3) mixed_col_kernel runs over
 // the colblk list (its predecessors' prefixes are all published: its look-back
 // ends at the row block before it).  Deadlock-free: (2) waits only on
 // aggregates published by (1) or by its own resident waves in ticket order,
@@ -300,32 +300,15 @@ mixed_col_size_kernel(Args A, const uint32_t* ids) {
   }
 }
 
+// (3): the colblk pipeline over the colblk list; kHide: HideObsoletePoints
+// fused (the visible rows, as mixed_col_size_kernel<true> counted them).
+template <bool kHide>
 __global__ void __launch_bounds__(kTPB, PBL_COL_PIPE_WG) mixed_col_kernel(Args A, const uint32_t* ids) {
   __shared__ col::cpipe::CLds L;
   const uint32_t nb = A.in.n_blocks;
   uint32_t* hdr = reinterpret_cast<uint32_t*>(A.out.workspace);
   const uint32_t n_row = __hip_atomic_load(to_glb(hdr) + kWsRowCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  col::cpipe::col_pipe_body(L, A, ListQueue{hdr + kWsColTick2, ids + n_row, nb - n_row, nb});
-}
-
-// (3) with HideObsoletePoints fused: the one-block-per-workgroup colblk form
-// (col_rows_hide) over the colblk list, in ticket order; every row block has
-// its inclusive prefix by now.
-__global__ void __launch_bounds__(kTPB) mixed_col_hide_kernel(Args A, const uint32_t* ids) {
-  __shared__ col::Lds s;
-  __shared__ uint32_t tk;
-  const uint32_t nb = A.in.n_blocks;
-  uint32_t* hdr = reinterpret_cast<uint32_t*>(A.out.workspace);
-  const uint32_t n_row = __hip_atomic_load(to_glb(hdr) + kWsRowCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (;;) {
-    if (threadIdx.x == 0) tk = g_atomic_add(hdr + kWsColTick2, 1u);
-    __syncthreads();
-    const uint32_t t = tk;
-    if (t >= nb - n_row) break;
-    const uint32_t b = to_glb(ids)[n_row + t];
-    col::col_block<true>(s, A, b, to_glb(A.in.block_format)[b]);
-    __syncthreads();  // (the LDS and tk are the next block's)
-  }
+  col::cpipe::col_pipe_body<ListQueue, false, kHide>(L, A, ListQueue{hdr + kWsColTick2, ids + n_row, nb - n_row, nb});
 }
 
 // Size pass epilogue: a block that decoded reports PBL_OK, not the forced
@@ -446,8 +429,9 @@ int launch_mixed(const pbl_block_batch* batch, const pbl::Args& a, hipStream_t s
   hipLaunchKernelGGL(pbl::row::mixed_split_scatter_kernel, dim3(nch), dim3(pbl::kTPB), 0, st, a,
                      static_cast<const uint32_t*>(counts), nch, ids);
   int cus = 0;
-  const uint64_t g_c = pbl::persistent_grid(st, pbl::kKMixedCol, reinterpret_cast<const void*>(pbl::row::mixed_col_kernel),
-                                            nb, &cus);
+  const void* cfn = hide ? reinterpret_cast<const void*>(pbl::row::mixed_col_kernel<true>)
+                         : reinterpret_cast<const void*>(pbl::row::mixed_col_kernel<false>);
+  const uint64_t g_c = pbl::persistent_grid(st, hide ? pbl::kKMixedColHide : pbl::kKMixedCol, cfn, nb, &cus);
   if (!g_c) return PBL_DEVICE_ERROR;
   const uint32_t g_cs = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 32));
   const uint32_t small = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4));
@@ -470,11 +454,10 @@ int launch_mixed(const pbl_block_batch* batch, const pbl::Args& a, hipStream_t s
   else
     hipLaunchKernelGGL(pbl::row::pool::rowblk_pool_kernel<false>, dim3(uint32_t(g_p)), dim3(pbl::row::pool::kTPBP), 0,
                        st, a, cids);
-  if (hide)  // (workgroups loop over the colblk list's tickets; 21 KB of LDS each)
-    hipLaunchKernelGGL(pbl::row::mixed_col_hide_kernel, dim3(uint32_t(std::min<uint64_t>(nb, uint64_t(cus) * 7))),
-                       dim3(pbl::kTPB), 0, st, a, cids);
+  if (hide)
+    hipLaunchKernelGGL(pbl::row::mixed_col_kernel<true>, dim3(uint32_t(g_c)), dim3(pbl::kTPB), 0, st, a, cids);
   else
-    hipLaunchKernelGGL(pbl::row::mixed_col_kernel, dim3(uint32_t(g_c)), dim3(pbl::kTPB), 0, st, a, cids);
+    hipLaunchKernelGGL(pbl::row::mixed_col_kernel<false>, dim3(uint32_t(g_c)), dim3(pbl::kTPB), 0, st, a, cids);
   if (values)
     hipLaunchKernelGGL(pbl::row::rowc::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;

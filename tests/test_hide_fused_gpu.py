@@ -146,3 +146,24 @@ def test_mixed_batches(flags):
     t = size_batch(bb).read_totals()
     assert int(t.n_kv) == int(o["n_kv"]) and int(t.key_bytes) == int(o["key_bytes_total"])
     assert int(t.val_bytes) == int(o["val_bytes_total"])
+
+
+@pytest.mark.parametrize("every", [2, 4, 7])
+def test_colblk_config3_obsolete_rows(every):
+    """Config-3 blocks with every `every`-th row isObsolete (bench.py --hide):
+    the pipeline's fused hide against the oracle, also when the batch carries
+    the one-block-per-workgroup hints (the flag routes to the pipeline)."""
+    from pebble_amd.colblk import gen_col_blocks
+    buf, off, lens, n = gen_col_blocks(5 + every, 300, 32768, obsolete_every=every)
+    o = oracle.transform_batch(oracle.decode_batch(buf, off, lens, N.PBL_FMT_COL_CRDB1, None, 0), 0, True)
+    assert o["n_kv"] < n
+    for extra in (0, N.PBL_BATCH_VARLEN, N.PBL_KERNEL_SINGLE):
+        g = decode(BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_COL_CRDB1, HIDE | extra)).to_host()
+        assert_same(g, o, f"config-3 obsolete every {every} extra={extra:#x}")
+
+
+@pytest.mark.parametrize("every", [2, 4])
+def test_row_config2_obsolete_points(every):
+    buf, off, lens, n = gen_row_blocks(9 + every, 400, 32768, 16, 16, 100, obsolete_every=every)
+    g = check(buf, off, lens, 0, f"config-2 obsolete every {every}")
+    assert g["n_kv"] < n
