@@ -288,8 +288,7 @@ def main():
     elif a.workload == "col":
         fmt = N.PBL_FMT_COL_CRDB1
         buf, off, lens, n_kv = gen_col_blocks(seed, nb, a.block_size, n_threads=16, obsolete_every=a.hide)
-        kernel = ("colblk_decode_kernel" if a.kernel == "single" else
-                  "colblk_hide_kernel" if a.hide else "colblk_pipe_kernel")
+        kernel = "colblk_decode_kernel" if a.kernel == "single" and not a.hide else "colblk_pipe_kernel"
         wl = (f"config3: {nb} x {a.block_size // 1024} KiB colblk blocks per GPU, cockroachkvs crdb1 schema "
               f"(KeyGenConfig alphabet 26, RoachKeyLen 12, PrefixLenShared 4, 1 key/prefix), 128 B values"
               + (f", every {a.hide}th row isObsolete, HideObsoletePoints fused" if a.hide else ""))
