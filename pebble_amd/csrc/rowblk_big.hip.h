@@ -163,6 +163,12 @@ __global__ void __launch_bounds__(kWave) big_block_sizes_kernel(Args A) {
 // value is HBM-bandwidth work, which a single wave inside the pipeline (each
 // granule behind the previous store's vmcnt) turned into latency-bound work,
 // and its serial walk would hold the workgroup's pipeline.
+#ifndef PBL_BIG_WIN
+#define PBL_BIG_WIN 16  // blocks per wave per round (the big ones among them walked one after another)
+#endif
+#ifndef PBL_BIG_U
+#define PBL_BIG_U 8  // value granules per lane in flight (16: within noise on config 5)
+#endif
 __global__ void __launch_bounds__(kWave) big_block_values_kernel(Args A) {
   __shared__ uint4 keybuf4[kLdsBlkBytes / 16];
   const uint32_t nb = A.in.n_blocks, flags = A.in.flags;
@@ -170,9 +176,9 @@ __global__ void __launch_bounds__(kWave) big_block_values_kernel(Args A) {
   if (__hip_atomic_load(to_glb(reinterpret_cast<uint32_t*>(A.out.workspace) + kWsBigCount), __ATOMIC_RELAXED,
                         __HIP_MEMORY_SCOPE_AGENT) == 0)
     return;
-  for (uint64_t base = uint64_t(blockIdx.x) * kWave; base < nb; base += uint64_t(gridDim.x) * kWave) {
+  for (uint64_t base = uint64_t(blockIdx.x) * PBL_BIG_WIN; base < nb; base += uint64_t(gridDim.x) * PBL_BIG_WIN) {
     const uint64_t bl = base + lane_id();
-    uint64_t big = __ballot(bl < nb && to_glb(A.in.block_len)[bl] > kMaxFastLen &&
+    uint64_t big = __ballot(lane_id() < PBL_BIG_WIN && bl < nb && to_glb(A.in.block_len)[bl] > kMaxFastLen &&
                             (!A.in.block_format || to_glb(A.in.block_format)[bl] == PBL_FMT_ROW) &&
                             to_glb(A.out.blk_status)[bl] == PBL_OK);
     while (big) {
@@ -182,7 +188,7 @@ __global__ void __launch_bounds__(kWave) big_block_values_kernel(Args A) {
       const uint64_t bases[kNumComp] = {A.out.blk_kv_base[b], A.out.blk_key_base[b], A.out.blk_val_base[b],
                                         A.out.blk_rst_base ? A.out.blk_rst_base[b] : 0};
       SlowState ss;
-      slow_walk_t<SlowGlb, 8>(SlowGlb{to_glb(A.in.blocks + A.in.block_off[b]), blen}, blen, flags, A.in.synthetic_seq_num,
+      slow_walk_t<SlowGlb, PBL_BIG_U>(SlowGlb{to_glb(A.in.blocks + A.in.block_off[b]), blen}, blen, flags, A.in.synthetic_seq_num,
                               to_lds_ptr(reinterpret_cast<uint8_t*>(keybuf4)), uint32_t(kLdsBlkBytes), kPassAll,
                               A.out, b, bases, &ss);
     }

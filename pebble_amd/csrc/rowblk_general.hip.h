@@ -114,6 +114,8 @@ __device__ __forceinline__ void slow_walk_t(const Src S, uint64_t len, uint32_t 
   uint64_t nkv = 0, kb = 0, vb = 0, full_len = 0;
   int64_t offset = 0;
   uint32_t ri = 0;
+  // restart word ri, held in a register: re-read only when the walk passes it
+  uint32_t rw_ri = (pass == kPassAll && nr > 0 && restarts >= 0) ? S.le32(uint64_t(restarts)) : 0u;
   uint32_t status = PBL_OK;
   // the next entry's header window is loaded before this entry's stores: a
   // load's data waits for every older vector-memory op, so a header read
@@ -181,9 +183,12 @@ __device__ __forceinline__ void slow_walk_t(const Src S, uint64_t len, uint32_t 
       else fl |= PBL_KV_BLOB_HANDLE;
     }
     if (pass == kPassAll) {
-      while (ri < uint32_t(nr) && int64_t(S.le32(uint64_t(restarts) + 4 * ri) & kRestartMask) < offset) ri++;
+      while (ri < uint32_t(nr) && int64_t(rw_ri & kRestartMask) < offset) {
+        ri++;
+        if (ri < uint32_t(nr)) rw_ri = S.le32(uint64_t(restarts) + 4 * ri);
+      }
       if (ri < uint32_t(nr)) {
-        const uint32_t rw = S.le32(uint64_t(restarts) + 4 * ri);
+        const uint32_t rw = rw_ri;
         if (int64_t(rw & kRestartMask) == offset) {
           fl |= PBL_KV_RESTART;
           if (rw & 0x80000000u) fl |= PBL_KV_RESTART_SAMEPFX;

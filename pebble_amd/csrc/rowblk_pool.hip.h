@@ -527,6 +527,47 @@ __device__ __forceinline__ void key_load(const Slot<kHide>& W, const Src& V, boo
   }
 }
 
+// A user key off the fast form (longer than 16 bytes, or a deeper prefix
+// chain): the chunks that reach into the shared prefix are merged along the
+// chain; the rest lie in the entry's own bytes and go four 16-B loads at a
+// time (the loads of a step in flight together).
+#ifndef PBL_POOL_KOWN
+#define PBL_POOL_KOWN 4
+#endif
+// Keys whose own bytes run past kWaveKey leave those to the whole wave
+// (wave_key_own): only the chunks that reach into the shared prefix are
+// stored here.
+#ifndef PBL_POOL_WAVEKEY
+#define PBL_POOL_WAVEKEY 128
+#endif
+constexpr uint32_t kWaveKey = PBL_POOL_WAVEKEY;
+__device__ __forceinline__ bool wave_key(uint32_t ukl, uint32_t sh) { return ukl > kWaveKey && ukl >= sh + 16; }
+template <class Src>
+__device__ __forceinline__ void store_key_general(const uint64_t* M0, const Src& V, uint64_t m, uint32_t ukl,
+                                                  gptr<uint8_t> dst) {
+  const uint32_t sh = m_sh(m);
+  const int32_t own = int32_t(m_ksrc(m)) - int32_t(sh);  // block offset of key byte 0 in the entry's bytes
+  uint32_t c = 0;
+  for (; c < ukl && c < sh; c += 16) {
+    const uint32_t n = ukl - c < 16 ? ukl - c : 16u;
+    store_n(dst + c, key_chunk(M0, V, m, c, n), n);
+  }
+  if (wave_key(ukl, sh)) return;
+  for (; c < ukl; c += 16 * PBL_POOL_KOWN) {
+    uint4 w[PBL_POOL_KOWN];
+#pragma unroll
+    for (int k = 0; k < PBL_POOL_KOWN; k++) {
+      const uint32_t cc = c + 16 * k;
+      w[k] = cc < ukl ? V.ld16(own + int32_t(cc)) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < PBL_POOL_KOWN; k++) {
+      const uint32_t cc = c + 16 * k;
+      if (cc < ukl) store_n(dst + cc, w[k], ukl - cc < 16 ? ukl - cc : 16u);
+    }
+  }
+}
+
 // The batch's stores.  Key output offsets: an exclusive wave scan of the user-
 // key lengths per u, `kcar` carrying the running total (KV nkv gets the total).
 template <bool kHide, class Src>
@@ -537,12 +578,14 @@ __device__ __forceinline__ void key_store(const Slot<kHide>& W, const Src& V, co
   const pbl_decode_out& O = A.out;
   const gptr<uint8_t> kbytes = to_glb(O.key_bytes) + kbb;
   const bool raw = (flags & PBL_ROW_RAW_KEYS) != 0;
+  uint32_t kc0[kKU];
 #pragma unroll
   for (int u = 0; u < kKU; u++) {
     const uint32_t j = j0 + kWave * u + l;
     const uint64_t m = K.m[u];
     const uint32_t ukl = j < nkv ? ukl_of(m, raw) : 0u;
     const uint32_t incl = dpp_incl_scan(ukl);
+    kc0[u] = kcar;
     const uint32_t ko = kcar + incl - ukl;
     kcar += last_lane(incl);
     if (j > nkv) continue;
@@ -555,10 +598,7 @@ __device__ __forceinline__ void key_store(const Slot<kHide>& W, const Src& V, co
     if (!key_fast(m, K.mp[u], raw)) {
       const uint32_t e = kHide ? uint32_t(W.ent[j]) : j;
       t = trailer_of(W.m0, V, int(e), m, &f, flags);
-      for (uint32_t c = 0; c < ukl; c += 16) {
-        const uint32_t n = ukl - c < 16 ? ukl - c : 16u;
-        store_n(kbytes + ko + c, key_chunk(W.m0, V, m, c, n), n);
-      }
+      store_key_general(W.m0, V, m, ukl, kbytes + ko);
     } else {
       if (raw) t = 0;
       else if (kl < 8) t = kKindInvalid;
@@ -581,6 +621,36 @@ __device__ __forceinline__ void key_store(const Slot<kHide>& W, const Src& V, co
     if (O.kv_flags) st_out(to_glb(O.kv_flags) + (kvb + j), uint8_t(f));
     if (O.entry_off) st_out(to_glb(O.entry_off) + (kvb + j), uint32_t(m_ksrc(m) - m_hl(m)));
   }
+  // the own bytes [shared, ukl) of long keys: one contiguous range of the
+  // entry each, copied by the whole wave (16-B chunks, the last one ending at
+  // the key's end, four per lane in flight)
+#pragma unroll
+  for (int u = 0; u < kKU; u++) {
+    const uint32_t j = j0 + kWave * u + l;
+    const uint64_t m = K.m[u];
+    const uint32_t ukl = j < nkv ? ukl_of(m, raw) : 0u, sh = m_sh(m);
+    const bool wk = j < nkv && !key_fast(m, K.mp[u], raw) && wave_key(ukl, sh);
+    const uint32_t incl = dpp_incl_scan(ukl);  // (the batch's key offsets again)
+    const uint32_t ko = kc0[u] + incl - ukl;
+    for (uint64_t lm = __ballot(wk); lm; lm &= lm - 1) {
+      const int sl = __builtin_ctzll(lm);
+      const int32_t src = __shfl(int32_t(m_ksrc(m)), sl, kWave);
+      const uint32_t len = __shfl(ukl - sh, sl, kWave), dst = __shfl(ko + sh, sl, kWave);
+      for (uint32_t o0 = 16u * l; o0 < len; o0 += 64u * kWave) {
+        uint4 y[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t o = o0 + 16u * kWave * k, q = o < len - 16 ? o : len - 16;
+          y[k] = V.ld16(src + int32_t(o < len ? q : 0u));
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t o = o0 + 16u * kWave * k, q = o < len - 16 ? o : len - 16;
+          if (o < len) st_out((gptr<u32x4_ug>)(kbytes + dst + q), u32x4_ug{y[k].x, y[k].y, y[k].z, y[k].w});
+        }
+      }
+    }
+  }
 }
 
 // Value bytes of a block, 8 lanes per KV: lane c of a group copies its
@@ -596,7 +666,10 @@ __device__ __forceinline__ void key_store(const Slot<kHide>& W, const Src& V, co
 #define PBL_POOL_VG 8
 #endif
 constexpr int kVG = PBL_POOL_VG;
-constexpr uint32_t kWaveVal = 1024;
+#ifndef PBL_POOL_WAVEVAL
+#define PBL_POOL_WAVEVAL 1024
+#endif
+constexpr uint32_t kWaveVal = PBL_POOL_WAVEVAL;
 // One step of the value copy: kVG KVs per 8-lane group, j = j0 + 8 u + lane / 8.
 // Only the loaded chunks are held between a step's loads and its stores (the
 // offsets are re-read from the slot).
@@ -640,9 +713,19 @@ __device__ __forceinline__ void val_store(const uint32_t* vp, uint32_t nkv, uint
     const VSeg S = val_seg(vp, nkv, jl + 8 * u);
     if (S.has) st_out((gptr<u32x4_ug>)(vbytes + S.vo + S.q), u32x4_ug(B.x[u]));
     if (S.vl > 128 && S.vl <= kWaveVal) {
-      for (uint32_t o = 16 * c + 128; o < S.vl; o += 128) {
-        const uint32_t q = o < S.vl - 16 ? o : S.vl - 16;
-        st_out((gptr<u32x4_ug>)(vbytes + S.vo + q), u32x4_ug(*(gptr<const u32x4_ug>)(g + S.vs + q)));
+      // the value's further chunks, four per lane in flight
+      for (uint32_t o0 = 16 * c + 128; o0 < S.vl; o0 += 512) {
+        u32x4 y[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t o = o0 + 128 * k, q = o < S.vl - 16 ? o : S.vl - 16;
+          if (o < S.vl) y[k] = *(gptr<const u32x4_ug>)(g + S.vs + q);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t o = o0 + 128 * k, q = o < S.vl - 16 ? o : S.vl - 16;
+          if (o < S.vl) st_out((gptr<u32x4_ug>)(vbytes + S.vo + q), u32x4_ug(y[k]));
+        }
       }
     } else if (S.vl < 16) {
       for (uint32_t o = c; o < S.vl; o += 8) vbytes[S.vo + o] = g[S.vs + o];

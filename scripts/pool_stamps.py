@@ -19,7 +19,12 @@ from pebble_amd.batch import BlockBatch, decode  # noqa: E402
 from pebble_amd.rowblk import gen_row_blocks  # noqa: E402
 
 nb = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
-buf, off, lens, n = gen_row_blocks(42, nb, 32768, 16, 16, 100, n_threads=16)
+wl = os.environ.get("WORKLOAD", "row")  # row (config 2) or zipf:RI (config 5, row format)
+if wl.startswith("zipf"):
+    from pebble_amd.batch import gen_zipf_blocks
+    buf, off, lens, n = gen_zipf_blocks(42, nb, N.PBL_FMT_ROW, int(wl.split(":")[1]), 32768, n_threads=16)
+else:
+    buf, off, lens, n = gen_row_blocks(42, nb, 32768, 16, 16, 100, n_threads=16)
 b = BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, N.PBL_KERNEL_POOL)
 for _ in range(3):
     out = decode(b)
