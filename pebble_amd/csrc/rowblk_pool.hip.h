@@ -489,10 +489,26 @@ __device__ __forceinline__ uint4 key_chunk(const uint64_t* M0, const Src& V, uin
 #define PBL_POOL_KU 1
 #endif
 constexpr int kKU = PBL_POOL_KU;
+// PBL_POOL_KMETA 0: the metadata words are not held between a batch's loads
+// and its stores (re-read from the slot: two LDS reads, fewer VGPRs per
+// step in flight).
+#ifndef PBL_POOL_KMETA
+#define PBL_POOL_KMETA 1
+#endif
 struct KBatch {
-  uint64_t m[kKU], mp[kKU], tr[kKU];
+#if PBL_POOL_KMETA
+  uint64_t m[kKU], mp[kKU];
+#endif
+  uint64_t tr[kKU];
   uint4 ka[kKU], kp[kKU];
 };
+// The metadata word of visible KV j and its prefix parent's (0 past nkv).
+template <bool kHide>
+__device__ __forceinline__ void kv_meta(const Slot<kHide>& W, uint32_t j, uint32_t nkv, uint64_t* m, uint64_t* mp) {
+  const uint32_t e = kHide ? (j < nkv ? uint32_t(W.ent[j]) : 0u) : j;
+  *m = j < nkv ? W.m0[e] : 0ull;
+  *mp = (j < nkv && m_sh(*m) != 0) ? W.m0[m_par(*m)] : 0ull;
+}
 
 __device__ __forceinline__ uint32_t ukl_of(uint64_t m, bool raw) {
   const uint32_t kl = m_klen(m);
@@ -507,23 +523,26 @@ template <bool kHide, class Src>
 __device__ __forceinline__ void key_load(const Slot<kHide>& W, const Src& V, bool raw, uint32_t j0, uint32_t nkv,
                                          KBatch& K) {
   const int l = lane_id();
+  uint64_t Km[kKU], Kmp[kKU];
+#pragma unroll
+  for (int u = 0; u < kKU; u++) kv_meta<kHide>(W, j0 + kWave * u + l, nkv, &Km[u], &Kmp[u]);
+#if PBL_POOL_KMETA
 #pragma unroll
   for (int u = 0; u < kKU; u++) {
-    const uint32_t j = j0 + kWave * u + l;
-    const uint32_t e = kHide ? (j < nkv ? uint32_t(W.ent[j]) : 0u) : j;
-    K.m[u] = j < nkv ? W.m0[e] : 0ull;
-    K.mp[u] = (j < nkv && m_sh(K.m[u]) != 0) ? W.m0[m_par(K.m[u])] : 0ull;
+    K.m[u] = Km[u];
+    K.mp[u] = Kmp[u];
   }
+#endif
 #pragma unroll
   for (int u = 0; u < kKU; u++) {
     const uint32_t j = j0 + kWave * u + l;
-    const uint64_t m = K.m[u];
+    const uint64_t m = Km[u];
     const uint32_t kl = m_klen(m), sh = m_sh(m), ukl = ukl_of(m, raw);
-    const bool fast = j < nkv && key_fast(m, K.mp[u], raw);
+    const bool fast = j < nkv && key_fast(m, Kmp[u], raw);
     K.tr[u] = 0;
     if (fast && !raw && kl >= 8) K.tr[u] = V.ld8(m_ksrc(m) + (kl - 8 - sh));
     if (fast && ukl) K.ka[u] = V.ld16(int32_t(m_ksrc(m)) - int32_t(sh));
-    if (fast && ukl && sh) K.kp[u] = V.ld16(int32_t(m_ksrc(K.mp[u])));
+    if (fast && ukl && sh) K.kp[u] = V.ld16(int32_t(m_ksrc(Kmp[u])));
   }
 }
 
@@ -579,10 +598,20 @@ __device__ __forceinline__ void key_store(const Slot<kHide>& W, const Src& V, co
   const gptr<uint8_t> kbytes = to_glb(O.key_bytes) + kbb;
   const bool raw = (flags & PBL_ROW_RAW_KEYS) != 0;
   uint32_t kc0[kKU];
+  uint64_t Km[kKU], Kmp[kKU];
+#pragma unroll
+  for (int u = 0; u < kKU; u++) {
+#if PBL_POOL_KMETA
+    Km[u] = K.m[u];
+    Kmp[u] = K.mp[u];
+#else
+    kv_meta<kHide>(W, j0 + kWave * u + l, nkv, &Km[u], &Kmp[u]);
+#endif
+  }
 #pragma unroll
   for (int u = 0; u < kKU; u++) {
     const uint32_t j = j0 + kWave * u + l;
-    const uint64_t m = K.m[u];
+    const uint64_t m = Km[u];
     const uint32_t ukl = j < nkv ? ukl_of(m, raw) : 0u;
     const uint32_t incl = dpp_incl_scan(ukl);
     kc0[u] = kcar;
@@ -595,7 +624,7 @@ __device__ __forceinline__ void key_store(const Slot<kHide>& W, const Src& V, co
     const uint32_t kl = m_klen(m), sh = m_sh(m);
     uint64_t t;
     uint32_t f = m_fl(m);
-    if (!key_fast(m, K.mp[u], raw)) {
+    if (!key_fast(m, Kmp[u], raw)) {
       const uint32_t e = kHide ? uint32_t(W.ent[j]) : j;
       t = trailer_of(W.m0, V, int(e), m, &f, flags);
       store_key_general(W.m0, V, m, ukl, kbytes + ko);
@@ -627,9 +656,9 @@ __device__ __forceinline__ void key_store(const Slot<kHide>& W, const Src& V, co
 #pragma unroll
   for (int u = 0; u < kKU; u++) {
     const uint32_t j = j0 + kWave * u + l;
-    const uint64_t m = K.m[u];
+    const uint64_t m = Km[u];
     const uint32_t ukl = j < nkv ? ukl_of(m, raw) : 0u, sh = m_sh(m);
-    const bool wk = j < nkv && !key_fast(m, K.mp[u], raw) && wave_key(ukl, sh);
+    const bool wk = j < nkv && !key_fast(m, Kmp[u], raw) && wave_key(ukl, sh);
     const uint32_t incl = dpp_incl_scan(ukl);  // (the batch's key offsets again)
     const uint32_t ko = kc0[u] + incl - ukl;
     for (uint64_t lm = __ballot(wk); lm; lm &= lm - 1) {
@@ -1061,14 +1090,13 @@ __device__ __forceinline__ void block_emit(const Pend& P, const Slot<kHide>& W, 
   // first restart words: all in one round trip
   LbWindows<kLbWin> G;
   if (b > 0) G.issue(LbPtrs(lb_state, nb), int64_t(b) - 1);
-  KBatch K, K1;
+  KBatch K;
   VBatch VB, VB1;
   uint32_t rs0 = 0;
   const bool ok0 = P.status == PBL_OK;
   if (ok0) {
     key_load<kHide, GSrc>(W, KS, raw, 0, nkv, K);
     val_load(W.vp, gb, nkv, 0, VB);
-    if (kUni && kVDepth == 2) key_load<kHide, GSrc>(W, KS, raw, kWave, nkv, K1);
     if (kVDepth == 2) val_load(W.vp, gb, nkv, 8 * kVG, VB1);
     if (O.restarts && uint32_t(l) < nres) rs0 = KS.le32(P.roff + 4 * l);
   }
@@ -1110,26 +1138,17 @@ __device__ __forceinline__ void block_emit(const Pend& P, const Slot<kHide>& W, 
         VB = VN;
       }
     } else {
-      for (uint32_t j0 = 0; j0 <= nkv; j0 += 2 * kWave) {
-        KBatch KN, KN1;
-        VBatch VN, VN1;
-        if (j0 + 2 * kWave <= nkv) {
-          key_load<kHide, GSrc>(W, KS, raw, j0 + 2 * kWave, nkv, KN);
-          val_load(W.vp, gb, nkv, j0 + 2 * kWave, VN);
-        }
+      // the values two steps ahead, the keys one
+      for (uint32_t j0 = 0; j0 <= nkv; j0 += kWave) {
+        KBatch KN;
+        VBatch VN;
+        if (j0 + kWave <= nkv) key_load<kHide, GSrc>(W, KS, raw, j0 + kWave, nkv, KN);
+        if (j0 + 2 * kWave < nkv) val_load(W.vp, gb, nkv, j0 + 2 * kWave, VN);
         key_store<kHide, GSrc>(W, KS, A, b, j0, nkv, kvb, kbb, K, kcar);
         val_store(W.vp, nkv, j0, VB, gb, vbytes);
-        if (j0 + kWave > nkv) break;
-        if (j0 + 3 * kWave <= nkv) {
-          key_load<kHide, GSrc>(W, KS, raw, j0 + 3 * kWave, nkv, KN1);
-          val_load(W.vp, gb, nkv, j0 + 3 * kWave, VN1);
-        }
-        key_store<kHide, GSrc>(W, KS, A, b, j0 + kWave, nkv, kvb, kbb, K1, kcar);
-        val_store(W.vp, nkv, j0 + kWave, VB1, gb, vbytes);
         K = KN;
-        VB = VN;
-        K1 = KN1;
-        VB1 = VN1;
+        VB = VB1;
+        VB1 = VN;
       }
     }
     if (O.restarts)
