@@ -72,6 +72,16 @@ __device__ __forceinline__ Src slot_src(const Slot& P, const Args& A) {
              (glb_cu8)(A.in.blocks + P.boff), P.nhead, P.tail_lo, P.blen};
 }
 
+// 16 bytes of block E at block offset j (any alignment, [j, j + 16) inside the
+// block): from the staged head or tail when they hold them, else global.
+__device__ __forceinline__ uint4 slot_ld16(const Slot& E, const Args& A, uint32_t j) {
+  if (j + 16 <= E.nhead) return lds_bytes16((lds_cu32)to_lds(E.head4), E.shift + j);
+  if (j >= E.tail_lo && j + 16 <= E.blen) return lds_bytes16((lds_cu32)to_lds(E.tail4), E.shift + j - E.tail_lo);
+  typedef u32x4 u32x4_ua __attribute__((aligned(1)));
+  const u32x4 v = *(gptr<const u32x4_ua>)(to_glb(A.in.blocks) + E.boff + j);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // Head / tail geometry of a block (same split as col_block).
 __device__ __forceinline__ void geometry(uint32_t blen, uint32_t* nhead, uint32_t* tail_lo) {
   *nhead = blen < kStage ? blen : kStage;
@@ -237,9 +247,43 @@ __device__ __forceinline__ void col_parse(CLds& L, Slot& P, const Slot& E, const
 }
 
 // ---- emit phase (whole workgroup) --------------------------------------------------
+// The values range of a block: 16-B chunks of the source (chunk k at range
+// offset min(16 k, n - 16): the last one ends at the range's end), each read
+// from the staged head or tail or from global memory and stored unaligned at
+// the same offset of the output; kValU chunks per thread per step.  The first
+// step is loaded at the start of the emit (ValStep), so its round trip runs
+// under the key build and the per-row stores.
+#ifndef PBL_COL_VALU
+#define PBL_COL_VALU 4
+#endif
+constexpr int kValU = PBL_COL_VALU;
+struct ValStep {
+  u32x4 x[kValU];
+};
+__device__ __forceinline__ void val_step_load(const Slot& E, const Args& A, uint32_t j0, uint32_t n, uint32_t k0,
+                                              ValStep& V) {
+  const uint32_t nch = (n + 15) >> 4;
+#pragma unroll
+  for (int u = 0; u < kValU; u++) {
+    const uint32_t k = k0 + kTPB * u, q = 16 * k < n - 16 ? 16 * k : n - 16;
+    uint4 w = make_uint4(0, 0, 0, 0);
+    if (n >= 16 && k < nch) w = slot_ld16(E, A, j0 + q);
+    V.x[u] = u32x4{w.x, w.y, w.z, w.w};
+  }
+}
+__device__ __forceinline__ void val_step_store(uint8_t* vout, uint32_t n, uint32_t k0, const ValStep& V) {
+  typedef u32x4 u32x4_ua __attribute__((aligned(1)));
+  const uint32_t nch = (n + 15) >> 4;
+#pragma unroll
+  for (int u = 0; u < kValU; u++) {
+    const uint32_t k = k0 + kTPB * u, q = 16 * k < n - 16 ? 16 * k : n - 16;
+    if (n >= 16 && k < nch) __builtin_nontemporal_store(u32x4_ua(V.x[u]), (gptr<u32x4_ua>)(to_glb(vout) + q));
+  }
+}
+
 template <bool F>
 __device__ __forceinline__ void col_emit_rows(CLds& L, const Slot& E, const Args& A, uint32_t schema, const Src& S,
-                                              bool prebuilt, uint32_t ex0, uint32_t tot0) {
+                                              bool prebuilt, uint32_t ex0, uint32_t tot0, const ValStep& V0) {
   const int t = threadIdx.x;
   const pbl_decode_out& O = A.out;
   const uint32_t b = E.b;
@@ -323,73 +367,26 @@ __device__ __forceinline__ void col_emit_rows(CLds& L, const Slot& E, const Args
   if (t == 0) key_off[kvb + b + rows] = cbase;
   CSTAMP(A, b, 6);
 
-  // value bytes: one contiguous range.  Source granules inside the staged head
-  // or tail come from LDS (the values column usually starts inside the 12 KiB
-  // head: reading those bytes from global again cost ~25 % extra fetch); the
-  // rest global -> global, four output granules per thread per step so their
-  // source loads are in flight together
+  // value bytes: one contiguous range (val_step_*), the first step loaded at
+  // the start of the emit
   {
-    const uint64_t src_lo = E.boff + d.v_data + d.v_lo;
-    const int64_t rel_lo = int64_t(d.v_data + d.v_lo);  // block-relative
-    const uint64_t n = d.v_hi - d.v_lo;
-    const uint64_t lo = vbb, hi = vbb + n;
-    const gptr<const uint8_t> G = to_glb(A.in.blocks);
-    const int64_t s_end = int64_t(src_lo + n);
-    const lds_cu32 HW = (lds_cu32)to_lds(E.head4), TW = (lds_cu32)to_lds(E.tail4);
-    const int64_t nhead = E.nhead, tail_lo = E.tail_lo, blen = E.blen, shift = E.shift;
-    constexpr int U = 4;
-#ifdef PBL_EXP_COL_NOVAL  // traffic attribution only: value bytes skipped
-    for (uint64_t g0 = hi; g0 < hi; g0 += 16ull * kTPB * U) {
-#else
-    for (uint64_t g0 = (lo & ~uint64_t(15)) + 16ull * t; g0 < hi; g0 += 16ull * kTPB * U) {
-#endif
-      u32x4 x[U], y[U];
-      uint32_t sh[U];
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const uint64_t ga = g0 + 16ull * kTPB * u;
-        const int64_t j = rel_lo + int64_t(ga) - int64_t(lo);  // block offset of the granule's first byte
-        const int64_t sx = int64_t(src_lo) + int64_t(ga) - int64_t(lo);
-        const int64_t sa = sx & ~int64_t(15);
-        sh[u] = uint32_t(sx - sa);
-        const bool live = ga < hi;
-        x[u] = u32x4{0, 0, 0, 0};
-        y[u] = u32x4{0, 0, 0, 0};
-        if (live && j >= 0 && j + 16 <= nhead) {
-          const uint4 w = lds_bytes16(HW, uint32_t(shift + j));
-          x[u] = u32x4{w.x, w.y, w.z, w.w};
-          sh[u] = 0;
-        } else if (live && j >= tail_lo && j + 16 <= blen) {
-          const uint4 w = lds_bytes16(TW, uint32_t(shift + j - tail_lo));
-          x[u] = u32x4{w.x, w.y, w.z, w.w};
-          sh[u] = 0;
-        } else {
-          if (live && sa + 16 > int64_t(src_lo) && sa < s_end) x[u] = *(gptr<const u32x4>)(G + sa);
-          if (live && sh[u] && sa + 32 > int64_t(src_lo) && sa + 16 < s_end) y[u] = *(gptr<const u32x4>)(G + sa + 16);
-        }
+    const uint32_t j0 = d.v_data + d.v_lo, n = d.v_hi - d.v_lo;
+    uint8_t* vout = O.val_bytes + vbb;
+    if (n >= 16) {
+      const uint32_t nch = (n + 15) >> 4;
+      val_step_store(vout, n, uint32_t(t), V0);
+      for (uint32_t k0 = uint32_t(t) + kTPB * kValU; k0 < nch; k0 += kTPB * kValU) {
+        ValStep V;
+        val_step_load(E, A, j0, n, k0, V);
+        val_step_store(vout, n, k0, V);
       }
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const uint64_t ga = g0 + 16ull * kTPB * u;
-        if (ga >= hi) continue;
-        const uint4 xx = make_uint4(x[u].x, x[u].y, x[u].z, x[u].w);
-        const uint4 yy = make_uint4(y[u].x, y[u].y, y[u].z, y[u].w);
-        store16(O.val_bytes, ga, lo, hi, sh[u] ? funnel16(xx, yy, sh[u]) : xx);
-      }
+    } else {
+      for (uint32_t i = uint32_t(t); i < n; i += kTPB) to_glb(vout)[i] = uint8_t(S.byte(j0 + i));
     }
   }
   CSTAMP(A, b, 7);
 }
 
-// 16 bytes of block E at block offset j (any alignment, [j, j + 16) inside the
-// block): from the staged head or tail when they hold them, else global.
-__device__ __forceinline__ uint4 slot_ld16(const Slot& E, const Args& A, uint32_t j) {
-  if (j + 16 <= E.nhead) return lds_bytes16((lds_cu32)to_lds(E.head4), E.shift + j);
-  if (j >= E.tail_lo && j + 16 <= E.blen) return lds_bytes16((lds_cu32)to_lds(E.tail4), E.shift + j - E.tail_lo);
-  typedef u32x4 u32x4_ua __attribute__((aligned(1)));
-  const u32x4 v = *(gptr<const u32x4_ua>)(to_glb(A.in.blocks) + E.boff + j);
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
 
 // HideObsoletePoints fused into the pipeline's emit (data_block.go:1680-1697):
 // chunk by chunk, a block scan of (visible, key length) and of the visible
@@ -494,6 +491,8 @@ __device__ __forceinline__ void col_emit_t(CLds& L, const Slot& E, const Args& A
     col_emit_rows_hide<F>(L, E, A, schema, S);
     return;
   }
+  ValStep V0;  // the values' first step, in flight under the key build
+  val_step_load(E, A, E.d.v_data + E.d.v_lo, E.d.v_hi - E.d.v_lo, uint32_t(t), V0);
   // keys of a single-chunk block are built in LDS first (one scan + one barrier)
   const uint32_t rows = E.d.rows;
   const bool prebuilt = rows <= kChunk && E.tot0 <= kKeyBuf;
@@ -508,7 +507,7 @@ __device__ __forceinline__ void col_emit_t(CLds& L, const Slot& E, const Args& A
     __syncthreads();
   }
   CSTAMP(A, b, 4);
-  col_emit_rows<F>(L, E, A, schema, S, prebuilt, ex, tot);
+  col_emit_rows<F>(L, E, A, schema, S, prebuilt, ex, tot, V0);
 }
 
 template <bool kHide>
