@@ -298,11 +298,7 @@ __device__ __forceinline__ void col_emit_rows(CLds& L, const Slot& E, const Args
 
   // per-row arrays
   const UCol& vo = d.v_off;
-#ifdef PBL_EXP_COL_NOROW  // traffic attribution only (scripts/col_traffic.sh): per-row arrays skipped
-  for (uint32_t r = t; r <= 0u; r += kTPB) {
-#else
   for (uint32_t r = t; r <= rows; r += kTPB) {
-#endif
     const uint32_t v = vo.w ? uint32_t(S.le(vo.at + r * vo.w, vo.w)) : 0;
     val_off[kvb + b + r] = v - d.v_lo;
     if (r < rows) {
@@ -327,9 +323,6 @@ __device__ __forceinline__ void col_emit_rows(CLds& L, const Slot& E, const Args
   // aligned 16-B granules (keys past the buffer go straight to global memory)
   lds_u8 kb8 = (lds_u8)to_lds(L.key4);
   uint32_t cbase = 0;
-#ifdef PBL_EXP_COL_NOKEY
-  prebuilt = false;
-#endif
   if (prebuilt) {
     // single chunk, built in LDS while wave 0 resolved the look-back
     if (uint32_t(t) < rows) key_off[kvb + b + t] = ex0;
@@ -339,11 +332,7 @@ __device__ __forceinline__ void col_emit_rows(CLds& L, const Slot& E, const Args
       store16(O.key_bytes, ga, lo, hi, lds_bytes16(W, uint32_t(kKeyPad + ga - lo)));
     cbase = tot0;
   }
-#ifdef PBL_EXP_COL_NOKEY  // traffic attribution only: key bytes skipped
-  for (uint32_t c = 0; c < 0u; c++) {
-#else
   for (uint32_t c = 0; c < (prebuilt ? 0u : nch); c++) {
-#endif
     const uint32_t r = c * kChunk + t;
     RowParts p;
     p.klen = 0;
