@@ -157,25 +157,41 @@ __global__ void __launch_bounds__(kWave) big_block_sizes_kernel(Args A) {
   }
 }
 
-// Outputs of the blocks past the LDS stage, launched after rowblk_pipe_kernel
-// on the same stream (which resolved their bases into blk_*_base).  One wave
-// per block, all big blocks at once, 8 value granules per lane in flight: a big
-// value is HBM-bandwidth work, which a single wave inside the pipeline (each
-// granule behind the previous store's vmcnt) turned into latency-bound work,
-// and its serial walk would hold the workgroup's pipeline.
+// Outputs of the blocks past the LDS stage, launched after the row kernel on
+// the same stream (which resolved their bases into blk_*_base).  The walk is a
+// latency chain per block (an entry's header, its key bytes, its value), so
+// what pays is blocks in flight: tier 1 walks with a kBigKeySmall key buffer
+// (8 KiB of LDS: ~19 one-wave workgroups per CU, a workgroup per 16-block
+// window, every window's big blocks at once); a block with a longer key
+// (its sizes pass, with the full buffer, said OK) is listed in the workspace
+// (ids area, count at header word kWsBigRedo) and walked again by tier 2 with
+// the whole 32 KiB buffer, rewriting the same outputs.  8 value granules per
+// lane in flight.
 #ifndef PBL_BIG_WIN
-#define PBL_BIG_WIN 16  // blocks per wave per round (the big ones among them walked one after another)
+#define PBL_BIG_WIN 16  // blocks per tier-1 workgroup
 #endif
 #ifndef PBL_BIG_U
 #define PBL_BIG_U 8  // value granules per lane in flight (16: within noise on config 5)
 #endif
+constexpr uint32_t kBigKeySmall = 8192;
+constexpr int kWsBigRedo = 5;  // header u32 [5]: tier-2 blocks (their ids in the ids area)
+
+__device__ __forceinline__ void big_block_walk(const Args& A, uint32_t b, lptr<uint8_t> keybuf, uint32_t keycap,
+                                               SlowState* ss) {
+  const uint32_t blen = A.in.block_len[b];
+  const uint64_t bases[kNumComp] = {A.out.blk_kv_base[b], A.out.blk_key_base[b], A.out.blk_val_base[b],
+                                    A.out.blk_rst_base ? A.out.blk_rst_base[b] : 0};
+  slow_walk_t<SlowGlb, PBL_BIG_U>(SlowGlb{to_glb(A.in.blocks + A.in.block_off[b]), blen}, blen, A.in.flags,
+                                  A.in.synthetic_seq_num, keybuf, keycap, kPassAll, A.out, b, bases, ss);
+}
+
 __global__ void __launch_bounds__(kWave) big_block_values_kernel(Args A) {
-  __shared__ uint4 keybuf4[kLdsBlkBytes / 16];
-  const uint32_t nb = A.in.n_blocks, flags = A.in.flags;
+  __shared__ uint4 keybuf4[kBigKeySmall / 16];
+  const uint32_t nb = A.in.n_blocks;
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(A.out.workspace);
   // (the size pass counted the big blocks; usually there are none)
-  if (__hip_atomic_load(to_glb(reinterpret_cast<uint32_t*>(A.out.workspace) + kWsBigCount), __ATOMIC_RELAXED,
-                        __HIP_MEMORY_SCOPE_AGENT) == 0)
-    return;
+  if (__hip_atomic_load(to_glb(hdr) + kWsBigCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  uint32_t* redo = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(A.out.workspace) + ws_ids_offset(nb));
   for (uint64_t base = uint64_t(blockIdx.x) * PBL_BIG_WIN; base < nb; base += uint64_t(gridDim.x) * PBL_BIG_WIN) {
     const uint64_t bl = base + lane_id();
     uint64_t big = __ballot(lane_id() < PBL_BIG_WIN && bl < nb && to_glb(A.in.block_len)[bl] > kMaxFastLen &&
@@ -184,14 +200,25 @@ __global__ void __launch_bounds__(kWave) big_block_values_kernel(Args A) {
     while (big) {
       const uint32_t b = uint32_t(base) + uint32_t(__builtin_ctzll(big));
       big &= big - 1;
-      const uint32_t blen = A.in.block_len[b];
-      const uint64_t bases[kNumComp] = {A.out.blk_kv_base[b], A.out.blk_key_base[b], A.out.blk_val_base[b],
-                                        A.out.blk_rst_base ? A.out.blk_rst_base[b] : 0};
       SlowState ss;
-      slow_walk_t<SlowGlb, PBL_BIG_U>(SlowGlb{to_glb(A.in.blocks + A.in.block_off[b]), blen}, blen, flags, A.in.synthetic_seq_num,
-                              to_lds_ptr(reinterpret_cast<uint8_t*>(keybuf4)), uint32_t(kLdsBlkBytes), kPassAll,
-                              A.out, b, bases, &ss);
+      big_block_walk(A, b, to_lds_ptr(reinterpret_cast<uint8_t*>(keybuf4)), kBigKeySmall, &ss);
+      // (the sizes pass walked it with the full buffer: a failure here is a key
+      // past the small one)
+      if (ss.status != PBL_OK && lane_id() == 0) to_glb(redo)[g_atomic_add(hdr + kWsBigRedo, 1u)] = b;
     }
+  }
+}
+
+__global__ void __launch_bounds__(kWave) big_block_values2_kernel(Args A) {
+  __shared__ uint4 keybuf4[kLdsBlkBytes / 16];
+  const uint32_t nb = A.in.n_blocks;
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(A.out.workspace);
+  const uint32_t n = __hip_atomic_load(to_glb(hdr) + kWsBigRedo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t* redo = reinterpret_cast<const uint32_t*>(reinterpret_cast<uint8_t*>(A.out.workspace) +
+                                                           ws_ids_offset(nb));
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    SlowState ss;
+    big_block_walk(A, to_glb(redo)[i], to_lds_ptr(reinterpret_cast<uint8_t*>(keybuf4)), uint32_t(kLdsBlkBytes), &ss);
   }
 }
 

@@ -388,6 +388,15 @@ uint64_t persistent_grid(hipStream_t st, PersistentKernel k, const void* fn, uin
 }  // namespace pbl
 
 namespace {
+// The big row blocks' outputs (rowblk_big.hip.h): tier 1, a workgroup per
+// 16-block window, then tier 2 over the blocks tier 1 listed.
+void launch_big_values(const pbl::Args& a, hipStream_t st, uint32_t small) {
+  const uint32_t nb = a.in.n_blocks;
+  const uint32_t g1 = (nb + PBL_BIG_WIN - 1) / PBL_BIG_WIN;
+  hipLaunchKernelGGL(pbl::row::rowc::big_block_values_kernel, dim3(g1), dim3(pbl::kWave), 0, st, a);
+  hipLaunchKernelGGL(pbl::row::rowc::big_block_values2_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+}
+
 // Row batches on the staging-pool kernel (rowblk_pool.hip.h), with the same
 // big-block passes around it.
 int launch_row_pool(const pbl::Args& a, hipStream_t st, bool values) {
@@ -408,7 +417,7 @@ int launch_row_pool(const pbl::Args& a, hipStream_t st, bool values) {
   else
     hipLaunchKernelGGL(pbl::row::pool::rowblk_pool_kernel<false>, dim3(uint32_t(grid)), dim3(pbl::row::pool::kTPBP),
                        0, st, a, static_cast<const uint32_t*>(nullptr));
-  if (values) hipLaunchKernelGGL(pbl::row::rowc::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+  if (values) launch_big_values(a, st, small);
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }
 
@@ -458,8 +467,7 @@ int launch_mixed(const pbl_block_batch* batch, const pbl::Args& a, hipStream_t s
     hipLaunchKernelGGL(pbl::row::mixed_col_kernel<true>, dim3(uint32_t(g_c)), dim3(pbl::kTPB), 0, st, a, cids);
   else
     hipLaunchKernelGGL(pbl::row::mixed_col_kernel<false>, dim3(uint32_t(g_c)), dim3(pbl::kTPB), 0, st, a, cids);
-  if (values)
-    hipLaunchKernelGGL(pbl::row::rowc::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+  if (values) launch_big_values(a, st, small);
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }
 

@@ -101,3 +101,30 @@ def test_row_shape_mixes(mix, kern):
     assert g["n_kv"] == n and g["status_mask"] == 0
     g0 = check(buf, off, lens, 0, f"mix={mix} default", 0)
     assert g0["n_kv"] == n
+
+
+def test_big_blocks_with_long_keys(kern):
+    """Blocks past the 32 KiB stage whose keys outgrow the big-block pass's
+    8 KiB key buffer (tier 1 lists them, tier 2 walks them again with the whole
+    buffer), next to big blocks with short keys, shared prefixes reaching deep
+    into the long keys, and ordinary blocks."""
+    from rowutil import make_trailer
+    rng = random.Random(77)
+    blocks = []
+    for i in range(6):
+        w = Writer(rng.choice([1, 4, 16]))
+        base = bytes(rng.randrange(256) for _ in range(rng.choice([9000, 12000, 20000])))
+        for k in range(8):
+            key = base[: len(base) - 40] + b"%08d" % (1000 * i + k) + bytes(rng.randrange(256) for _ in range(32))
+            w.add(key, make_trailer(100 + k, 1), bytes([k]) * rng.choice([100, 3000, 40000]))
+        blocks.append(w.finish())
+    for i in range(6):
+        w = Writer(16)
+        for k in range(5):
+            w.add(b"short%04d-%02d" % (i, k), make_trailer(5 + k, 1), bytes([i]) * 20000)
+        blocks.append(w.finish())
+    small = gen_row_blocks(9, 20, 32768, 16, 16, 100)
+    blocks += [bytes(small[0][o:o + l]) for o, l in zip(small[1], small[2])]
+    assert sum(len(b) > 32768 for b in blocks) >= 10
+    rng.shuffle(blocks)
+    check(*pack(blocks), 0, "big blocks, long keys", kern)
