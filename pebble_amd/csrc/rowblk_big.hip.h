@@ -161,19 +161,22 @@ __global__ void __launch_bounds__(kWave) big_block_sizes_kernel(Args A) {
 // the same stream (which resolved their bases into blk_*_base).  The walk is a
 // latency chain per block (an entry's header, its key bytes, its value), so
 // what pays is blocks in flight: tier 1 walks with a kBigKeySmall key buffer
-// (8 KiB of LDS: ~19 one-wave workgroups per CU, a workgroup per 16-block
+// (8 KiB of LDS: ~19 one-wave workgroups per CU, a workgroup per 8-block
 // window, every window's big blocks at once); a block with a longer key
 // (its sizes pass, with the full buffer, said OK) is listed in the workspace
 // (ids area, count at header word kWsBigRedo) and walked again by tier 2 with
 // the whole 32 KiB buffer, rewriting the same outputs.  8 value granules per
 // lane in flight.
 #ifndef PBL_BIG_WIN
-#define PBL_BIG_WIN 16  // blocks per tier-1 workgroup
+#define PBL_BIG_WIN 8  // blocks per tier-1 workgroup (config 5: 126 us at 8, 170 at 16)
 #endif
 #ifndef PBL_BIG_U
 #define PBL_BIG_U 8  // value granules per lane in flight (16: within noise on config 5)
 #endif
-constexpr uint32_t kBigKeySmall = 8192;
+#ifndef PBL_BIG_KEYBUF
+#define PBL_BIG_KEYBUF 8192
+#endif
+constexpr uint32_t kBigKeySmall = PBL_BIG_KEYBUF;
 constexpr int kWsBigRedo = 5;  // header u32 [5]: tier-2 blocks (their ids in the ids area)
 
 __device__ __forceinline__ void big_block_walk(const Args& A, uint32_t b, lptr<uint8_t> keybuf, uint32_t keycap,

@@ -389,7 +389,7 @@ uint64_t persistent_grid(hipStream_t st, PersistentKernel k, const void* fn, uin
 
 namespace {
 // The big row blocks' outputs (rowblk_big.hip.h): tier 1, a workgroup per
-// 16-block window, then tier 2 over the blocks tier 1 listed.
+// PBL_BIG_WIN-block window, then tier 2 over the blocks tier 1 listed.
 void launch_big_values(const pbl::Args& a, hipStream_t st, uint32_t small) {
   const uint32_t nb = a.in.n_blocks;
   const uint32_t g1 = (nb + PBL_BIG_WIN - 1) / PBL_BIG_WIN;
