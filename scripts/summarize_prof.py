@@ -56,12 +56,14 @@ if "FETCH_SIZE" in means and "WRITE_SIZE" in means:
     fetch = means["FETCH_SIZE"] * 2 * 1024
     write = means["WRITE_SIZE"] * 1024
     out["hbm_bytes_per_launch"] = fetch + write
-    base = "pmc_traffic" if WORKLOAD == "row" else f"pmc_traffic_{WORKLOAD.replace(':', '_ri')}"
+    base = ("pmc_traffic" if WORKLOAD == "row" else "pmc_traffic_zipf" if WORKLOAD == "zipf:col" else
+            f"pmc_traffic_{WORKLOAD.replace(':', '_ri')}")
     tname = base + (f"_hide{HIDE}" if HIDE else "") + ".json"
     json.dump({"kernel": KERNEL, "workload": WORKLOAD.split(":")[0], "workload_blocks": NB, "block_size": 32768,
                "lib_sha16": LIB_SHA, "hide": HIDE,
                "fetch_bytes_corrected": fetch, "write_bytes": write,
-               **({"restart_interval": int(WORKLOAD.split(":")[1]) if ":" in WORKLOAD else 16, "zipf_format": "row"}
+               **(({"restart_interval": 16, "zipf_format": "col"} if WORKLOAD == "zipf:col" else
+                   {"restart_interval": int(WORKLOAD.split(":")[1]) if ":" in WORKLOAD else 16, "zipf_format": "row"})
                   if WORKLOAD.startswith("zipf") else {}),
                "hbm_bytes_per_launch": fetch + write,
                "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes; FETCH_SIZE(KiB)x2x1024 "
