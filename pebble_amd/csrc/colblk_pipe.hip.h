@@ -63,7 +63,7 @@ struct CLds {
   uint32_t bad, nxt, st;
 };
 #ifndef PBL_COL_PIPE_WG
-#define PBL_COL_PIPE_WG 3  // workgroups per CU: 3 -> 168 VGPRs per lane (4 -> 128 spilled 160 B/lane to scratch: +0.8 GB of traffic per launch)
+#define PBL_COL_PIPE_WG 4  // workgroups per CU (128 VGPRs): config 3 1423 against 1257 at 3 (166 VGPRs); round 2's form spilled 160 B/lane at 4
 #endif
 static_assert(sizeof(CLds) <= 163840 / PBL_COL_PIPE_WG, "pipelined colblk workgroups per CU");
 
@@ -256,6 +256,9 @@ __device__ __forceinline__ void col_parse(CLds& L, Slot& P, const Slot& E, const
 #ifndef PBL_COL_VALU
 #define PBL_COL_VALU 4
 #endif
+#ifndef PBL_COL_VAL_EARLY
+#define PBL_COL_VAL_EARLY 0  // (its 16 VGPRs spill at 4 workgroups per CU)
+#endif
 constexpr int kValU = PBL_COL_VALU;
 struct ValStep {
   u32x4 x[kValU];
@@ -363,7 +366,13 @@ __device__ __forceinline__ void col_emit_rows(CLds& L, const Slot& E, const Args
     uint8_t* vout = O.val_bytes + vbb;
     if (n >= 16) {
       const uint32_t nch = (n + 15) >> 4;
-      val_step_store(vout, n, uint32_t(t), V0);
+      if (PBL_COL_VAL_EARLY) {
+        val_step_store(vout, n, uint32_t(t), V0);
+      } else {
+        ValStep V;
+        val_step_load(E, A, j0, n, uint32_t(t), V);
+        val_step_store(vout, n, uint32_t(t), V);
+      }
       for (uint32_t k0 = uint32_t(t) + kTPB * kValU; k0 < nch; k0 += kTPB * kValU) {
         ValStep V;
         val_step_load(E, A, j0, n, k0, V);
@@ -480,8 +489,8 @@ __device__ __forceinline__ void col_emit_t(CLds& L, const Slot& E, const Args& A
     col_emit_rows_hide<F>(L, E, A, schema, S);
     return;
   }
-  ValStep V0;  // the values' first step, in flight under the key build
-  val_step_load(E, A, E.d.v_data + E.d.v_lo, E.d.v_hi - E.d.v_lo, uint32_t(t), V0);
+  ValStep V0;  // the values' first step, in flight under the key build (PBL_COL_VAL_EARLY)
+  if (PBL_COL_VAL_EARLY) val_step_load(E, A, E.d.v_data + E.d.v_lo, E.d.v_hi - E.d.v_lo, uint32_t(t), V0);
   // keys of a single-chunk block are built in LDS first (one scan + one barrier)
   const uint32_t rows = E.d.rows;
   const bool prebuilt = rows <= kChunk && E.tot0 <= kKeyBuf;

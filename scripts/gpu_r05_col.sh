@@ -12,3 +12,6 @@ done
 if [ -n "$PARITY" ]; then
   PBL_LIB=exp/$PARITY.so timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_colblk_gpu.py tests/test_hide_fused_gpu.py tests/test_mixed_gpu.py tests/test_baseline_configs_gpu.py tests/test_zipf_gpu.py > $O/pytest.log 2>&1; tail -3 $O/pytest.log
 fi
+if [ -n "$MIXED" ]; then
+  for v in ${VARIANTS}; do L=""; [ $v != base ] && L=exp/$v.so; PBL_LIB=$L run ${v}_cfg4 --workload mixed; PBL_LIB=$L run ${v}_cfg5col --workload zipf --zipf-format col; done
+fi
