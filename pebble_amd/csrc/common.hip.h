@@ -54,7 +54,6 @@ __device__ __forceinline__ uint64_t with_seq(uint64_t tr, uint64_t seq, uint32_t
 }
 
 constexpr uint64_t kWsHeader = 256;
-constexpr int kWsBigCount = 1;  // header u32 [1]: blocks past the LDS stage (row pipeline)
 constexpr int kWsColTick = 2;   // header u32 [2]: the colblk queue's ticket counter (mixed batches)
 constexpr int kWsRowCount = 3;  // header u32 [3]: row-format blocks in a mixed batch
 constexpr uint32_t kSplitChunk = 4096;  // blocks per chunk of the mixed-batch split
@@ -85,9 +84,14 @@ constexpr uint64_t kStampWords = 0;
 __host__ __device__ inline uint64_t ws_ids_offset(uint32_t n_blocks) {
   return ws_bytes(n_blocks) + kStampWords * 8ull * n_blocks;
 }
-__host__ __device__ inline uint64_t ws_alloc_bytes(uint32_t n_blocks) {
+// Then the big row blocks' lists (rowblk_big.hip.h): the sizes pass's tier-2
+// list (count at header word 5); the blocks the row kernel's own walk left
+// (count at word 6), for the values pass.
+__host__ __device__ inline uint64_t ws_redo_offset(uint32_t n_blocks) {
   return ws_ids_offset(n_blocks) + 4ull * n_blocks + 4ull * (n_blocks / kSplitChunk + 1) + 8;
 }
+__host__ __device__ inline uint64_t ws_pend_offset(uint32_t n_blocks) { return ws_redo_offset(n_blocks) + 4ull * n_blocks; }
+__host__ __device__ inline uint64_t ws_alloc_bytes(uint32_t n_blocks) { return ws_pend_offset(n_blocks) + 4ull * n_blocks; }
 
 
 // Address-space-typed pointers.  A generic pointer compiles to FLAT

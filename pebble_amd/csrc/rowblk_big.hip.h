@@ -1,7 +1,8 @@
 // rowblk_big.hip.h — what every row kernel shares besides the walk: the entry
 // header decode, the Iter.Init checks, the diagnostic phase stamps, and the two
-// passes for blocks past the 32 KiB LDS stage (big_block_sizes_kernel before
-// the decode launch, big_block_values_kernel after it).
+// passes for blocks past the 32 KiB LDS stage (big_block_sizes_kernel /
+// big_block_sizes2_kernel before the decode launch, big_block_values_kernel
+// after it for what the row kernel left).
 //
 // Semantics: cockroachdb/pebble sstable/rowblk/rowblk_iter.go — Init :241-276,
 // readFirstKey :418-485, readEntry :333-416 (varints :345-398).
@@ -114,61 +115,8 @@ __device__ __forceinline__ uint32_t init_checks(const Rd& rd, uint32_t blen, uin
   return PBL_OK;
 }
 
-// Size pass for the blocks past the LDS stage (blen > kMaxFastLen), one wave
-// per block, launched ahead of rowblk_pipe_kernel on the same stream.  Their
-// count walk reads global memory entry by entry; inside the pipeline it would
-// hold back the look-back of every later ticket.  Here all of them walk at
-// once and publish their aggregates, so the pipeline's parse_slow only
-// resolves.  Same init checks and the same slow_walk as parse_slow, so the
-// aggregate is the one parse_slow computes.
-__global__ void __launch_bounds__(kWave) big_block_sizes_kernel(Args A) {
-  __shared__ uint4 keybuf4[kLdsBlkBytes / 16];
-  const uint32_t nb = A.in.n_blocks, flags = A.in.flags;
-  uint8_t* ws = reinterpret_cast<uint8_t*>(A.out.workspace);
-  uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
-  // 64 lengths per wave per round; the big blocks among them one after another
-  for (uint64_t base = uint64_t(blockIdx.x) * kWave; base < nb; base += uint64_t(gridDim.x) * kWave) {
-   const uint64_t bl = base + lane_id();
-   // (row blocks only: a mixed batch's colblk blocks are the colblk pipeline's)
-   uint64_t big = __ballot(bl < nb && to_glb(A.in.block_len)[bl] > kMaxFastLen &&
-                           (!A.in.block_format || to_glb(A.in.block_format)[bl] == PBL_FMT_ROW));
-   while (big) {
-    const uint32_t b = uint32_t(base) + uint32_t(__builtin_ctzll(big));
-    big &= big - 1;
-    const uint32_t blen = A.in.block_len[b];
-    const uint8_t* gblk = A.in.blocks + A.in.block_off[b];
-    uint32_t roff, nres;
-    if (init_checks(GlbRd{gblk}, blen, flags, &roff, &nres) != PBL_OK) continue;  // (parse_block's error path publishes)
-    SlowState ss;
-    uint64_t dummy[kNumComp] = {0, 0, 0, 0};
-    slow_walk(gblk, false, blen, flags, A.in.synthetic_seq_num, reinterpret_cast<uint8_t*>(keybuf4), uint32_t(kLdsBlkBytes), 0, A.out, b, dummy,
-              &ss);
-    const bool okk = ss.status == PBL_OK;
-    const uint64_t agg[kNumComp] = {okk ? ss.nkv : 0, okk ? ss.kb : 0, okk ? ss.vb : 0, okk ? ss.nr : 0};
-    lb_publish(lb_state, nb, b, agg);
-    if (lane_id() == 0) {  // for parse_slow (write_block_meta replaces them)
-      g_atomic_add(reinterpret_cast<uint32_t*>(ws) + kWsBigCount, 1u);
-      to_glb(A.out.blk_status)[b] = ss.status;
-      to_glb(A.out.blk_kv_base)[b] = agg[0];
-      to_glb(A.out.blk_key_base)[b] = agg[1];
-      to_glb(A.out.blk_val_base)[b] = agg[2];
-    }
-   }
-  }
-}
-
-// Outputs of the blocks past the LDS stage, launched after the row kernel on
-// the same stream (which resolved their bases into blk_*_base).  The walk is a
-// latency chain per block (an entry's header, its key bytes, its value), so
-// what pays is blocks in flight: tier 1 walks with a kBigKeySmall key buffer
-// (8 KiB of LDS: ~19 one-wave workgroups per CU, a workgroup per 8-block
-// window, every window's big blocks at once); a block with a longer key
-// (its sizes pass, with the full buffer, said OK) is listed in the workspace
-// (ids area, count at header word kWsBigRedo) and walked again by tier 2 with
-// the whole 32 KiB buffer, rewriting the same outputs.  8 value granules per
-// lane in flight.
 #ifndef PBL_BIG_WIN
-#define PBL_BIG_WIN 8  // blocks per tier-1 workgroup (config 5: 126 us at 8, 170 at 16)
+#define PBL_BIG_WIN 8  // blocks per sizes tier-1 workgroup (the values pass's form: 126 us at 8, 170 at 16)
 #endif
 #ifndef PBL_BIG_U
 #define PBL_BIG_U 8  // value granules per lane in flight (16: within noise on config 5)
@@ -176,52 +124,110 @@ __global__ void __launch_bounds__(kWave) big_block_sizes_kernel(Args A) {
 #ifndef PBL_BIG_KEYBUF
 #define PBL_BIG_KEYBUF 8192
 #endif
-constexpr uint32_t kBigKeySmall = PBL_BIG_KEYBUF;
-constexpr int kWsBigRedo = 5;  // header u32 [5]: tier-2 blocks (their ids in the ids area)
+constexpr uint32_t kBigKeySmall = PBL_BIG_KEYBUF;  // the sizes tier-1 key buffer
+constexpr int kWsBigRedo = 5;  // header u32 [5]: sizes tier-2 blocks (their ids in the redo area, ws_redo_offset)
+constexpr int kWsBigPend = 6;  // header u32 [6]: blocks the row kernel did not write (ids at ws_pend_offset)
 
-__device__ __forceinline__ void big_block_walk(const Args& A, uint32_t b, lptr<uint8_t> keybuf, uint32_t keycap,
-                                               SlowState* ss) {
-  const uint32_t blen = A.in.block_len[b];
-  const uint64_t bases[kNumComp] = {A.out.blk_kv_base[b], A.out.blk_key_base[b], A.out.blk_val_base[b],
-                                    A.out.blk_rst_base ? A.out.blk_rst_base[b] : 0};
-  slow_walk_t<SlowGlb, PBL_BIG_U>(SlowGlb{to_glb(A.in.blocks + A.in.block_off[b]), blen}, blen, A.in.flags,
-                                  A.in.synthetic_seq_num, keybuf, keycap, kPassAll, A.out, b, bases, ss);
+// Size pass for the blocks past the LDS stage (blen > kMaxFastLen), launched
+// ahead of the row kernel on the same stream.  Their count walk reads global
+// memory entry by entry; inside the pipeline it would hold back the look-back
+// of every later ticket.  Here all of them walk at once and publish their
+// aggregates, so the pipeline's parse_slow only resolves.  Same init checks and
+// the same slow walk as parse_slow, so the aggregate is the one parse_slow
+// computes.  Two tiers: tier 1 one one-wave
+// workgroup per PBL_BIG_WIN-block window with a kBigKeySmall key buffer; a
+// block whose walk needs more (PBL_UNSUPPORTED) is listed in the redo area and
+// walked by tier 2 with the whole 32 KiB buffer.  (Tier 1 was one workgroup per
+// 64 blocks, 4 per CU, with the 32 KiB buffer: config 5's 2195 big blocks took
+// 59 us, two to three serial walks per wave; 33 us in windows, 16 us without
+// one atomic per big block on a shared counter.)
+__device__ __forceinline__ void big_block_publish(const Args& A, uint32_t b, const SlowState& ss) {
+  const uint32_t nb = A.in.n_blocks;
+  uint64_t* lb_state = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(A.out.workspace) + kWsHeader);
+  const bool okk = ss.status == PBL_OK;
+  const uint64_t agg[kNumComp] = {okk ? ss.nkv : 0, okk ? ss.kb : 0, okk ? ss.vb : 0, okk ? ss.nr : 0};
+  lb_publish(lb_state, nb, b, agg);
+  if (lane_id() == 0) {  // for parse_slow (write_block_meta replaces them)
+    to_glb(A.out.blk_status)[b] = ss.status;
+    to_glb(A.out.blk_kv_base)[b] = agg[0];
+    to_glb(A.out.blk_key_base)[b] = agg[1];
+    to_glb(A.out.blk_val_base)[b] = agg[2];
+  }
 }
 
-__global__ void __launch_bounds__(kWave) big_block_values_kernel(Args A) {
+__device__ __forceinline__ bool big_block_count(const Args& A, uint32_t b, lptr<uint8_t> keybuf, uint32_t keycap,
+                                                SlowState* ss) {
+  const uint32_t blen = A.in.block_len[b];
+  const uint8_t* gblk = A.in.blocks + A.in.block_off[b];
+  uint32_t roff, nres;
+  if (init_checks(GlbRd{gblk}, blen, A.in.flags, &roff, &nres) != PBL_OK) return false;  // (parse_block's error path publishes)
+  const uint64_t dummy[kNumComp] = {0, 0, 0, 0};
+  slow_walk_t<SlowGlb, 1>(SlowGlb{to_glb(gblk), blen}, blen, A.in.flags, A.in.synthetic_seq_num, keybuf, keycap, kPassCount,
+                          A.out, b, dummy, ss);
+  return true;
+}
+
+__global__ void __launch_bounds__(kWave) big_block_sizes_kernel(Args A) {
   __shared__ uint4 keybuf4[kBigKeySmall / 16];
   const uint32_t nb = A.in.n_blocks;
   uint32_t* hdr = reinterpret_cast<uint32_t*>(A.out.workspace);
-  // (the size pass counted the big blocks; usually there are none)
-  if (__hip_atomic_load(to_glb(hdr) + kWsBigCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
-  uint32_t* redo = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(A.out.workspace) + ws_ids_offset(nb));
+  uint32_t* redo = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(A.out.workspace) + ws_redo_offset(nb));
   for (uint64_t base = uint64_t(blockIdx.x) * PBL_BIG_WIN; base < nb; base += uint64_t(gridDim.x) * PBL_BIG_WIN) {
     const uint64_t bl = base + lane_id();
+    // (row blocks only: a mixed batch's colblk blocks are the colblk pipeline's)
     uint64_t big = __ballot(lane_id() < PBL_BIG_WIN && bl < nb && to_glb(A.in.block_len)[bl] > kMaxFastLen &&
-                            (!A.in.block_format || to_glb(A.in.block_format)[bl] == PBL_FMT_ROW) &&
-                            to_glb(A.out.blk_status)[bl] == PBL_OK);
+                            (!A.in.block_format || to_glb(A.in.block_format)[bl] == PBL_FMT_ROW));
     while (big) {
       const uint32_t b = uint32_t(base) + uint32_t(__builtin_ctzll(big));
       big &= big - 1;
       SlowState ss;
-      big_block_walk(A, b, to_lds_ptr(reinterpret_cast<uint8_t*>(keybuf4)), kBigKeySmall, &ss);
-      // (the sizes pass walked it with the full buffer: a failure here is a key
-      // past the small one)
-      if (ss.status != PBL_OK && lane_id() == 0) to_glb(redo)[g_atomic_add(hdr + kWsBigRedo, 1u)] = b;
+      if (!big_block_count(A, b, to_lds_ptr(reinterpret_cast<uint8_t*>(keybuf4)), kBigKeySmall, &ss)) continue;
+      if (ss.status == PBL_UNSUPPORTED) {  // a key past the small buffer (or a total past 4 GiB): tier 2
+        if (lane_id() == 0) to_glb(redo)[g_atomic_add(hdr + kWsBigRedo, 1u)] = b;
+        continue;
+      }
+      big_block_publish(A, b, ss);
     }
   }
 }
 
-__global__ void __launch_bounds__(kWave) big_block_values2_kernel(Args A) {
+__global__ void __launch_bounds__(kWave) big_block_sizes2_kernel(Args A) {
   __shared__ uint4 keybuf4[kLdsBlkBytes / 16];
   const uint32_t nb = A.in.n_blocks;
-  uint32_t* hdr = reinterpret_cast<uint32_t*>(A.out.workspace);
+  const uint32_t* hdr = reinterpret_cast<const uint32_t*>(A.out.workspace);
   const uint32_t n = __hip_atomic_load(to_glb(hdr) + kWsBigRedo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t* redo = reinterpret_cast<const uint32_t*>(reinterpret_cast<uint8_t*>(A.out.workspace) +
-                                                           ws_ids_offset(nb));
+                                                           ws_redo_offset(nb));
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint32_t b = to_glb(redo)[i];
     SlowState ss;
-    big_block_walk(A, to_glb(redo)[i], to_lds_ptr(reinterpret_cast<uint8_t*>(keybuf4)), uint32_t(kLdsBlkBytes), &ss);
+    if (big_block_count(A, b, to_lds_ptr(reinterpret_cast<uint8_t*>(keybuf4)), uint32_t(kLdsBlkBytes), &ss))
+      big_block_publish(A, b, ss);
+  }
+}
+
+// Outputs of the blocks past the LDS stage.  The row kernel walks each one
+// itself once its look-back has resolved the block's bases (block_big in
+// rowblk_pool.hip.h: the wave's slot as the key buffer, the value copy hidden
+// behind the other waves' work); the blocks it could not (a key past the slot)
+// it lists, and this pass, launched after it on the same stream, walks them
+// with the whole 32 KiB key buffer.  8 value granules per lane in flight.
+__global__ void __launch_bounds__(kWave) big_block_values_kernel(Args A) {
+  __shared__ uint4 keybuf4[kLdsBlkBytes / 16];
+  const uint32_t nb = A.in.n_blocks;
+  const uint32_t* hdr = reinterpret_cast<const uint32_t*>(A.out.workspace);
+  const uint32_t n = __hip_atomic_load(to_glb(hdr) + kWsBigPend, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t* pend = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(A.out.workspace) +
+                                                           ws_pend_offset(nb));
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint32_t b = to_glb(pend)[i];
+    const uint32_t blen = A.in.block_len[b];
+    const uint64_t bases[kNumComp] = {A.out.blk_kv_base[b], A.out.blk_key_base[b], A.out.blk_val_base[b],
+                                      A.out.blk_rst_base ? A.out.blk_rst_base[b] : 0};
+    SlowState ss;
+    slow_walk_t<SlowGlb, PBL_BIG_U>(SlowGlb{to_glb(A.in.blocks + A.in.block_off[b]), blen}, blen, A.in.flags,
+                                    A.in.synthetic_seq_num, to_lds_ptr(reinterpret_cast<uint8_t*>(keybuf4)),
+                                    uint32_t(kLdsBlkBytes), kPassAll, A.out, b, bases, &ss);
   }
 }
 

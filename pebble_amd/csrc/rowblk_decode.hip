@@ -388,13 +388,17 @@ uint64_t persistent_grid(hipStream_t st, PersistentKernel k, const void* fn, uin
 }  // namespace pbl
 
 namespace {
-// The big row blocks' outputs (rowblk_big.hip.h): tier 1, a workgroup per
-// PBL_BIG_WIN-block window, then tier 2 over the blocks tier 1 listed.
+// The big row blocks' passes (rowblk_big.hip.h): sizes before the row kernel
+// (tier 1 a workgroup per PBL_BIG_WIN-block window, tier 2 over the blocks it
+// listed); after it, the outputs of the blocks the row kernel did not write.
+void launch_big_sizes(const pbl::Args& a, hipStream_t st, uint32_t small) {
+  const uint32_t g1 = (a.in.n_blocks + PBL_BIG_WIN - 1) / PBL_BIG_WIN;
+  hipLaunchKernelGGL(pbl::row::rowc::big_block_sizes_kernel, dim3(g1), dim3(pbl::kWave), 0, st, a);
+  hipLaunchKernelGGL(pbl::row::rowc::big_block_sizes2_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+}
+
 void launch_big_values(const pbl::Args& a, hipStream_t st, uint32_t small) {
-  const uint32_t nb = a.in.n_blocks;
-  const uint32_t g1 = (nb + PBL_BIG_WIN - 1) / PBL_BIG_WIN;
-  hipLaunchKernelGGL(pbl::row::rowc::big_block_values_kernel, dim3(g1), dim3(pbl::kWave), 0, st, a);
-  hipLaunchKernelGGL(pbl::row::rowc::big_block_values2_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+  hipLaunchKernelGGL(pbl::row::rowc::big_block_values_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
 }
 
 // Row batches on the staging-pool kernel (rowblk_pool.hip.h), with the same
@@ -410,7 +414,7 @@ int launch_row_pool(const pbl::Args& a, hipStream_t st, bool values) {
                                              pbl::row::pool::kTPBP);
   if (!grid) return PBL_DEVICE_ERROR;
   const uint32_t small = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4));
-  hipLaunchKernelGGL(pbl::row::rowc::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+  launch_big_sizes(a, st, small);
   if (hide)
     hipLaunchKernelGGL(pbl::row::pool::rowblk_pool_kernel<true>, dim3(uint32_t(grid)), dim3(pbl::row::pool::kTPBP), 0,
                        st, a, static_cast<const uint32_t*>(nullptr));
@@ -445,7 +449,7 @@ int launch_mixed(const pbl_block_batch* batch, const pbl::Args& a, hipStream_t s
   const uint32_t g_cs = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 32));
   const uint32_t small = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4));
   const uint32_t* cids = static_cast<const uint32_t*>(ids);
-  hipLaunchKernelGGL(pbl::row::rowc::big_block_sizes_kernel, dim3(small), dim3(pbl::kWave), 0, st, a);
+  launch_big_sizes(a, st, small);
   if (hide)
     hipLaunchKernelGGL(pbl::row::mixed_col_size_kernel<true>, dim3(g_cs), dim3(pbl::kWave), 0, st, a, cids);
   else

@@ -63,6 +63,34 @@ struct SlowGlb {  // block in global memory
     }
     return sh ? col::funnel16(x, y, sh) : x;
   }
+  // Block bytes from offset v -> out[lo, hi), 16-B destination granules, U per
+  // lane in flight.  Every granule's two source loads are issued before any is
+  // used, at addresses clamped to the block's own granules (those bytes feed
+  // only masked destination bytes); the shift is one per value.  Through ld16
+  // each granule's guarded loads and funnel waited in turn: config 5's
+  // big-block values pass, one 48 KB value per block, took 125 us.
+  template <int U>
+  __device__ __forceinline__ void copy(uint64_t v, uint8_t* out, uint64_t lo, uint64_t hi) const {
+    const uint64_t s0 = uint64_t(g), g_lo = s0 & ~uint64_t(15), g_hi = (s0 + len - 1) & ~uint64_t(15);
+    const uint64_t d = s0 + v - lo;  // source address of destination offset ga: d + ga
+    const uint32_t sh = __builtin_amdgcn_readfirstlane(uint32_t(d) & 15u);
+    for (uint64_t g0 = (lo & ~uint64_t(15)) + 16ull * lane_id(); g0 < hi; g0 += 16ull * kWave * U) {
+      u32x4 x[U], y[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t sa = (d + g0 + 16ull * kWave * u) & ~uint64_t(15);
+        x[u] = *(gptr<const u32x4>)(min(max(sa, g_lo), g_hi));
+        if (sh) y[u] = *(gptr<const u32x4>)(min(max(sa + 16, g_lo), g_hi));
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t ga = g0 + 16ull * kWave * u;
+        const uint4 a = make_uint4(x[u].x, x[u].y, x[u].z, x[u].w);
+        if (ga < hi)
+          store16(out, ga, lo, hi, sh ? col::funnel16(a, make_uint4(y[u].x, y[u].y, y[u].z, y[u].w), sh) : a);
+      }
+    }
+  }
 };
 
 // byte k (< 16) of a 16-byte window, by shifts (a runtime-indexed register
@@ -212,17 +240,21 @@ __device__ __forceinline__ void slow_walk_t(const Src S, uint64_t len, uint32_t 
     if (pass == kPassAll) {
       // value: 16-B destination granules from source windows, U per lane in flight
       const uint64_t lo = bases[2] + vb, hi = lo + vl;
-      for (uint64_t g0 = (lo & ~uint64_t(15)) + 16ull * l; g0 < hi; g0 += 16ull * kWave * U) {
-        uint4 w[U];
+      if constexpr (std::is_same<Src, SlowGlb>::value) {
+        S.template copy<U>(v, O.val_bytes, lo, hi);
+      } else {
+        for (uint64_t g0 = (lo & ~uint64_t(15)) + 16ull * l; g0 < hi; g0 += 16ull * kWave * U) {
+          uint4 w[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-          const uint64_t ga = g0 + 16ull * kWave * u;
-          w[u] = ga < hi ? S.ld16(int64_t(v) + int64_t(ga - lo)) : make_uint4(0, 0, 0, 0);
-        }
+          for (int u = 0; u < U; u++) {
+            const uint64_t ga = g0 + 16ull * kWave * u;
+            w[u] = ga < hi ? S.ld16(int64_t(v) + int64_t(ga - lo)) : make_uint4(0, 0, 0, 0);
+          }
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-          const uint64_t ga = g0 + 16ull * kWave * u;
-          if (ga < hi) store16(O.val_bytes, ga, lo, hi, w[u]);
+          for (int u = 0; u < U; u++) {
+            const uint64_t ga = g0 + 16ull * kWave * u;
+            if (ga < hi) store16(O.val_bytes, ga, lo, hi, w[u]);
+          }
         }
       }
     }

@@ -928,9 +928,13 @@ __device__ __noinline__ void block_slow(Stage& S, uint8_t* keybuf, uint32_t keyc
 }
 
 // A block past the stage: big_block_sizes_kernel walked it, published its
-// aggregate and left {status, counts} in its block-metadata slots;
-// big_block_values_kernel writes its outputs after this launch.  Out of line.
-__device__ __noinline__ void block_big(const Args A, uint32_t b, uint64_t boff, uint32_t blen) {
+// aggregate and left {status, counts} in its block-metadata slots.  Once its
+// bases resolve, the wave walks it from global memory and writes its outputs,
+// its slot as the key buffer; a key past the slot lists the block for
+// big_block_values_kernel (after this launch).  (Config 5: 2195 big blocks,
+// one 48 KB value each; the separate values pass took 87 us.)  Out of line.
+__device__ __noinline__ void block_big(const Args A, uint32_t b, uint64_t boff, uint32_t blen, uint8_t* keybuf,
+                                       uint32_t keycap) {
   const int l = lane_id();
   const uint32_t nb = A.in.n_blocks;
   const pbl_decode_out& O = A.out;
@@ -950,6 +954,16 @@ __device__ __noinline__ void block_big(const Args A, uint32_t b, uint64_t boff, 
       to_glb(O.val_off)[excl[0] + b] = 0;
     }
     write_block_meta(O, b, nb, st2, excl, agg, true);
+  }
+  if (st2 == PBL_OK) {
+    SlowState ss;
+    slow_walk_t<SlowGlb, PBL_BIG_U>(SlowGlb{to_glb(A.in.blocks + boff), blen}, blen, A.in.flags,
+                                    A.in.synthetic_seq_num, to_lds_ptr(keybuf), keycap, kPassAll, O, b, excl, &ss);
+    if (ss.status != PBL_OK && l == 0) {
+      uint32_t* hdr = reinterpret_cast<uint32_t*>(O.workspace);
+      uint32_t* pend = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(O.workspace) + ws_pend_offset(nb));
+      to_glb(pend)[g_atomic_add(hdr + rowc::kWsBigPend, 1u)] = b;
+    }
   }
 }
 
@@ -983,7 +997,7 @@ __device__ __forceinline__ Pend block_front(PoolLds<kHide>& L, uint32_t s, uint3
 
   if (blen > kMaxFastLen) {
     release(L, s);
-    block_big(A, b, boff, blen);
+    block_big(A, b, boff, blen, reinterpret_cast<uint8_t*>(&W), uint32_t(sizeof(W)));
     return P;
   }
   PSTAMP(A, b, 1, l == 0);

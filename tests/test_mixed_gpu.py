@@ -93,6 +93,29 @@ def test_mixed_big_and_corrupt_blocks(kernel):
     assert g["n_bad_blocks"] >= 1
 
 
+
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_mixed_big_blocks_with_long_keys(kernel):
+    """Big row blocks whose keys outgrow the big-block passes' 8 KiB key buffer
+    in a mixed batch: the sizes pass lists them for its second tier (the redo
+    list has its own workspace area, past the format split's ids, which the
+    row and colblk kernels read after it)."""
+    from pebble_amd.rowblk import Writer, make_trailer
+    rng = random.Random(78)
+    rows, cols = pool(8, 12, 12)
+    big = []
+    for i in range(4):
+        w = Writer(rng.choice([1, 16]))
+        base = bytes(rng.randrange(256) for _ in range(rng.choice([9000, 20000])))
+        for k in range(6):
+            w.add(base + b"%08d" % (100 * i + k), make_trailer(10 + k, 1), bytes([k]) * rng.choice([100, 30000]))
+        big.append(w.finish())
+    assert all(len(b) > 32768 for b in big)
+    R, C = N.PBL_FMT_ROW, N.PBL_FMT_COL_CRDB1
+    blocks = rows[:6] + [big[0]] + cols[:6] + [big[1], big[2]] + rows[6:] + cols[6:] + [big[3]]
+    fmts = [R] * 6 + [R] + [C] * 6 + [R, R] + [R] * 6 + [C] * 6 + [R]
+    check(blocks, fmts, kernel, 8, "big long keys")
+
 def test_mixed_overflow_retry_and_size_pass():
     from pebble_amd.batch import Capacity
     rows, cols = pool(8, 20, 20)

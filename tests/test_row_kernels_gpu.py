@@ -104,10 +104,11 @@ def test_row_shape_mixes(mix, kern):
 
 
 def test_big_blocks_with_long_keys(kern):
-    """Blocks past the 32 KiB stage whose keys outgrow the big-block pass's
-    8 KiB key buffer (tier 1 lists them, tier 2 walks them again with the whole
-    buffer), next to big blocks with short keys, shared prefixes reaching deep
-    into the long keys, and ordinary blocks."""
+    """Blocks past the 32 KiB stage whose keys outgrow the 8 KiB key buffers
+    of the sizes pass's tier 1 and of the row kernel's own walk (the sizes tier
+    2 and the values pass take them, with the whole 32 KiB buffer), next to big
+    blocks with short keys, shared prefixes reaching deep into the long keys,
+    and ordinary blocks."""
     from rowutil import make_trailer
     rng = random.Random(77)
     blocks = []
@@ -128,3 +129,22 @@ def test_big_blocks_with_long_keys(kern):
     assert sum(len(b) > 32768 for b in blocks) >= 10
     rng.shuffle(blocks)
     check(*pack(blocks), 0, "big blocks, long keys", kern)
+
+
+def test_big_blocks_with_keys_near_the_slot():
+    """Big blocks whose keys sit around the row kernel's slot and the sizes
+    pass's 8 KiB buffer: some walked by the row kernel itself, some listed for
+    the values pass, some for the sizes pass's second tier."""
+    from rowutil import make_trailer
+    rng = random.Random(79)
+    blocks = []
+    for i, kl in enumerate([3000, 5000, 6500, 7000, 7500, 7900, 8100, 8150, 8300]):
+        w = Writer(rng.choice([1, 16]))
+        base = bytes(rng.randrange(256) for _ in range(kl - 16))
+        for k in range(3):
+            w.add(base + b"%08d" % (10 * i + k), make_trailer(7 + k, 1), bytes([k + i]) * rng.choice([50, 30000]))
+        blocks.append(w.finish())
+    small = gen_row_blocks(10, 12, 32768, 16, 16, 100)
+    blocks += [bytes(small[0][o:o + l]) for o, l in zip(small[1], small[2])]
+    rng.shuffle(blocks)
+    check(*pack(blocks), 0, "big blocks, keys near the slot")
