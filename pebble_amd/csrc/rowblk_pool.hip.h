@@ -699,6 +699,10 @@ constexpr int kVG = PBL_POOL_VG;
 #define PBL_POOL_WAVEVAL 1024
 #endif
 constexpr uint32_t kWaveVal = PBL_POOL_WAVEVAL;
+#ifndef PBL_POOL_MEDU
+#define PBL_POOL_MEDU 4
+#endif
+constexpr int kMedU = PBL_POOL_MEDU;  // chunks per lane in flight for values of 129 B .. kWaveVal
 // One step of the value copy: kVG KVs per 8-lane group, j = j0 + 8 u + lane / 8.
 // Only the loaded chunks are held between a step's loads and its stores (the
 // offsets are re-read from the slot).
@@ -742,16 +746,16 @@ __device__ __forceinline__ void val_store(const uint32_t* vp, uint32_t nkv, uint
     const VSeg S = val_seg(vp, nkv, jl + 8 * u);
     if (S.has) st_out((gptr<u32x4_ug>)(vbytes + S.vo + S.q), u32x4_ug(B.x[u]));
     if (S.vl > 128 && S.vl <= kWaveVal) {
-      // the value's further chunks, four per lane in flight
-      for (uint32_t o0 = 16 * c + 128; o0 < S.vl; o0 += 512) {
-        u32x4 y[4];
+      // the value's further chunks, kMedU per lane in flight
+      for (uint32_t o0 = 16 * c + 128; o0 < S.vl; o0 += 128 * kMedU) {
+        u32x4 y[kMedU];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < kMedU; k++) {
           const uint32_t o = o0 + 128 * k, q = o < S.vl - 16 ? o : S.vl - 16;
           if (o < S.vl) y[k] = *(gptr<const u32x4_ug>)(g + S.vs + q);
         }
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < kMedU; k++) {
           const uint32_t o = o0 + 128 * k, q = o < S.vl - 16 ? o : S.vl - 16;
           if (o < S.vl) st_out((gptr<u32x4_ug>)(vbytes + S.vo + q), u32x4_ug(y[k]));
         }
@@ -814,8 +818,12 @@ __device__ __forceinline__ void copy_values_grp(const uint32_t* vp, gptr<const u
   copy_long_values(vp, g, nkv, vbytes);
 }
 
-// Values longer than kWaveVal: the whole wave, four 16-B chunks per lane in
+// Values longer than kWaveVal: the whole wave, kLongU 16-B chunks per lane in
 // flight.
+#ifndef PBL_POOL_LONGU
+#define PBL_POOL_LONGU 8  // config 5 RI 16: 889 / 905 / 874 GiB/s at 4 / 8 / 16
+#endif
+constexpr int kLongU = PBL_POOL_LONGU;
 __device__ __forceinline__ void copy_long_values(const uint32_t* vp, gptr<const uint8_t> g, uint32_t nkv,
                                                  gptr<uint8_t> vbytes) {
   const int l = lane_id();
@@ -826,15 +834,15 @@ __device__ __forceinline__ void copy_long_values(const uint32_t* vp, gptr<const 
     for (uint64_t lm = __ballot(j < nkv && len > kWaveVal); lm; lm &= lm - 1) {
       const int sl = __builtin_ctzll(lm);
       const uint32_t ls = __shfl(a >> 16, sl, kWave), ll = __shfl(len, sl, kWave), lo = __shfl(a & 0xffffu, sl, kWave);
-      for (uint32_t o0 = 16u * l; o0 < ll; o0 += 64u * kWave) {
-        u32x4 y[4];
+      for (uint32_t o0 = 16u * l; o0 < ll; o0 += 16u * kLongU * kWave) {
+        u32x4 y[kLongU];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < kLongU; k++) {
           const uint32_t o = o0 + 16u * kWave * k, q = o < ll - 16 ? o : ll - 16;
           y[k] = *(gptr<const u32x4_ug>)(g + ls + (o < ll ? q : 0u));
         }
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < kLongU; k++) {
           const uint32_t o = o0 + 16u * kWave * k, q = o < ll - 16 ? o : ll - 16;
           if (o < ll) st_out((gptr<u32x4_ug>)(vbytes + lo + q), u32x4_ug(y[k]));
         }
