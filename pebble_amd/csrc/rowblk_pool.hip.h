@@ -1,13 +1,11 @@
 // rowblk_pool.hip.h — the row-format decode with one wave per block, eight
-// waves per CU, a shared pool of LDS staging buffers, and two blocks in flight
-// per wave.
+// waves per CU and a shared pool of LDS staging buffers.
 //
 // Only the parse needs a block's bytes in LDS; the keys and the value bytes
 // (80 % of the output) are gathered global->global from the block that was
 // just read (L2 / MALL-hot) through compact per-KV metadata in the wave's own
-// slot.  So a 32 KiB stage is held only for the DMA and the walk, and a wave
-// carries two blocks: while block i's look-back resolves, the wave stages and
-// walks block i+1 into its other slot, then emits block i.
+// slot.  So a 32 KiB stage is held only for the DMA, the walk and the
+// metadata pass, and the other waves stage their blocks while this one emits.
 //
 //   acquire   a wave takes a free stage from the workgroup's pool (LDS mask),
 //             THEN a ticket (the only order that keeps the look-back
@@ -20,10 +18,8 @@
 //   meta      per-entry metadata words (key source, shared and key length,
 //             prefix parent, header length, flags) and per-KV value offsets
 //             written from the registers into the slot; the stage is released
-//   -- the wave stages, walks and publishes its NEXT block here --
-//   resolve   the exclusive prefix (one round trip: every predecessor has long
-//             published), issued together with the first step's and the
-//             restart words' loads
+//   resolve   the exclusive prefix by decoupled look-back, issued together
+//             with the first step's and the restart words' loads
 //   steps     64 KVs per step, keys and values together (a line of the block
 //             is fetched once for both), each step's loads issued before the
 //             previous step's stores:
@@ -32,13 +28,14 @@
 //                       its prefix chain
 //               values  8 lanes per KV, 16-B chunks
 //
-// LDS per CU: 3 stages x 32.8 KB + 16 slots x ~4 KB (8 waves x 2 blocks).
+// LDS per CU: 3 stages x 32.8 KB + 8 slots x ~8 KB (one per wave).
 //
 // Blocks outside the fast-path limits (more entries than a slot holds, keys
 // past kMaxKl, 3-byte header varints, ...) take the wave-serial general walk
 // (rowblk_general.hip.h) on the staged bytes; blocks past kMaxFastLen are sized
-// and written by big_block_{sizes,values}_kernel around this launch.  Results
-// are identical on every path.
+// by big_block_sizes_kernel before this launch and written by the wave that
+// draws their ticket (block_big; rowblk_big.hip.h).  Results are identical on
+// every path.
 //
 // Semantics: cockroachdb/pebble sstable/rowblk/rowblk_iter.go — Init :241-276,
 // readFirstKey :418-485, readEntry :333-416, decodeInternalKey :487-504, value
@@ -54,9 +51,6 @@ namespace pool {
 #ifndef PBL_POOL_STAGES
 #define PBL_POOL_STAGES 3
 #endif
-#ifndef PBL_POOL_DEPTH
-#define PBL_POOL_DEPTH 1  // blocks in flight per wave (slots per wave): 1 or 2
-#endif
 #ifndef PBL_POOL_SLEEP
 #define PBL_POOL_SLEEP 8  // s_sleep units (64 cycles) between polls of the stage mask
 #endif
@@ -65,8 +59,6 @@ namespace pool {
 #endif
 constexpr int kNW = PBL_POOL_WAVES;      // waves per workgroup (one workgroup per CU)
 constexpr int kNS = PBL_POOL_STAGES;     // staging buffers per workgroup
-constexpr int kDepth = PBL_POOL_DEPTH;
-static_assert(kDepth == 1 || kDepth == 2, "one or two blocks in flight per wave");
 constexpr int kTPBP = kNW * kWave;
 constexpr uint32_t kMaxKl = 4095;        // internal-key bytes per entry on the fast path
 
@@ -95,7 +87,7 @@ __device__ __forceinline__ uint64_t m_pack(uint32_t ksrc, uint32_t sh, uint32_t 
 // visible KV (HideObsoletePoints drops obsolete entries from the outputs, never
 // from the chain; without hiding the two indices agree).  Entries per slot:
 // what the LDS left after the stages holds, at most 511 (the parent field).
-constexpr int kPerSlot = (163840 - kNS * int(sizeof(Stage)) - 256) / (kNW * kDepth);
+constexpr int kPerSlot = (163840 - kNS * int(sizeof(Stage)) - 256) / kNW;
 template <bool kHide>
 constexpr int slot_kv() {
   const int n = ((kPerSlot - 32) / (kHide ? 14 : 12)) & ~7;
@@ -113,7 +105,7 @@ struct Slot {
 template <bool kHide>
 struct PoolLds {
   Stage st[kNS];
-  Slot<kHide> sl[kNW * kDepth];
+  Slot<kHide> sl[kNW];
   uint32_t free_mask;  // bit s: stage s is free
 };
 static_assert(sizeof(PoolLds<true>) <= 163840 && sizeof(PoolLds<false>) <= 163840, "one pool workgroup per CU");
@@ -1211,14 +1203,11 @@ __global__ void __launch_bounds__(kTPBP, 1) rowblk_pool_kernel(Args A, const uin
   __shared__ PoolLds<kHide> L;
   if (threadIdx.x == 0) L.free_mask = (1u << kNS) - 1u;
   __syncthreads();
-  Slot<kHide>* W = L.sl + kDepth * wave_id();
+  Slot<kHide>& W = L.sl[wave_id()];
   const uint32_t nb = A.in.n_blocks;
   uint32_t* tick = reinterpret_cast<uint32_t*>(A.out.workspace);
   const uint32_t nt = ids ? __hip_atomic_load(to_glb(tick) + kWsRowCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                           : nb;
-  Pend P;
-  P.live = false;
-  uint32_t cur = 0;
   for (;;) {
 #ifdef PBL_STAMPS
     const uint64_t t_acq = __builtin_amdgcn_s_memtime();
@@ -1239,17 +1228,10 @@ __global__ void __launch_bounds__(kTPBP, 1) rowblk_pool_kernel(Args A, const uin
 #endif
     const uint64_t boff = to_glb(A.in.block_off)[t0];
     const uint32_t blen = to_glb(A.in.block_len)[t0];
-    const Pend Q = block_front<kHide>(L, s, t0, boff, blen, W[cur], A);
-    if (kDepth == 1) {
-      if (Q.live) block_emit<kHide>(Q, W[0], A);
-    } else {
-      if (P.live) block_emit<kHide>(P, W[cur ^ 1], A);
-      P = Q;
-      cur ^= 1;
-    }
+    const Pend Q = block_front<kHide>(L, s, t0, boff, blen, W, A);
+    if (Q.live) block_emit<kHide>(Q, W, A);
     wave_sync();  // (the slot is the next block's)
   }
-  if (kDepth == 2 && P.live) block_emit<kHide>(P, W[cur ^ 1], A);
 }
 
 }  // namespace pool
