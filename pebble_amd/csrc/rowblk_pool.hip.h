@@ -189,7 +189,10 @@ __device__ __forceinline__ uint4 gld16(gptr<const uint8_t> g, int32_t i, uint32_
 struct PAcc {
   uint32_t ne, cnt, kb, vb;  // entries, visible KVs, their user-key / value bytes
 };
-constexpr int kRunBuf = 16;
+#ifndef PBL_POOL_RUNBUF
+#define PBL_POOL_RUNBUF 16  // entries of a run parked in registers by its walk
+#endif
+constexpr int kRunBuf = PBL_POOL_RUNBUF;
 // One run's head, parked in registers by the walk for the metadata pass.
 struct PRun {
   uint32_t ea[kRunBuf];  // entry offset | hidden << 15 | shared << 16 | SET-with-value-prefix << 31
