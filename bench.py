@@ -66,6 +66,9 @@ def parse():
     p.add_argument("--hide", type=int, default=0,
                    help="HideObsoletePoints fused (PBL_ROW_HIDE_OBSOLETE) on row / col batches whose every N-th "
                         "KV per block is an obsolete point (0: off)"),
+    p.add_argument("--tiering", type=int, default=0,
+                   help="col workload: Pebblev8 blocks with the tiering columns (span ids 1..N), decoded with "
+                        "PBL_COL_TIERING into the per-KV KVMeta arrays (0: off)")
     p.add_argument("--zipf-format", choices=["row", "col"], default="row",
                    help="config 5 block format (col = colblk DefaultKeySchema)")
     p.add_argument("--seed", type=int, default=42)
@@ -144,6 +147,7 @@ def alg_bytes(h: dict, nb: int, input_bytes: int) -> int:
     byte read once plus every output byte written once."""
     n = h["n_kv"]
     out = (8 * n            # trailer
+           + (16 * n if "tiering_span_id" in h else 0)  # KVMeta (span, attribute)
            + n              # kv_flags
            + 4 * n          # entry_off
            + 2 * 4 * (n + nb)  # key_off, val_off (N+1 per block)
@@ -261,6 +265,10 @@ def main():
     flags = N.PBL_ROW_VALUE_PREFIX if a.value_prefix else 0
     if a.hide:
         flags |= N.PBL_ROW_HIDE_OBSOLETE
+    meta = a.tiering > 0
+    if meta:
+        assert a.workload == "col", "--tiering applies to the col workload"
+        flags |= N.PBL_COL_TIERING
     flags |= {"auto": 0, "single": N.PBL_KERNEL_SINGLE, "pipe": N.PBL_KERNEL_PIPE, "pool": N.PBL_KERNEL_POOL}[a.kernel]
     row_kernel = "rowblk_pool_kernel"
     seed = a.seed + 7919 * rank
@@ -287,11 +295,13 @@ def main():
                "every 8th a short table-tail block (2 / 4 / 8 KiB)"))
     elif a.workload == "col":
         fmt = N.PBL_FMT_COL_CRDB1
-        buf, off, lens, n_kv = gen_col_blocks(seed, nb, a.block_size, n_threads=16, obsolete_every=a.hide)
+        buf, off, lens, n_kv = gen_col_blocks(seed, nb, a.block_size, n_threads=16, obsolete_every=a.hide,
+                                              tiering=a.tiering)
         kernel = "colblk_decode_kernel" if a.kernel == "single" and not a.hide else "colblk_pipe_kernel"
         wl = (f"config3: {nb} x {a.block_size // 1024} KiB colblk blocks per GPU, cockroachkvs crdb1 schema "
               f"(KeyGenConfig alphabet 26, RoachKeyLen 12, PrefixLenShared 4, 1 key/prefix), 128 B values"
-              + (f", every {a.hide}th row isObsolete, HideObsoletePoints fused" if a.hide else ""))
+              + (f", every {a.hide}th row isObsolete, HideObsoletePoints fused" if a.hide else "")
+              + (f", Pebblev8 tiering columns (span ids 1..{a.tiering}) decoded to per-KV KVMeta" if meta else ""))
     elif a.workload == "zipf":
         from pebble_amd.batch import gen_zipf_blocks
         fmt = N.PBL_FMT_ROW if a.zipf_format == "row" else N.PBL_FMT_COL_DEFAULT
@@ -334,7 +344,7 @@ def main():
     batch = BlockBatch.from_host(buf, off, lens, dev, fmt, flags, block_format=block_fmt)
 
     # size the outputs exactly with one decode, then reuse them every step
-    first = decode(batch)
+    first = decode(batch, meta=meta)
     h = first.to_host()
     if a.hide:  # the visible KVs only: fewer than were written
         assert 0 < h["n_kv"] < n_kv and h["status_mask"] == 0, (h["n_kv"], n_kv, h["status_mask"])
@@ -352,7 +362,7 @@ def main():
         h_in = h
     else:
         del first
-        out = DecodedBatch.allocate(nb, cap, dev)
+        out = DecodedBatch.allocate(nb, cap, dev, meta=meta)
     del h
     gathered = torch.zeros(world * 4, dtype=torch.int64, device=dev) if world > 1 else None
     if world > 1 and a.dist_backend == "gloo":  # (gloo gathers host tensors)
@@ -418,7 +428,8 @@ def main():
     tname = ("pmc_traffic" if a.workload == "row" and a.kernel == "auto" else
              f"pmc_traffic_{a.kernel}" if a.workload == "row" else
              f"pmc_traffic_zipf_ri{a.restart_interval}" if a.workload == "zipf" and a.zipf_format == "row" else
-             f"pmc_traffic_{a.workload}") + (f"_hide{a.hide}" if a.hide else "") + ".json"
+             f"pmc_traffic_{a.workload}") + (f"_hide{a.hide}" if a.hide else "") + (
+             f"_tier{a.tiering}" if a.tiering else "") + ".json"
     tp = os.path.join(ROOT, "profiles", tname)
     if os.path.exists(tp):
         try:
@@ -457,7 +468,8 @@ def main():
     if not a.no_e2e and rank == 0 and plan is None:
         del out  # (HBM for the pipeline's slots)
         torch.cuda.empty_cache()
-        res["e2e_pcie"] = e2e_rate(buf, off, lens, flags & ~N.PBL_BATCH_VARLEN, dev, cap, fmt, block_fmt, hres,
+        res["e2e_pcie"] = e2e_rate(buf, off, lens, flags & ~(N.PBL_BATCH_VARLEN | N.PBL_COL_TIERING), dev, cap, fmt,
+                                   block_fmt, hres,
                                    chunk=a.e2e_chunk)
 
     res["gen_seconds"] = round(gen_s, 2)

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define PBL_ABI_VERSION 7
+#define PBL_ABI_VERSION 8
 
 /* ---- status codes (per block, and OR-ed as bit masks into totals) ---------- */
 enum {
@@ -89,6 +89,25 @@ enum {
                                      and mixed (block_format) batches alike.  (The
                                      name is historical: it applies to colblk
                                      blocks too.)                                   */
+#define PBL_COL_TIERING 0x10u     /* colblk blocks carry the Pebblev8 tiering columns
+                                     (TableFormat.TieringColumnConfig, sstable/format.go:
+                                     305-316: WithTieringColumns, data_block.go:594-601):
+                                     the data columns tieringSpanID (Uint), tieringAttribute
+                                     (Uint) and secondaryBlobHandle (RawBytes) follow
+                                     isObsolete (data_block.go:514-525).  With it, every
+                                     colblk KV's KVMeta -- what DataBlockIter.FirstWithMeta
+                                     / NextWithMeta / SeekGEWithMeta return
+                                     (data_block.go:1574-1641) -- is written to
+                                     pbl_decode_out.tiering_span_id / tiering_attr when
+                                     those are non-NULL, and the two Uint columns are
+                                     decoded with DecodeColumn's checks (a block missing
+                                     them, or failing them, is PBL_CORRUPT_COLBLK_HEADER:
+                                     the reference panics in initTieringMetadata).
+                                     Without it the meta arrays, when given, receive
+                                     zeros (KVMeta{}: !SupportsTiering).  Row blocks
+                                     always give zeros (rowblk.Iter has no meta columns;
+                                     NextWithMeta on the row iterator returns KVMeta{}).
+                                     Keys and values decode identically either way.   */
 #define PBL_BATCH_VARLEN 0x100u   /* scheduling hint, no effect on results: block
                                      lengths vary widely (e.g. Zipf value sizes), so a
                                      colblk batch takes the one-block-per-workgroup
@@ -189,6 +208,9 @@ typedef struct pbl_decode_out {
   uint64_t kv_cap, key_cap, val_cap, rst_cap;
   void* workspace;        /* device scratch of pbl_workspace_bytes(n_blocks) bytes */
   uint64_t workspace_bytes;
+  uint64_t* tiering_span_id; /* [kv_cap] (optional) base.KVMeta.TieringSpanID per KV   */
+  uint64_t* tiering_attr;    /* [kv_cap] (optional) base.KVMeta.TieringAttribute per KV;
+                                both or neither; see PBL_COL_TIERING                  */
 } pbl_decode_out;
 
 /* ABI version of the loaded library (== PBL_ABI_VERSION). */
@@ -222,10 +244,10 @@ int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stre
  * (ctypes, cgo): writes up to `cap` u64 values and returns how many it has:
  *   sizeof(pbl_block_batch), the offsets of its 9 fields in declaration order,
  *   sizeof(pbl_totals), the offsets of its 8 fields,
- *   sizeof(pbl_decode_out), the offsets of its 20 fields,
+ *   sizeof(pbl_decode_out), the offsets of its 22 fields,
  *   then likewise pbl_transforms, pbl_footer, pbl_index_out, pbl_kv_out,
- *   pbl_value_out and pbl_kv (sizeof, then every field's offset in declaration
- *   order).
+ *   pbl_value_out, pbl_kv and pbl_kv_meta (sizeof, then every field's offset in
+ *   declaration order).
  */
 size_t pbl_struct_layout(uint64_t* out, size_t cap);
 
@@ -459,7 +481,8 @@ uint64_t pbl_transform_workspace_bytes(uint32_t n_blocks);
  * Apply `t` to a decoded batch (`in`, as pbl_decode_batch left it, n_blocks
  * blocks) into `out` (same layout contract; caller-allocated; out->workspace of
  * pbl_transform_workspace_bytes): every visible KV (HideObsoletePoints drops the
- * obsolete ones) keeps its order, flags, entry offset and value; its trailer
+ * obsolete ones) keeps its order, flags, entry offset, KVMeta (tiering_span_id /
+ * tiering_attr, copied when both `in` and `out` carry them) and value; its trailer
  * takes the synthetic sequence number (InternalKey.SetSeqNum); its user key
  * becomes F[:Split(F)] ++ suffix (suffix set) or F, F = prefix ++ key (row
  * blocks; colblk: prefix ++ key[:Split(key)] ++ suffix); keys of entries that
@@ -536,6 +559,19 @@ void pbl_colblk_writer_reset(pbl_colblk_writer* w);
 int pbl_colblk_writer_add(pbl_colblk_writer* w, const uint8_t* key, size_t key_len, int64_t prefix_len,
                           uint64_t trailer, const uint8_t* value, size_t value_len, int value_kind,
                           int is_obsolete);
+/* Pebblev8 data blocks (sstable/format.go:305-316): DataBlockEncoder.Init with
+ * WithTieringColumns() (data_block.go:610-627).  Call on a fresh or reset writer,
+ * before the first add; the setting survives pbl_colblk_writer_reset. */
+void pbl_colblk_writer_set_tiering(pbl_colblk_writer* w, int tiering);
+/* DataBlockEncoder.AddWithSecondaryBlobHandle (data_block.go:712-765) with a
+ * base.KVMeta: the meta is stored only when its attribute is non-zero
+ * (KVMeta.IsSet, internal/base/internal.go:698-702), and meta and handle are
+ * ignored unless the writer has the tiering columns.  Same returns as
+ * pbl_colblk_writer_add. */
+int pbl_colblk_writer_add_meta(pbl_colblk_writer* w, const uint8_t* key, size_t key_len, int64_t prefix_len,
+                               uint64_t trailer, const uint8_t* value, size_t value_len, int value_kind,
+                               int is_obsolete, uint64_t tiering_span_id, uint64_t tiering_attr,
+                               const uint8_t* secondary_handle, size_t secondary_handle_len);
 uint32_t pbl_colblk_writer_rows(const pbl_colblk_writer* w);
 /* DataBlockEncoder.Size() as it was at `rows` rows (rows() or rows()-1). */
 size_t pbl_colblk_writer_size(const pbl_colblk_writer* w, uint32_t rows);
@@ -557,7 +593,11 @@ typedef struct pbl_colgen_config {
   uint32_t obsolete_every;     /* 0, or: row k of a block has isObsolete set
                                   when k % obsolete_every == obsolete_every-1
                                   (HideObsoletePoints measurements)         */
-  uint32_t reserved;
+  uint32_t tiering;            /* 0, or: Pebblev8 blocks with the tiering
+                                  columns; row k's KVMeta is span 1 + r % tiering,
+                                  attribute (base_wall_time / 1e9) + r % 3600,
+                                  unset (KVMeta{}) for one row in ten, r drawn
+                                  per row from the block's seed             */
 } pbl_colgen_config;
 
 /*
@@ -616,6 +656,11 @@ typedef struct pbl_kv {   /* base.InternalKV over the decoded arrays (block/kv.g
   uint32_t reserved;
 } pbl_kv;
 
+typedef struct pbl_kv_meta { /* base.KVMeta (internal/base/internal.go:686-689)    */
+  uint64_t tiering_span_id;
+  uint64_t tiering_attribute;
+} pbl_kv_meta;
+
 typedef struct pbl_data_iter pbl_data_iter;
 pbl_data_iter* pbl_data_iter_new(void);
 void pbl_data_iter_free(pbl_data_iter* it);
@@ -631,6 +676,15 @@ const pbl_kv* pbl_data_iter_next(pbl_data_iter* it);
 const pbl_kv* pbl_data_iter_prev(pbl_data_iter* it);
 const pbl_kv* pbl_data_iter_seek_ge(pbl_data_iter* it, const uint8_t* key, uint64_t key_len, uint32_t flags);
 const pbl_kv* pbl_data_iter_seek_lt(pbl_data_iter* it, const uint8_t* key, uint64_t key_len, uint32_t flags);
+/* FirstWithMeta / NextWithMeta / SeekGEWithMeta (colblk data_block.go:1574-1600;
+ * the MetaIterator of sstable/reader_iter.go:26-33): the same positioning, and
+ * *meta = the KV's KVMeta from the decoded tiering_span_id / tiering_attr
+ * arrays, or KVMeta{} when the iterator lands on no KV or the arrays were not
+ * decoded (NULL in `host`, as for row blocks and non-tiering formats). */
+const pbl_kv* pbl_data_iter_first_with_meta(pbl_data_iter* it, pbl_kv_meta* meta);
+const pbl_kv* pbl_data_iter_next_with_meta(pbl_data_iter* it, pbl_kv_meta* meta);
+const pbl_kv* pbl_data_iter_seek_ge_with_meta(pbl_data_iter* it, const uint8_t* key, uint64_t key_len,
+                                              uint32_t flags, pbl_kv_meta* meta);
 /* (kv, 0) same prefix; (NULL, 1) positioned at a KV of another prefix; (NULL, 0) none */
 const pbl_kv* pbl_data_iter_seek_prefix_ge(pbl_data_iter* it, const uint8_t* key, uint64_t key_len, uint32_t flags,
                                            int* prefix_did_not_match);

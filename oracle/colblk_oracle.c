@@ -31,6 +31,14 @@
  *   defaultKeySeeker           sstable/colblk/data_block.go:361-366, 428-442
  *   cockroachKeySeeker         cockroachkvs/cockroachkvs.go:782-802 (init), 1009-1071
  *                              (MaterializeUserKey)
+ *   DataBlockIter.decodeMeta   sstable/colblk/data_block.go:1602-1641 (FLAG_TIERING, the
+ *                              Pebblev8 tiering columns, ids :514-525): tieringSpanIDs /
+ *                              tieringAttributes decoded by DecodeColumn as Uint columns;
+ *                              KVMeta{} without the flag.  Pinned by the v8 block of
+ *                              sstable/testdata/writer_tiering_histogram (the only
+ *                              tiering bytes the reference holds).  A missing or
+ *                              malformed tiering column, where Go panics in
+ *                              initTieringMetadata, is CORRUPT_COLBLK_HEADER.
  *
  * Where Go would panic during metadata init the oracle reports
  * CORRUPT_COLBLK_HEADER; where Go would silently read outside a column during
@@ -149,6 +157,7 @@ typedef struct {
   ucol trailers;
   bmcol prefix_changed, external, obsolete;
   rbcol values;
+  ucol span, attr;  /* tiering columns (zero columns unless decoded) */
   uint32_t shared_len, data_len; /* prefix-bytes shared prefix length and data length */
 } coldec;
 
@@ -181,6 +190,17 @@ static int init_decoder(const uint8_t* blk, uint64_t len, uint32_t schema, colde
   }
   c->shared_len = (uint32_t)u_at(d, &c->keys.rb.off, 0);
   c->data_len = (uint32_t)u_at(d, &c->keys.rb.off, c->keys.rb.n);
+  return 1;
+}
+
+/* initTieringMetadata (data_block.go:1605-1631): the two Uint columns after
+ * isObsolete, by DecodeColumn (type check, end == next page start). */
+static int init_tiering(coldec* c) {
+  const blkdec* d = &c->d;
+  uint32_t S = c->ncols_schema;
+  uint64_t s, nx, e;
+  if (!column(d, S + 5, DT_UINT, &s, &nx) || !dec_uints(d, s, d->rows, &c->span, &e) || e != nx) return 0;
+  if (!column(d, S + 6, DT_UINT, &s, &nx) || !dec_uints(d, s, d->rows, &c->attr, &e) || e != nx) return 0;
   return 1;
 }
 
@@ -266,12 +286,14 @@ static int64_t materialize(const coldec* c, uint32_t row, uint8_t* dst) {
   return (int64_t)n;
 }
 
-/* Two passes (count, then fill) over DataBlockIter First/Next. */
-int orc_colblk_decode(const uint8_t* blk, uint64_t len, uint32_t schema, orc_block_out* o) {
+/* Two passes (count, then fill) over DataBlockIter First/Next (NextWithMeta
+ * with FLAG_TIERING). */
+int orc_colblk_decode_flags(const uint8_t* blk, uint64_t len, uint32_t schema, uint32_t flags, orc_block_out* o) {
   o->n_kv = o->key_bytes = o->val_bytes = o->n_restarts = 0;
   if (schema != FMT_COL_DEFAULT && schema != FMT_COL_CRDB1) return UNSUPPORTED;
   coldec c;
   if (!init_decoder(blk, len, schema, &c)) return CORRUPT_COLBLK_HEADER;
+  if ((flags & FLAG_TIERING) && !init_tiering(&c)) return CORRUPT_COLBLK_HEADER;
   uint64_t kb = 0, vb = 0;
   uint32_t rows = c.d.rows;
   for (uint32_t r = 0; r < rows; r++) {
@@ -299,6 +321,10 @@ int orc_colblk_decode(const uint8_t* blk, uint64_t len, uint32_t schema, orc_blo
     if (bm_at(&c.d, &c.external, r)) fl |= (hi > lo && (blk[lo] & 0xC0) == 0x80) ? KV_VALBLK : KV_BLOB;
     if (o->kv_flags) o->kv_flags[r] = fl;
     if (o->entry_off) o->entry_off[r] = r;
+    if (o->span) { /* decodeMeta (data_block.go:1633-1641); KVMeta{} without tiering */
+      o->span[r] = u_at(&c.d, &c.span, r);
+      o->attr[r] = u_at(&c.d, &c.attr, r);
+    }
     o->key_off[r] = (uint32_t)kb;
     o->val_off[r] = (uint32_t)vb;
     kb += (uint64_t)kl;
@@ -307,6 +333,10 @@ int orc_colblk_decode(const uint8_t* blk, uint64_t len, uint32_t schema, orc_blo
   o->key_off[rows] = (uint32_t)kb;
   o->val_off[rows] = (uint32_t)vb;
   return OK;
+}
+
+int orc_colblk_decode(const uint8_t* blk, uint64_t len, uint32_t schema, orc_block_out* o) {
+  return orc_colblk_decode_flags(blk, len, schema, 0, o);
 }
 
 /* Iterate-only CPU baseline for colblk (SURVEY.md §8(d) mode i), shaped like
@@ -391,10 +421,10 @@ uint64_t orc_colblk_scan_checksum(const uint8_t* blk, uint64_t len, uint32_t sch
  * (sstable/colblk/data_block.go:1680-1697): rows whose isObsolete bit is set
  * (data_block.go:519) are skipped; the block is checked and decoded whole
  * first, so a block that fails without the transform fails with it. */
-static int colblk_decode_hide(const uint8_t* blk, uint64_t len, uint32_t fmt, orc_block_out* o) {
+static int colblk_decode_hide(const uint8_t* blk, uint64_t len, uint32_t fmt, uint32_t flags, orc_block_out* o) {
   orc_block_out t;
   memset(&t, 0, sizeof(t));
-  int st = orc_colblk_decode(blk, len, fmt, &t);
+  int st = orc_colblk_decode_flags(blk, len, fmt, flags, &t);
   if (st != OK) {
     o->n_kv = o->key_bytes = o->val_bytes = o->n_restarts = 0;
     return st;
@@ -407,8 +437,10 @@ static int colblk_decode_hide(const uint8_t* blk, uint64_t len, uint32_t fmt, or
   uint32_t* vo = calloc(n + 1, 4);
   uint8_t* kb = calloc(t.key_bytes + 1, 1);
   uint8_t* vb = calloc(t.val_bytes + 1, 1);
-  orc_block_out f = {0, 0, 0, 0, tr, fl, eo, ko, vo, kb, vb, NULL};
-  st = orc_colblk_decode(blk, len, fmt, &f);
+  uint64_t* sp = calloc(n + 1, 8);
+  uint64_t* at = calloc(n + 1, 8);
+  orc_block_out f = {0, 0, 0, 0, tr, fl, eo, ko, vo, kb, vb, NULL, sp, at};
+  st = orc_colblk_decode_flags(blk, len, fmt, flags, &f);
   uint64_t m = 0, kn = 0, vn = 0;
   for (uint64_t i = 0; st == OK && i < n; i++) {
     if (fl[i] & KV_OBSOLETE) continue;
@@ -417,6 +449,10 @@ static int colblk_decode_hide(const uint8_t* blk, uint64_t len, uint32_t fmt, or
       o->trailer[m] = tr[i];
       if (o->kv_flags) o->kv_flags[m] = fl[i];
       if (o->entry_off) o->entry_off[m] = eo[i];
+      if (o->span) {
+        o->span[m] = sp[i];
+        o->attr[m] = at[i];
+      }
       o->key_off[m] = (uint32_t)kn;
       o->val_off[m] = (uint32_t)vn;
       memcpy(o->keys + kn, kb + ko[i], kl);
@@ -430,7 +466,7 @@ static int colblk_decode_hide(const uint8_t* blk, uint64_t len, uint32_t fmt, or
     o->key_off[m] = (uint32_t)kn;
     o->val_off[m] = (uint32_t)vn;
   }
-  free(tr); free(fl); free(eo); free(ko); free(vo); free(kb); free(vb);
+  free(tr); free(fl); free(eo); free(ko); free(vo); free(kb); free(vb); free(sp); free(at);
   o->n_kv = st == OK ? m : 0;
   o->key_bytes = st == OK ? kn : 0;
   o->val_bytes = st == OK ? vn : 0;
@@ -439,14 +475,25 @@ static int colblk_decode_hide(const uint8_t* blk, uint64_t len, uint32_t fmt, or
 }
 
 static int decode_block(const uint8_t* blk, uint64_t len, uint32_t fmt, uint32_t flags, orc_block_out* o) {
-  if (fmt != FMT_ROW && (flags & FLAG_HIDE_OBSOLETE)) return colblk_decode_hide(blk, len, fmt, o);
+  if (fmt != FMT_ROW && (flags & FLAG_HIDE_OBSOLETE)) return colblk_decode_hide(blk, len, fmt, flags, o);
+  if (fmt == FMT_ROW && o->span) { /* rowblk.Iter: no meta columns, KVMeta{} */
+    uint64_t* sp = o->span;
+    uint64_t* at = o->attr;
+    o->span = o->attr = NULL;
+    int st = decode_block(blk, len, fmt, flags, o);
+    if (st == OK && o->trailer)
+      for (uint64_t i = 0; i < o->n_kv; i++) sp[i] = at[i] = 0;
+    o->span = sp;
+    o->attr = at;
+    return st;
+  }
   if (fmt == FMT_ROW && (flags & FLAG_HIDE_OBSOLETE) && !(flags & FLAG_RAW_KEYS)) {
     /* HideObsoletePoints: rowblk.Iter under blockiter.Transforms{HideObsoletePoints} */
     const orc_transforms t = {0, 1, 0, NULL, 0, NULL, 0};
     return orc_rowblk_decode_tf(blk, len, flags & ~FLAG_HIDE_OBSOLETE, &t, o);
   }
   if (fmt == FMT_ROW) return orc_rowblk_decode(blk, len, flags, o);
-  return orc_colblk_decode(blk, len, fmt, o);
+  return orc_colblk_decode_flags(blk, len, fmt, flags, o);
 }
 
 /* Batch decode of a (possibly mixed) batch in the device layout; block b has
@@ -469,6 +516,8 @@ int orc_decode_batch(const uint8_t* blocks, const uint64_t* off, const uint32_t*
       o.keys = bo->key_bytes + kb;
       o.vals = bo->val_bytes + vb;
       o.restarts = bo->restarts ? bo->restarts + rb : NULL;
+      o.span = bo->tiering_span_id ? bo->tiering_span_id + kvb : NULL;
+      o.attr = bo->tiering_attr ? bo->tiering_attr + kvb : NULL;
     }
     int st = decode_block(blocks + off[b], len[b], block_fmt ? block_fmt[b] : fmt, flags, &o);
     if (fill && st != OK) {

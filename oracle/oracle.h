@@ -15,6 +15,7 @@ enum { FMT_ROW = 0, FMT_COL_DEFAULT = 1, FMT_COL_CRDB1 = 2 };
 #define FLAG_NO_VALUER 0x2u
 #define FLAG_RAW_KEYS 0x4u /* rowblk.RawIter (rowblk_iter.go:1743-1794) */
 #define FLAG_HIDE_OBSOLETE 0x8u /* blockiter.Transforms.HideObsoletePoints during the decode */
+#define FLAG_TIERING 0x10u /* colblk blocks carry the Pebblev8 tiering columns (decodeMeta) */
 
 #define KV_RESTART 0x01u
 #define KV_RESTART_SAMEPFX 0x02u
@@ -36,6 +37,9 @@ typedef struct orc_block_out {
   uint8_t* keys;
   uint8_t* vals;
   uint32_t* restarts;
+  /* base.KVMeta per KV (NULL = not requested; zeros unless FLAG_TIERING) */
+  uint64_t* span;
+  uint64_t* attr;
 } orc_block_out;
 
 /* Batch form in exactly the device layout of include/pebble_amd.h
@@ -56,6 +60,8 @@ typedef struct orc_batch_out {
   uint32_t* blk_status;
   uint64_t n_kv, key_bytes_total, val_bytes_total, n_restarts;
   uint32_t status_mask, n_bad_blocks;
+  uint64_t* tiering_span_id; /* optional, as pbl_decode_out */
+  uint64_t* tiering_attr;
 } orc_batch_out;
 
 /* blockiter.Transforms (sstable/blockiter/transforms.go:20-56) for the row
@@ -77,5 +83,6 @@ int orc_decode_varint(const uint8_t* p, const uint8_t* end, uint32_t* v);
 int orc_rowblk_decode(const uint8_t* blk, uint64_t len, uint32_t flags, orc_block_out* o);
 uint64_t orc_rowblk_scan_checksum(const uint8_t* blk, uint64_t len, uint32_t flags, uint64_t* n_kv);
 int orc_colblk_decode(const uint8_t* blk, uint64_t len, uint32_t schema, orc_block_out* o);
+int orc_colblk_decode_flags(const uint8_t* blk, uint64_t len, uint32_t schema, uint32_t flags, orc_block_out* o);
 uint64_t orc_colblk_scan_checksum(const uint8_t* blk, uint64_t len, uint32_t schema, uint64_t* n_kv);
 #endif

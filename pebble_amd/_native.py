@@ -42,7 +42,7 @@ PBL_TABLE_PEBBLEV5, PBL_TABLE_PEBBLEV6, PBL_TABLE_PEBBLEV7 = 7, 8, 9
 PBL_CHECKSUM_NONE, PBL_CHECKSUM_CRC32C, PBL_CHECKSUM_XXHASH, PBL_CHECKSUM_XXHASH64 = 0, 1, 2, 3
 PBL_COMPRESSION_NONE, PBL_COMPRESSION_SNAPPY, PBL_COMPRESSION_ZSTD, PBL_COMPRESSION_MINLZ = 0, 1, 7, 8
 
-ABI_VERSION = 7  # include/pebble_amd.h PBL_ABI_VERSION
+ABI_VERSION = 8  # include/pebble_amd.h PBL_ABI_VERSION
 
 PBL_FMT_ROW = 0
 PBL_FMT_COL_DEFAULT = 1
@@ -53,6 +53,7 @@ PBL_ROW_NO_VALUER = 0x2
 PBL_ROW_RAW_KEYS = 0x4
 PBL_BATCH_VARLEN = 0x100
 PBL_ROW_HIDE_OBSOLETE = 0x8
+PBL_COL_TIERING = 0x10
 PBL_KERNEL_SINGLE = 0x200
 PBL_KERNEL_PIPE = 0x400
 PBL_KERNEL_POOL = 0x4000
@@ -85,7 +86,7 @@ class ColGenConfigC(ctypes.Structure):
         ("prefix_len_shared", ctypes.c_uint32), ("roach_key_len", ctypes.c_uint32),
         ("avg_keys_per_prefix", ctypes.c_uint32), ("base_wall_time", ctypes.c_uint64),
         ("pct_logical", ctypes.c_uint32), ("value_len", ctypes.c_uint32),
-        ("obsolete_every", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+        ("obsolete_every", ctypes.c_uint32), ("tiering", ctypes.c_uint32),
     ]
 
 
@@ -116,6 +117,7 @@ class DecodeOutC(ctypes.Structure):
         ("kv_cap", ctypes.c_uint64), ("key_cap", ctypes.c_uint64),
         ("val_cap", ctypes.c_uint64), ("rst_cap", ctypes.c_uint64),
         ("workspace", _vp), ("workspace_bytes", ctypes.c_uint64),
+        ("tiering_span_id", _vp), ("tiering_attr", _vp),
     ]
 
 
@@ -167,6 +169,10 @@ class KvC(ctypes.Structure):  # pbl_kv (base.InternalKV over the decoded arrays)
                 ("reserved", ctypes.c_uint32)]
 
 
+class KvMetaC(ctypes.Structure):  # pbl_kv_meta (base.KVMeta)
+    _fields_ = [("tiering_span_id", ctypes.c_uint64), ("tiering_attribute", ctypes.c_uint64)]
+
+
 PBL_CMP_DEFAULT, PBL_CMP_TESTKEYS, PBL_CMP_CRDB = 0, 1, 2
 _kvp = ctypes.POINTER(KvC)
 _u8p = ctypes.c_char_p
@@ -185,6 +191,10 @@ SIGNATURES = {
     "pbl_data_iter_seek_lt": (_kvp, [_vp, _u8p, ctypes.c_uint64, ctypes.c_uint32]),
     "pbl_data_iter_seek_prefix_ge": (_kvp, [_vp, _u8p, ctypes.c_uint64, ctypes.c_uint32,
                                             ctypes.POINTER(ctypes.c_int)]),
+    "pbl_data_iter_first_with_meta": (_kvp, [_vp, ctypes.POINTER(KvMetaC)]),
+    "pbl_data_iter_next_with_meta": (_kvp, [_vp, ctypes.POINTER(KvMetaC)]),
+    "pbl_data_iter_seek_ge_with_meta": (_kvp, [_vp, _u8p, ctypes.c_uint64, ctypes.c_uint32,
+                                               ctypes.POINTER(KvMetaC)]),
     "pbl_data_iter_next_with_same_prefix": (_kvp, [_vp, ctypes.POINTER(ctypes.c_int)]),
     "pbl_data_iter_next_prefix": (_kvp, [_vp, _u8p, ctypes.c_uint64]),
     "pbl_data_iter_is_lower_bound": (ctypes.c_int, [_vp, _u8p, ctypes.c_uint64]),
@@ -240,6 +250,11 @@ SIGNATURES = {
     "pbl_colblk_writer_add": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int64,
                                              ctypes.c_uint64, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int,
                                              ctypes.c_int]),
+    "pbl_colblk_writer_set_tiering": (None, [_vp, ctypes.c_int]),
+    "pbl_colblk_writer_add_meta": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int64,
+                                                  ctypes.c_uint64, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int,
+                                                  ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_char_p,
+                                                  ctypes.c_size_t]),
     "pbl_colblk_writer_rows": (ctypes.c_uint32, [_vp]),
     "pbl_colblk_writer_size": (ctypes.c_size_t, [_vp, ctypes.c_uint32]),
     "pbl_colblk_writer_finish": (ctypes.c_size_t, [_vp, ctypes.c_uint32, _vp, ctypes.c_size_t]),

@@ -137,10 +137,13 @@ class DecodedBatch:
     cap: Capacity
     _host_totals: Optional[N.TotalsC] = field(default=None, repr=False)
     source: Optional[BlockBatch] = field(default=None, repr=False)  # the batch it was decoded from
+    # base.KVMeta per KV (Pebblev8 tiering, PBL_COL_TIERING); None = not requested
+    tiering_span_id: Optional[torch.Tensor] = None
+    tiering_attr: Optional[torch.Tensor] = None
 
     @classmethod
     def allocate(cls, n_blocks: int, cap: Capacity, device, entry_off: bool = True,
-                 restarts: bool = True) -> "DecodedBatch":
+                 restarts: bool = True, meta: bool = False) -> "DecodedBatch":
         d = torch.device(device)
         u = lambda n, dt: torch.empty(max(int(n), 1), dtype=dt, device=d)  # noqa: E731
         lib = N.lib()
@@ -157,6 +160,8 @@ class DecodedBatch:
             blk_status=u(n_blocks, torch.int32),
             totals=torch.zeros(ctypes.sizeof(N.TotalsC), dtype=torch.uint8, device=d),
             workspace=u(ws, torch.uint8), cap=cap,
+            tiering_span_id=u(cap.kv, torch.int64) if meta else None,
+            tiering_attr=u(cap.kv, torch.int64) if meta else None,
         )
 
     def c_struct(self) -> N.DecodeOutC:
@@ -170,6 +175,7 @@ class DecodedBatch:
             self.blk_rst_base.data_ptr(), self.blk_status.data_ptr(), self.totals.data_ptr(),
             c.kv, c.key, c.val, c.rst if self.restarts is not None else 0,
             self.workspace.data_ptr(), self.workspace.numel(),
+            _dp(self.tiering_span_id), _dp(self.tiering_attr),
         )
 
     # ---- host readouts ------------------------------------------------------------
@@ -200,6 +206,9 @@ class DecodedBatch:
             "n_restarts": int(t.n_restarts), "status_mask": int(t.status_mask),
             "n_bad_blocks": int(t.n_bad_blocks), "n_slow_blocks": int(t.n_slow_blocks),
         }
+        if self.tiering_span_id is not None:
+            r["tiering_span_id"] = g(self.tiering_span_id, n, np.uint64)
+            r["tiering_attr"] = g(self.tiering_attr, n, np.uint64)
         return r
 
 
@@ -228,12 +237,13 @@ def size_batch(batch: BlockBatch, stream=None) -> DecodedBatch:
 
 
 def decode(batch: BlockBatch, cap: Optional[Capacity] = None, stream=None, entry_off: bool = True,
-           restarts: bool = True, exact: bool = False) -> DecodedBatch:
+           restarts: bool = True, exact: bool = False, meta: bool = False) -> DecodedBatch:
     """Decode a batch.  Without `cap`, capacities are estimated and the decode
     re-runs once with exact ones on PBL_OVERFLOW; `exact=True` runs the size
     pass first instead (one parse more, never a second decode).  The outputs are
     allocated on the launch stream, so the caching allocator never hands them to
-    other work while the kernel writes them."""
+    other work while the kernel writes them.  `meta`: also the per-KV KVMeta
+    arrays (the tiering columns of PBL_COL_TIERING batches; zeros otherwise)."""
     st = stream if stream is not None else torch.cuda.current_stream(batch.device)
     if cap is None and exact:
         sz = size_batch(batch, st)
@@ -242,7 +252,7 @@ def decode(batch: BlockBatch, cap: Optional[Capacity] = None, stream=None, entry
         cap = Capacity(kv=int(t.n_kv), key=int(t.key_bytes), val=int(t.val_bytes), rst=int(t.n_restarts))
     cap = cap or Capacity.estimate(batch)
     with torch.cuda.stream(st):
-        out = DecodedBatch.allocate(batch.n_blocks, cap, batch.device, entry_off, restarts)
+        out = DecodedBatch.allocate(batch.n_blocks, cap, batch.device, entry_off, restarts, meta)
     decode_into(batch, out, st)
     out.source = batch
     st.synchronize()
@@ -251,7 +261,7 @@ def decode(batch: BlockBatch, cap: Optional[Capacity] = None, stream=None, entry
         cap = Capacity(kv=int(t.n_kv) + 1, key=int(t.key_bytes) + 1, val=int(t.val_bytes) + 1,
                        rst=int(t.n_restarts) + 1)
         with torch.cuda.stream(st):
-            out = DecodedBatch.allocate(batch.n_blocks, cap, batch.device, entry_off, restarts)
+            out = DecodedBatch.allocate(batch.n_blocks, cap, batch.device, entry_off, restarts, meta)
         decode_into(batch, out, st)
         out.source = batch
         st.synchronize()

@@ -29,6 +29,12 @@ class DataIter:
                                                                                  else np.uint8))
             self._keep[k] = a
             setattr(o, k, a.ctypes.data)
+        for k in ("tiering_span_id", "tiering_attr"):  # KVMeta arrays, when decoded
+            a = host.get(k)
+            if a is not None:
+                a = np.ascontiguousarray(a if a.size else np.zeros(1, np.uint64))
+                self._keep[k] = a
+                setattr(o, k, a.ctypes.data)
         self._out = o
         self._it = self._lib.pbl_data_iter_new()
         if not self._it:
@@ -67,6 +73,23 @@ class DataIter:
 
     def SeekLT(self, key: bytes, flags: int = 0):
         return self._kv(self._lib.pbl_data_iter_seek_lt(self._it, key, len(key), flags))
+
+    # MetaIterator (colblk data_block.go:1574-1600): (kv, (TieringSpanID, TieringAttribute))
+    def _meta(self, p, m) -> Tuple[Optional[InternalKV], Tuple[int, int]]:
+        return self._kv(p), (int(m.tiering_span_id), int(m.tiering_attribute))
+
+    def FirstWithMeta(self):
+        m = N.KvMetaC()
+        return self._meta(self._lib.pbl_data_iter_first_with_meta(self._it, ctypes.byref(m)), m)
+
+    def NextWithMeta(self):
+        m = N.KvMetaC()
+        return self._meta(self._lib.pbl_data_iter_next_with_meta(self._it, ctypes.byref(m)), m)
+
+    def SeekGEWithMeta(self, key: bytes, flags: int = 0):
+        m = N.KvMetaC()
+        return self._meta(self._lib.pbl_data_iter_seek_ge_with_meta(self._it, key, len(key), flags,
+                                                                   ctypes.byref(m)), m)
 
     def SeekPrefixGE(self, key: bytes, flags: int = 0) -> Tuple[Optional[InternalKV], bool]:
         miss = ctypes.c_int(0)

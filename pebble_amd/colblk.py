@@ -33,12 +33,17 @@ class DataBlockEncoder:
     """colblk.DataBlockEncoder.  `add` performs KeyWriter.ComparePrev itself and
     returns KeyComparison.PrefixEqual()."""
 
-    def __init__(self, schema: int = SCHEMA_CRDB1, bundle_size: int = 16):
+    def __init__(self, schema: int = SCHEMA_CRDB1, bundle_size: int = 16, tiering: bool = False):
+        """`tiering`: Init(schema, WithTieringColumns()) -- the Pebblev8 layout
+        (sstable/format.go:305-316), whose add() also takes a base.KVMeta."""
         self._lib = N.lib()
         self._w = self._lib.pbl_colblk_writer_new(schema, bundle_size)
         if not self._w:
             raise ValueError(f"bad schema {schema} / bundle size {bundle_size}")
         self.schema = schema
+        self.tiering = tiering
+        if tiering:
+            self._lib.pbl_colblk_writer_set_tiering(self._w, 1)
 
     def __del__(self):
         w, self._w = getattr(self, "_w", None), None
@@ -49,9 +54,13 @@ class DataBlockEncoder:
         self._lib.pbl_colblk_writer_reset(self._w)
 
     def add(self, user_key: bytes, trailer: int, value: bytes = b"", value_kind: int = VALUE_IN_PLACE,
-            is_obsolete: bool = False, prefix_len: int = -1) -> bool:
-        r = self._lib.pbl_colblk_writer_add(self._w, user_key, len(user_key), prefix_len, trailer, value,
-                                           len(value), value_kind, int(is_obsolete))
+            is_obsolete: bool = False, prefix_len: int = -1, meta: tuple = (0, 0),
+            secondary_handle: bytes = b"") -> bool:
+        """Add / AddWithSecondaryBlobHandle (data_block.go:694-765); `meta` is
+        (TieringSpanID, TieringAttribute), stored when the attribute is set."""
+        r = self._lib.pbl_colblk_writer_add_meta(self._w, user_key, len(user_key), prefix_len, trailer, value,
+                                                len(value), value_kind, int(is_obsolete), int(meta[0]),
+                                                int(meta[1]), secondary_handle, len(secondary_handle))
         if r not in (0, 1):
             raise ValueError(f"invalid key {user_key!r}")
         return bool(r)
@@ -76,13 +85,15 @@ def gen_col_blocks(seed: int, n_blocks: int, block_size: int = 32768, schema: in
                    alphabet_len: int = 26, roach_key_len: int = 12, prefix_len_shared: int = 4,
                    avg_keys_per_prefix: int = 1, pct_logical: int = 0, value_len: int = 128,
                    base_wall_time: int = 1_700_000_000_000_000_000, n_threads: int = 0,
-                   obsolete_every: int = 0):
+                   obsolete_every: int = 0, tiering: int = 0):
     """Seeded synthetic colblk blocks at a fixed `block_size` stride (host numpy).
     Defaults are BASELINE config 3: cockroachkvs_bench_test.go:83-89 KeyGenConfig
-    (alphabet 26, RoachKeyLen 12, PrefixLenShared 4, 1 key per prefix) with 128 B values."""
+    (alphabet 26, RoachKeyLen 12, PrefixLenShared 4, 1 key per prefix) with 128 B values.
+    `tiering` > 0: Pebblev8 blocks with tiering columns and per-row KVMeta
+    (span ids 1..tiering; include/pebble_amd.h pbl_colgen_config)."""
     import os
     cfg = N.ColGenConfigC(seed, alphabet_len, prefix_len_shared, roach_key_len, avg_keys_per_prefix,
-                          base_wall_time, pct_logical, value_len, obsolete_every, 0)
+                          base_wall_time, pct_logical, value_len, obsolete_every, tiering)
     buf = np.zeros(n_blocks * block_size + 16, np.uint8)
     off = np.empty(n_blocks, np.uint64)
     lens = np.empty(n_blocks, np.uint32)

@@ -63,6 +63,7 @@ struct Desc {
   UCol v_off;
   uint32_t v_data, v_lo, v_hi;    // values data start and [off[0], off[rows])
   uint32_t key_end;               // page start of the values column
+  UCol span, attr;                // Pebblev8 tiering columns (PBL_COL_TIERING; else width 0, base 0)
 };
 
 struct Lds {
@@ -140,6 +141,11 @@ __device__ __forceinline__ uint64_t u_at(const Src& S, const UCol& u, uint32_t i
   const uint32_t o = u.at + i * u.w;
   return u.base + (F ? lds_le(S.head + o, u.w) : S.le(o, u.w));
 }
+// A Uint column past the staged head (the tiering columns follow the values):
+// through the head / tail / global reader.
+__device__ __forceinline__ uint64_t u_at_any(const Src& S, const UCol& u, uint32_t i) {
+  return u.w == 0 ? u.base : u.base + S.le(u.at + i * u.w, u.w);
+}
 template <bool F>
 __device__ __forceinline__ uint32_t key_byte(const Src& S, uint32_t o) {
   return F ? S.head[o] : S.byte(o);
@@ -205,57 +211,8 @@ struct Dir {
   }
 };
 
-__device__ __forceinline__ uint32_t parse_block(const Src& S, uint32_t schema, Desc* D) {
-  if (schema != PBL_FMT_COL_DEFAULT && schema != PBL_FMT_COL_CRDB1) return PBL_UNSUPPORTED;
-  const uint32_t nsc = schema == PBL_FMT_COL_CRDB1 ? 4 : 2;
-  Dir dir;
-  dir.custom = 4 + (schema == PBL_FMT_COL_CRDB1 ? 1 : 0);  // DataBlockCustomHeaderSize + schema header
-  if (S.len < dir.custom + 7) return PBL_CORRUPT_COLBLK_HEADER;
-  dir.ncols = uint32_t(S.le_u(dir.custom + 1, 2));
-  D->rows = uint32_t(S.le_u(dir.custom + 3, 4));
-  const uint32_t rows = D->rows;
-  uint64_t s, nx, e;
-  uint32_t dummy;
-  if (!dir.column(S, nsc + 0, kDtUint, &s, &nx) || !dec_uints(S, s, rows, &D->trailers, &e) || e != nx)
-    return PBL_CORRUPT_COLBLK_HEADER;
-  if (!dir.column(S, nsc + 1, kDtBool, &s, &nx) || !dec_bitmap(S, s, rows, &D->pc_at, &e) || e != nx)
-    return PBL_CORRUPT_COLBLK_HEADER;
-  if (!dir.column(S, nsc + 2, kDtBytes, &s, &nx) || !dec_rawbytes(S, s, rows, &D->v_off, &D->v_data, &e) ||
-      e != nx)
-    return PBL_CORRUPT_COLBLK_HEADER;
-  D->key_end = uint32_t(s);
-  if (!dir.column(S, nsc + 3, kDtBool, &s, &nx) || !dec_bitmap(S, s, rows, &D->ext_at, &e) || e != nx)
-    return PBL_CORRUPT_COLBLK_HEADER;
-  if (!dir.column(S, nsc + 4, kDtBool, &s, &nx) || !dec_bitmap(S, s, rows, &D->obs_at, &e) || e != nx)
-    return PBL_CORRUPT_COLBLK_HEADER;
-  // key columns: PrefixBytes ("empty PrefixBytes" panics for 0 rows)
-  if (!dir.column(S, 0, kDtPrefix, &s, &nx) || rows == 0 || s >= S.len) return PBL_CORRUPT_COLBLK_HEADER;
-  D->pb_shift = S.byte(uint32_t(s));
-  if (D->pb_shift > 16) return PBL_CORRUPT_COLBLK_HEADER;
-  const uint32_t nbund = 1 + ((rows - 1) >> D->pb_shift);
-  if (!dec_rawbytes(S, s + 1, rows + nbund, &D->pb_off, &D->pb_data, &e) || e != nx)
-    return PBL_CORRUPT_COLBLK_HEADER;
-  if (schema == PBL_FMT_COL_CRDB1) {
-    if (!dir.column(S, 1, kDtUint, &s, &nx) || !dec_uints(S, s, rows, &D->wall, &e) || e != nx)
-      return PBL_CORRUPT_COLBLK_HEADER;
-    if (!dir.column(S, 2, kDtUint, &s, &nx) || !dec_uints(S, s, rows, &D->logical, &e) || e != nx)
-      return PBL_CORRUPT_COLBLK_HEADER;
-  }
-  if (!dir.column(S, schema == PBL_FMT_COL_CRDB1 ? 3 : 1, kDtBytes, &s, &nx) ||
-      !dec_rawbytes(S, s, rows, &D->rb_off, &D->rb_data, &e) || e != nx)
-    return PBL_CORRUPT_COLBLK_HEADER;
-  (void)dummy;
-  const UCol& po = D->pb_off;
-  D->shared_len = po.w ? uint32_t(S.le_u(po.at, po.w)) : 0;
-  D->data_len = po.w ? uint32_t(S.le_u(po.at + (rows + nbund) * po.w, po.w)) : 0;
-  const UCol& vo = D->v_off;
-  D->v_lo = vo.w ? uint32_t(S.le_u(vo.at, vo.w)) : 0;
-  D->v_hi = vo.w ? uint32_t(S.le_u(vo.at + rows * vo.w, vo.w)) : 0;
-  if (D->shared_len > D->data_len || D->v_lo > D->v_hi) return PBL_CORRUPT_BOUNDS;
-  return PBL_OK;
-}
-
-// Same decode, one lane per column (wave 0, all 64 lanes call it), in uniform
+// DataBlockDecoder.Init + the KeySeeker init (data_block.go:1096-1109;
+// block.go:287-301 DecodeColumn), one lane per column (wave 0, all 64 lanes call it), in uniform
 // stages so that every lane issues the same reads: (1) its directory entry
 // (Dir::column), (2) the encoding bytes at its column's start, (3) per-kind
 // arithmetic restating dec_uints / dec_bitmap / dec_rawbytes, (4) the first and
@@ -263,6 +220,9 @@ __device__ __forceinline__ uint32_t parse_block(const Src& S, uint32_t schema, D
 // statuses combine by ballot exactly as the serial order would (every header
 // failure is PBL_CORRUPT_COLBLK_HEADER; the final bounds check is
 // PBL_CORRUPT_BOUNDS).  Lane 0 writes the shared fields; each column lane its own.
+// `tiering` (PBL_COL_TIERING): the Pebblev8 tieringSpanID / tieringAttribute
+// Uint columns (data_block.go:514-525) are decoded as initTieringMetadata does
+// (:1605-1631) by two more lanes; otherwise their descriptors are zero columns.
 __device__ __forceinline__ uint32_t sbyte(const Src& S, uint64_t o) { return o < S.len ? S.byte(uint32_t(o)) : 0u; }
 __device__ __forceinline__ uint64_t sle(const Src& S, uint64_t o, uint32_t w) {
   return (w && o + w <= S.len) ? S.le_u(uint32_t(o), w) : 0ull;
@@ -271,7 +231,7 @@ __device__ __forceinline__ bool uint_width_ok(uint32_t w, bool delta) {
   return w == 0 || w == 1 || w == 2 || w == 4 || (w == 8 && !delta);
 }
 
-__device__ __forceinline__ uint32_t parse_block_wave(const Src& S, uint32_t schema, Desc* D) {
+__device__ __forceinline__ uint32_t parse_block_wave(const Src& S, uint32_t schema, bool tiering, Desc* D) {
   const int l = lane_id();
   if (schema != PBL_FMT_COL_DEFAULT && schema != PBL_FMT_COL_CRDB1) return PBL_UNSUPPORTED;
   const uint32_t nsc = schema == PBL_FMT_COL_CRDB1 ? 4 : 2;
@@ -281,11 +241,20 @@ __device__ __forceinline__ uint32_t parse_block_wave(const Src& S, uint32_t sche
   const uint32_t rows = uint32_t(S.le_u(custom + 3, 4));
   if (l == 0) D->rows = rows;
   const uint32_t c = uint32_t(l);
-  const bool active = c < nsc + 5;
+  const bool active = c < nsc + (tiering ? 7u : 5u);
   // column kinds: 0 Uint, 1 Bool, 2 Bytes, 3 PrefixBytes
   const bool crdb = schema == PBL_FMT_COL_CRDB1;
+  const bool tier_col = c == nsc + 5 || c == nsc + 6;
+  if (tier_col && !tiering) {  // KVMeta{}: zero columns
+    UCol z;
+    z.base = 0;
+    z.w = 0;
+    z.at = 0;
+    if (c == nsc + 5) D->span = z;
+    else D->attr = z;
+  }
   const uint32_t kind = c == 0 ? 3u
-                        : (c == nsc || (crdb && (c == 1 || c == 2))) ? 0u
+                        : (c == nsc || tier_col || (crdb && (c == 1 || c == 2))) ? 0u
                         : (c == nsc + 1 || c == nsc + 3 || c == nsc + 4) ? 1u
                         : 2u;
   const uint32_t want = kind == 0 ? uint32_t(kDtUint) : kind == 1 ? uint32_t(kDtBool)
@@ -374,6 +343,8 @@ __device__ __forceinline__ uint32_t parse_block_wave(const Src& S, uint32_t sche
       D->data_len = uint32_t(lastv);
     } else if (kind == 0) {
       if (c == nsc) D->trailers = u;
+      else if (c == nsc + 5) D->span = u;
+      else if (c == nsc + 6) D->attr = u;
       else if (c == 1) D->wall = u;
       else D->logical = u;
     } else if (kind == 1) {
@@ -584,7 +555,7 @@ __device__ __forceinline__ void col_block(Lds& s, const Args& A, uint32_t b, uin
   const Src S{(lds_cu8)to_lds(s.head4), (lds_cu8)to_lds(s.tail4), (glb_cu8)(A.in.blocks + boff), nhead, tail_lo,
               blen};
   if (wave_id() == 0) {
-    const uint32_t st = parse_block_wave(S, schema, &s.d);
+    const uint32_t st = parse_block_wave(S, schema, (A.in.flags & PBL_COL_TIERING) != 0, &s.d);
     if (lane_id() == 0) {
       s.d.status = st;
       s.status = st;
@@ -678,6 +649,10 @@ __device__ __forceinline__ void col_rows(Lds& s, const Args& A, uint32_t b, uint
         O.kv_flags[kvb + r] = fl;
       }
       if (O.entry_off) O.entry_off[kvb + r] = r;
+      if (O.tiering_span_id) {  // decodeMeta (data_block.go:1633-1641)
+        O.tiering_span_id[kvb + r] = u_at_any(S, d.span, r);
+        O.tiering_attr[kvb + r] = u_at_any(S, d.attr, r);
+      }
     }
   }
 

@@ -231,7 +231,7 @@ __device__ __forceinline__ void col_parse(CLds& L, Slot& P, const Slot& E, const
   CSTAMP(A, P.b, 0);
   if (!kSizeOnly && wave_id() == 1 && E.mode != kNone) col_resolve(L, E, A);
   if (wave_id() == 0 && P.b < A.in.n_blocks) {
-    const uint32_t st = parse_block_wave(S, schema, &P.d);
+    const uint32_t st = parse_block_wave(S, schema, (A.in.flags & PBL_COL_TIERING) != 0, &P.d);
     if (lane_id() == 0) {
       L.bad = 0;
       P.status = st;
@@ -382,6 +382,14 @@ __device__ __forceinline__ void col_emit_rows(CLds& L, const Slot& E, const Args
       for (uint32_t i = uint32_t(t); i < n; i += kTPB) to_glb(vout)[i] = uint8_t(S.byte(j0 + i));
     }
   }
+  // KVMeta (decodeMeta, data_block.go:1633-1641): its own pass after the
+  // copies, so the per-row loop above keeps its register budget
+  if (O.tiering_span_id) {
+    for (uint32_t r = t; r < rows; r += kTPB) {
+      to_glb(O.tiering_span_id)[kvb + r] = u_at_any(S, d.span, r);
+      to_glb(O.tiering_attr)[kvb + r] = u_at_any(S, d.attr, r);
+    }
+  }
   CSTAMP(A, b, 7);
 }
 
@@ -465,6 +473,10 @@ __device__ __forceinline__ void col_emit_rows_hide(CLds& L, const Slot& E, const
       } else {
         for (uint32_t o = q8; o < len; o += 8) vout[o0 + o] = uint8_t(S.byte(src + o));
       }
+    }
+    if (O.tiering_span_id && vis) {  // KVMeta (decodeMeta, data_block.go:1633-1641)
+      to_glb(O.tiering_span_id)[kvb + cn + en] = u_at_any(S, d.span, r);
+      to_glb(O.tiering_attr)[kvb + cn + en] = u_at_any(S, d.attr, r);
     }
     cn += tn;
     ck += tk;

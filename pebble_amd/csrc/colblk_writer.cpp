@@ -17,7 +17,11 @@
 //                        Finish, Size)
 //   BitmapBuilder        sstable/colblk/bitmap.go:280-423 (Set/Size/InvertedSize/Invert/Finish)
 //   BlockEncoder         sstable/colblk/block.go:205-262
-//   DataBlockEncoder     sstable/colblk/data_block.go:600-790 (Init/Reset/Add/Size/Finish)
+//   DataBlockEncoder     sstable/colblk/data_block.go:600-790 (Init/Reset/Add/Size/Finish),
+//                        with the Pebblev8 tiering columns (WithTieringColumns :594-601;
+//                        internalAdd :753-761, Size :782-786, Finish :840-844): span and
+//                        attribute UintBuilders InitWithDefault, the secondary blob
+//                        handles a RawBytesBuilder
 //   defaultKeyWriter     sstable/colblk/data_block.go:230-345
 //   cockroachKeyWriter   cockroachkvs/cockroachkvs.go:575-766 (ComparePrev/WriteKey/FinishHeader)
 //   KeyGenConfig         cockroachkvs/test_utils.go (RandomKVs, randRoachKey, randTimestamp)
@@ -480,7 +484,8 @@ struct CrdbKeyWriter : KeyWriter {  // cockroachkvs.go:575-766
 };
 
 constexpr uint32_t kDataBlockCustomHeaderSize = 4;  // data_block.go:607
-constexpr int kFormatCols = 5;                        // trailer, prefixChanged, values, isValueExternal, isObsolete
+constexpr int kFormatCols = 5;     // trailer, prefixChanged, values, isValueExternal, isObsolete (dataBlockColumnMaxV1)
+constexpr int kFormatColsV2 = 8;   // + tieringSpanID, tieringAttribute, secondaryBlobHandle (dataBlockColumnMaxV2)
 
 }  // namespace
 
@@ -489,6 +494,10 @@ struct pbl_colblk_writer {
   UintB trailers;
   BitmapB prefix_same, is_value_external, is_obsolete;
   RawBytesB values;
+  // Pebblev8 tiering columns (OptionalColumnConfig.SupportsTiering)
+  bool tiering = false;
+  UintB tiering_span, tiering_attr;
+  RawBytesB secondary_handles;
   int rows = 0;
   uint32_t max_key_len = 0;
   uint32_t schema = 0;
@@ -498,6 +507,9 @@ struct pbl_colblk_writer {
     else kw = new DefaultKeyWriter(bundle);
     trailers.init(false);
     values.init();
+    tiering_span.init(true);
+    tiering_attr.init(true);
+    secondary_handles.init();
   }
   ~pbl_colblk_writer() { delete kw; }
   void reset() {
@@ -507,11 +519,15 @@ struct pbl_colblk_writer {
     values.reset();
     is_value_external.reset();
     is_obsolete.reset();
+    tiering_span.reset();
+    tiering_attr.reset();
+    secondary_handles.reset();
     rows = 0;
     max_key_len = 0;
   }
+  int format_cols() const { return tiering ? kFormatColsV2 : kFormatCols; }  // numFormatColumns
   uint32_t header_size() const {
-    return uint32_t(7 + 5 * (kw->ncols() + kFormatCols)) + kDataBlockCustomHeaderSize + uint32_t(kw->header_size());
+    return uint32_t(7 + 5 * (kw->ncols() + format_cols())) + kDataBlockCustomHeaderSize + uint32_t(kw->header_size());
   }
   uint32_t size_for(int r) const {  // DataBlockEncoder.Size at `r` rows
     uint32_t off = header_size();
@@ -521,6 +537,11 @@ struct pbl_colblk_writer {
     off = values.size(r, off);
     off = is_value_external.size(r, off);
     off = is_obsolete.size(r, off);
+    if (tiering) {
+      off = tiering_span.size(r, off);
+      off = tiering_attr.size(r, off);
+      off = secondary_handles.size(r, off);
+    }
     return off + 1;
   }
 };
@@ -535,9 +556,15 @@ pbl_colblk_writer* pbl_colblk_writer_new(uint32_t schema, int bundle_size) {
 void pbl_colblk_writer_free(pbl_colblk_writer* w) { delete w; }
 void pbl_colblk_writer_reset(pbl_colblk_writer* w) { w->reset(); }
 
-int pbl_colblk_writer_add(pbl_colblk_writer* w, const uint8_t* key, size_t key_len, int64_t prefix_len,
-                          uint64_t trailer, const uint8_t* value, size_t value_len, int value_kind,
-                          int is_obsolete) {
+void pbl_colblk_writer_set_tiering(pbl_colblk_writer* w, int tiering) { w->tiering = tiering != 0; }
+
+}  // extern "C"
+
+namespace {
+// DataBlockEncoder.internalAdd (data_block.go:730-765)
+int add_row(pbl_colblk_writer* w, const uint8_t* key, size_t key_len, int64_t prefix_len, uint64_t trailer,
+            const uint8_t* value, size_t value_len, int value_kind, int is_obsolete, uint64_t span, uint64_t attr,
+            const uint8_t* handle, size_t handle_len) {
   if (key_len == 0) return PBL_INVALID_ARG;
   int kl = int(key_len);
   KCmp c = w->kw->compare_prev(key, kl, int(prefix_len));
@@ -554,9 +581,33 @@ int pbl_colblk_writer_add(pbl_colblk_writer* w, const uint8_t* key, size_t key_l
   } else {
     w->values.put(value, value_len);
   }
+  if (w->tiering) {
+    if (attr != 0) {  // meta.IsSet() (internal/base/internal.go:700-702)
+      w->tiering_span.set(w->rows, span);
+      w->tiering_attr.set(w->rows, attr);
+    }
+    w->secondary_handles.put(handle, handle ? handle_len : 0);
+  }
   if (key_len > w->max_key_len) w->max_key_len = uint32_t(key_len);
   w->rows++;
   return c.prefix_equal() ? 1 : 0;
+}
+}  // namespace
+
+extern "C" {
+
+int pbl_colblk_writer_add(pbl_colblk_writer* w, const uint8_t* key, size_t key_len, int64_t prefix_len,
+                          uint64_t trailer, const uint8_t* value, size_t value_len, int value_kind,
+                          int is_obsolete) {
+  return add_row(w, key, key_len, prefix_len, trailer, value, value_len, value_kind, is_obsolete, 0, 0, nullptr, 0);
+}
+
+int pbl_colblk_writer_add_meta(pbl_colblk_writer* w, const uint8_t* key, size_t key_len, int64_t prefix_len,
+                               uint64_t trailer, const uint8_t* value, size_t value_len, int value_kind,
+                               int is_obsolete, uint64_t tiering_span_id, uint64_t tiering_attr,
+                               const uint8_t* secondary_handle, size_t secondary_handle_len) {
+  return add_row(w, key, key_len, prefix_len, trailer, value, value_len, value_kind, is_obsolete, tiering_span_id,
+                 tiering_attr, secondary_handle, secondary_handle_len);
 }
 
 uint32_t pbl_colblk_writer_rows(const pbl_colblk_writer* w) { return uint32_t(w->rows); }
@@ -571,7 +622,7 @@ size_t pbl_colblk_writer_finish(pbl_colblk_writer* w, uint32_t rows, uint8_t* ds
   if (!dst || dst_cap < size) return size;
   std::vector<uint8_t> buf(size, 0);
   uint8_t* b = buf.data();
-  int cols = w->kw->ncols() + kFormatCols;
+  int cols = w->kw->ncols() + w->format_cols();
   w->prefix_same.invert(r);
   uint32_t custom = kDataBlockCustomHeaderSize + uint32_t(w->kw->header_size());
   b[custom] = 1;  // Version1
@@ -594,6 +645,11 @@ size_t pbl_colblk_writer_finish(pbl_colblk_writer* w, uint32_t rows, uint8_t* ds
   col(kTypeBytes); poff = w->values.finish(r, poff, b);
   col(kTypeBool);  poff = w->is_value_external.finish(r, poff, b);
   col(kTypeBool);  poff = w->is_obsolete.finish(r, poff, b);
+  if (w->tiering) {
+    col(kTypeUint);  poff = w->tiering_span.finish(r, poff, b);
+    col(kTypeUint);  poff = w->tiering_attr.finish(r, poff, b);
+    col(kTypeBytes); poff = w->secondary_handles.finish(r, poff, b);
+  }
   b[poff++] = 0;  // block padding byte
   if (poff != size) return 0;
   std::memcpy(dst, b, size);
@@ -661,6 +717,7 @@ extern "C" uint64_t pbl_gen_col_blocks(const pbl_colgen_config* cfgp, uint32_t s
   std::vector<uint64_t> counts(n_threads, 0);
   auto work = [&](int t) {
     pbl_colblk_writer w(schema, 16);
+    w.tiering = cfg.tiering != 0;
     std::vector<std::string> keys;
     std::vector<uint8_t> val(cfg.value_len);
     for (uint32_t b = t; b < n_blocks; b += n_threads) {
@@ -676,8 +733,14 @@ extern "C" uint64_t pbl_gen_col_blocks(const pbl_colgen_config* cfgp, uint32_t s
         for (auto& x : val) x = uint8_t(sm64(s));
         uint64_t seq = (uint64_t(b) << 20) + k;
         bool obs = (prev && *prev == keys[k]) || (cfg.obsolete_every && k % cfg.obsolete_every == cfg.obsolete_every - 1);
-        pbl_colblk_writer_add(&w, reinterpret_cast<const uint8_t*>(keys[k].data()), keys[k].size(), -1,
-                              (seq << 8) | 1, val.data(), val.size(), 0, obs);
+        uint64_t span = 0, attr = 0;
+        if (cfg.tiering) {
+          const uint64_t r = sm64(s);
+          span = 1 + r % cfg.tiering;
+          attr = (r >> 32) % 10 == 0 ? 0 : cfg.base_wall_time / 1000000000ull + (r >> 8) % 3600;
+        }
+        add_row(&w, reinterpret_cast<const uint8_t*>(keys[k].data()), keys[k].size(), -1, (seq << 8) | 1, val.data(),
+                val.size(), 0, obs, span, attr, nullptr, 0);
         prev = &keys[k];
         if (w.size_for(w.rows) > block_size) break;
       }

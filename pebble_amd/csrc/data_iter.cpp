@@ -11,7 +11,9 @@
 // :1504-1635 after a forward walk off the end); SeekPrefixGE / NextWithSamePrefix
 // / NextPrefix / IsLowerBound as :542-598, :1204-1218; HideObsoletePoints
 // (blockiter.Transforms) skips KVs whose trailer carried the obsolete bit
-// (PBL_KV_OBSOLETE), as :1168-1179.  Comparers: base.DefaultComparer
+// (PBL_KV_OBSOLETE), as :1168-1179.  *_with_meta: colblk.DataBlockIter's
+// FirstWithMeta / NextWithMeta / SeekGEWithMeta (sstable/colblk/data_block.go:
+// 1574-1600, decodeMeta :1633-1641) over the decoded KVMeta arrays.  Comparers: base.DefaultComparer
 // (internal/base/comparer.go: bytes.Compare, Split = len), testkeys.Comparer
 // (internal/testkeys/testkeys.go:136-171) and cockroachkvs.Comparer
 // (cockroachkvs/cockroachkvs.go:298-339, :479-...).
@@ -30,6 +32,8 @@ struct pbl_data_iter {
   const uint32_t* val_off = nullptr;
   const uint8_t* key_bytes = nullptr;  // this block's bytes
   const uint8_t* val_bytes = nullptr;
+  const uint64_t* span = nullptr;  // KVMeta arrays (NULL: not decoded, KVMeta{})
+  const uint64_t* attr = nullptr;
   int64_t n = 0;
   int64_t i = -1;  // -1: before the first KV; n: past the last
   uint32_t cmp = PBL_CMP_DEFAULT;
@@ -199,6 +203,10 @@ int pbl_data_iter_init(pbl_data_iter* it, const pbl_decode_out* host, uint32_t n
   it->val_off = host->val_off + kv0 + block;
   it->key_bytes = host->key_bytes + host->blk_key_base[block];
   it->val_bytes = host->val_bytes + host->blk_val_base[block];
+  if (host->tiering_span_id && host->tiering_attr) {
+    it->span = host->tiering_span_id + kv0;
+    it->attr = host->tiering_attr + kv0;
+  }
   it->cmp = comparer;
   it->hide_obsolete = hide_obsolete_points != 0;
   it->invalidated = false;
@@ -233,6 +241,32 @@ const pbl_kv* pbl_data_iter_seek_lt(pbl_data_iter* it, const uint8_t* key, uint6
   (void)flags;
   it->has_pfx = false;
   return it->invalidated ? nullptr : bwd(it, lower(it, key, key_len, false) - 1);
+}
+}  // extern "C"
+
+namespace {
+// decodeMeta (data_block.go:1633-1641): the KV's meta, KVMeta{} when there is none
+const pbl_kv* with_meta(const pbl_data_iter* it, const pbl_kv* kv, pbl_kv_meta* meta) {
+  meta->tiering_span_id = meta->tiering_attribute = 0;
+  if (kv && it->span) {
+    meta->tiering_span_id = it->span[it->i];
+    meta->tiering_attribute = it->attr[it->i];
+  }
+  return kv;
+}
+}  // namespace
+
+extern "C" {
+
+const pbl_kv* pbl_data_iter_first_with_meta(pbl_data_iter* it, pbl_kv_meta* meta) {
+  return with_meta(it, pbl_data_iter_first(it), meta);
+}
+const pbl_kv* pbl_data_iter_next_with_meta(pbl_data_iter* it, pbl_kv_meta* meta) {
+  return with_meta(it, pbl_data_iter_next(it), meta);
+}
+const pbl_kv* pbl_data_iter_seek_ge_with_meta(pbl_data_iter* it, const uint8_t* key, uint64_t key_len,
+                                              uint32_t flags, pbl_kv_meta* meta) {
+  return with_meta(it, pbl_data_iter_seek_ge(it, key, key_len, flags), meta);
 }
 const pbl_kv* pbl_data_iter_seek_prefix_ge(pbl_data_iter* it, const uint8_t* key, uint64_t key_len, uint32_t flags,
                                            int* prefix_did_not_match) {

@@ -155,16 +155,23 @@ __device__ __forceinline__ void big_block_publish(const Args& A, uint32_t b, con
   }
 }
 
-__device__ __forceinline__ bool big_block_count(const Args& A, uint32_t b, lptr<uint8_t> keybuf, uint32_t keycap,
+// The count walk of a big block; a block failing Iter.Init's checks (zero
+// restarts, a restart table past the block, a bad first entry) gets that
+// status and a zero aggregate, which big_block_publish publishes like any other.
+__device__ __forceinline__ void big_block_count(const Args& A, uint32_t b, lptr<uint8_t> keybuf, uint32_t keycap,
                                                 SlowState* ss) {
   const uint32_t blen = A.in.block_len[b];
   const uint8_t* gblk = A.in.blocks + A.in.block_off[b];
   uint32_t roff, nres;
-  if (init_checks(GlbRd{gblk}, blen, A.in.flags, &roff, &nres) != PBL_OK) return false;  // (parse_block's error path publishes)
+  const uint32_t st = init_checks(GlbRd{gblk}, blen, A.in.flags, &roff, &nres);
+  if (st != PBL_OK) {
+    ss->nkv = ss->kb = ss->vb = ss->nr = 0;
+    ss->status = st;
+    return;
+  }
   const uint64_t dummy[kNumComp] = {0, 0, 0, 0};
   slow_walk_t<SlowGlb, 1>(SlowGlb{to_glb(gblk), blen}, blen, A.in.flags, A.in.synthetic_seq_num, keybuf, keycap, kPassCount,
                           A.out, b, dummy, ss);
-  return true;
 }
 
 __global__ void __launch_bounds__(kWave) big_block_sizes_kernel(Args A) {
@@ -181,7 +188,7 @@ __global__ void __launch_bounds__(kWave) big_block_sizes_kernel(Args A) {
       const uint32_t b = uint32_t(base) + uint32_t(__builtin_ctzll(big));
       big &= big - 1;
       SlowState ss;
-      if (!big_block_count(A, b, to_lds_ptr(reinterpret_cast<uint8_t*>(keybuf4)), kBigKeySmall, &ss)) continue;
+      big_block_count(A, b, to_lds_ptr(reinterpret_cast<uint8_t*>(keybuf4)), kBigKeySmall, &ss);
       if (ss.status == PBL_UNSUPPORTED) {  // a key past the small buffer (or a total past 4 GiB): tier 2
         if (lane_id() == 0) to_glb(redo)[g_atomic_add(hdr + kWsBigRedo, 1u)] = b;
         continue;
@@ -201,8 +208,8 @@ __global__ void __launch_bounds__(kWave) big_block_sizes2_kernel(Args A) {
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     const uint32_t b = to_glb(redo)[i];
     SlowState ss;
-    if (big_block_count(A, b, to_lds_ptr(reinterpret_cast<uint8_t*>(keybuf4)), uint32_t(kLdsBlkBytes), &ss))
-      big_block_publish(A, b, ss);
+    big_block_count(A, b, to_lds_ptr(reinterpret_cast<uint8_t*>(keybuf4)), uint32_t(kLdsBlkBytes), &ss);
+    big_block_publish(A, b, ss);
   }
 }
 

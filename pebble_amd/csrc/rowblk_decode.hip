@@ -265,7 +265,7 @@ mixed_col_size_kernel(Args A, const uint32_t* ids) {
     const uint32_t blen = to_glb(A.in.block_len)[b];
     const uint32_t schema = to_glb(A.in.block_format)[b];
     const col::Src S{nullptr, nullptr, (col::glb_cu8)(A.in.blocks + to_glb(A.in.block_off)[b]), 0u, 0xffffffffu, blen};
-    uint32_t st = col::parse_block_wave(S, schema, &d);
+    uint32_t st = col::parse_block_wave(S, schema, (A.in.flags & PBL_COL_TIERING) != 0, &d);
     const uint32_t rows = st == PBL_OK ? d.rows : 0;
     uint64_t kb = 0, nv = 0, vb = 0;
     bool bad = false;
@@ -309,6 +309,23 @@ __global__ void __launch_bounds__(kTPB, PBL_COL_PIPE_WG) mixed_col_kernel(Args A
   uint32_t* hdr = reinterpret_cast<uint32_t*>(A.out.workspace);
   const uint32_t n_row = __hip_atomic_load(to_glb(hdr) + kWsRowCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   col::cpipe::col_pipe_body<ListQueue, false, kHide>(L, A, ListQueue{hdr + kWsColTick2, ids + n_row, nb - n_row, nb});
+}
+
+// KVMeta{} for the row blocks' KVs (rowblk.Iter has no meta columns) when the
+// caller asked for the tiering arrays: one wave per block, after the decode
+// (a block that did not decode has no KV range).
+__global__ void __launch_bounds__(kWave) row_meta_zero_kernel(Args A) {
+  const pbl_decode_out& O = A.out;
+  const uint32_t nb = A.in.n_blocks;
+  for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const uint32_t fmt = A.in.block_format ? uint32_t(to_glb(A.in.block_format)[b]) : A.in.format;
+    if (fmt != PBL_FMT_ROW || to_glb(O.blk_status)[b] != PBL_OK) continue;
+    const uint64_t k0 = to_glb(O.blk_kv_base)[b], k1 = to_glb(O.blk_kv_base)[b + 1];
+    for (uint64_t k = k0 + lane_id(); k < k1; k += kWave) {
+      to_glb(O.tiering_span_id)[k] = 0;
+      to_glb(O.tiering_attr)[k] = 0;
+    }
+  }
 }
 
 // Size pass epilogue: a block that decoded reports PBL_OK, not the forced
@@ -496,7 +513,7 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
   if (batch->n_blocks == 0) return PBL_OK;
   if (!batch->blocks || !batch->block_off || !batch->block_len || !out->trailer || !out->key_off ||
       !out->val_off || !out->key_bytes || !out->val_bytes || !out->workspace ||
-      out->workspace_bytes < pbl::ws_alloc_bytes(batch->n_blocks))
+      out->workspace_bytes < pbl::ws_alloc_bytes(batch->n_blocks) || (!out->tiering_span_id != !out->tiering_attr))
     return PBL_INVALID_ARG;
   if (!batch->block_format && batch->format != PBL_FMT_ROW) return pbl_decode_batch_colblk(batch, out, stream);
   if (hipMemsetAsync(out->workspace, 0, pbl::ws_bytes(batch->n_blocks), st) != hipSuccess)
@@ -504,7 +521,11 @@ int pbl_decode_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* st
   pbl::Args a;
   a.in = *batch;
   a.out = *out;
-  return batch->block_format ? launch_mixed(batch, a, st, true) : launch_row(a, st, true);
+  const int rc = batch->block_format ? launch_mixed(batch, a, st, true) : launch_row(a, st, true);
+  if (rc != PBL_OK || !out->tiering_span_id) return rc;
+  const uint32_t g = batch->n_blocks < 8192 ? batch->n_blocks : 8192;
+  hipLaunchKernelGGL(pbl::row::row_meta_zero_kernel, dim3(g), dim3(pbl::kWave), 0, st, a);
+  return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }
 
 int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stream) {
@@ -528,6 +549,8 @@ int pbl_size_batch(const pbl_block_batch* batch, pbl_decode_out* out, void* stre
   o.key_bytes = nullptr;
   o.val_bytes = nullptr;
   o.restarts = nullptr;
+  o.tiering_span_id = nullptr;
+  o.tiering_attr = nullptr;
   o.kv_cap = o.key_cap = o.val_cap = o.rst_cap = 0;
   if (hipMemsetAsync(o.totals, 0, sizeof(pbl_totals), st) != hipSuccess) return PBL_DEVICE_ERROR;
   if (hipMemsetAsync(o.workspace, 0, pbl::ws_bytes(batch->n_blocks), st) != hipSuccess) return PBL_DEVICE_ERROR;
@@ -566,6 +589,7 @@ size_t pbl_struct_layout(uint64_t* out, size_t cap) {
       PBL_OFF(pbl_decode_out, blk_status), PBL_OFF(pbl_decode_out, totals), PBL_OFF(pbl_decode_out, kv_cap),
       PBL_OFF(pbl_decode_out, key_cap), PBL_OFF(pbl_decode_out, val_cap), PBL_OFF(pbl_decode_out, rst_cap),
       PBL_OFF(pbl_decode_out, workspace), PBL_OFF(pbl_decode_out, workspace_bytes),
+      PBL_OFF(pbl_decode_out, tiering_span_id), PBL_OFF(pbl_decode_out, tiering_attr),
       sizeof(pbl_transforms), PBL_OFF(pbl_transforms, synthetic_seq_num),
       PBL_OFF(pbl_transforms, hide_obsolete_points), PBL_OFF(pbl_transforms, split), PBL_OFF(pbl_transforms, prefix),
       PBL_OFF(pbl_transforms, suffix), PBL_OFF(pbl_transforms, prefix_len), PBL_OFF(pbl_transforms, suffix_len),
@@ -583,7 +607,8 @@ size_t pbl_struct_layout(uint64_t* out, size_t cap) {
       sizeof(pbl_value_out), PBL_OFF(pbl_value_out, val_off), PBL_OFF(pbl_value_out, val_bytes),
       PBL_OFF(pbl_value_out, blk_val_base), PBL_OFF(pbl_value_out, blk_status), PBL_OFF(pbl_value_out, val_cap),
       sizeof(pbl_kv), PBL_OFF(pbl_kv, user_key), PBL_OFF(pbl_kv, user_key_len), PBL_OFF(pbl_kv, trailer),
-      PBL_OFF(pbl_kv, value), PBL_OFF(pbl_kv, value_len), PBL_OFF(pbl_kv, kv_flags), PBL_OFF(pbl_kv, reserved)};
+      PBL_OFF(pbl_kv, value), PBL_OFF(pbl_kv, value_len), PBL_OFF(pbl_kv, kv_flags), PBL_OFF(pbl_kv, reserved),
+      sizeof(pbl_kv_meta), PBL_OFF(pbl_kv_meta, tiering_span_id), PBL_OFF(pbl_kv_meta, tiering_attribute)};
 #undef PBL_OFF
   const size_t n = sizeof(v) / sizeof(v[0]);
   for (size_t i = 0; i < n && i < cap && out; i++) out[i] = v[i];

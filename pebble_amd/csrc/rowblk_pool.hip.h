@@ -962,10 +962,16 @@ __device__ __noinline__ void block_big(const Args A, uint32_t b, uint64_t boff, 
     SlowState ss;
     slow_walk_t<SlowGlb, PBL_BIG_U>(SlowGlb{to_glb(A.in.blocks + boff), blen}, blen, A.in.flags,
                                     A.in.synthetic_seq_num, to_lds_ptr(keybuf), keycap, kPassAll, O, b, excl, &ss);
-    if (ss.status != PBL_OK && l == 0) {
+    if (ss.status == PBL_UNSUPPORTED && l == 0) {  // a key past the slot: the values pass rewrites the block
       uint32_t* hdr = reinterpret_cast<uint32_t*>(O.workspace);
       uint32_t* pend = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(O.workspace) + ws_pend_offset(nb));
       to_glb(pend)[g_atomic_add(hdr + rowc::kWsBigPend, 1u)] = b;
+    } else if (ss.status != PBL_OK && l == 0) {
+      // the same walk as the sizes pass over the same bytes cannot disagree
+      // with it; if it ever did, the block reports the walk's status
+      to_glb(O.blk_status)[b] = ss.status;
+      g_atomic_or(&O.totals->status_mask, 1u << ss.status);
+      g_atomic_add(&O.totals->n_bad_blocks, 1u);
     }
   }
 }

@@ -423,6 +423,10 @@ __global__ void __launch_bounds__(kTPB) tf_scatter_kernel(TfArgs A) {
         to_glb(O.trailer)[k] = v.tr;
         if (O.kv_flags) to_glb(O.kv_flags)[k] = v.fl;
         if (O.entry_off && I.entry_off) to_glb(O.entry_off)[k] = to_glb(I.entry_off)[kv0 + j];
+        if (O.tiering_span_id && I.tiering_span_id) {  // KVMeta travels with its KV
+          to_glb(O.tiering_span_id)[k] = to_glb(I.tiering_span_id)[kv0 + j];
+          to_glb(O.tiering_attr)[k] = to_glb(I.tiering_attr)[kv0 + j];
+        }
         to_glb(O.key_off)[okv + b + jo + rank] = ko;
         to_glb(O.val_off)[okv + b + jo + rank] = vo;
         // key: F[:p] ++ (suffix | F[p:]),  F = prefix ++ key
@@ -485,6 +489,7 @@ int pbl_transform_batch(const pbl_decode_out* in, uint32_t n_blocks, const pbl_t
       out->workspace_bytes < pbl_transform_workspace_bytes(n_blocks))
     return PBL_INVALID_ARG;
   if (t->hide_obsolete_points && !in->kv_flags) return PBL_INVALID_ARG;
+  if (!in->tiering_span_id != !in->tiering_attr || !out->tiering_span_id != !out->tiering_attr) return PBL_INVALID_ARG;
   if ((t->prefix_len && !t->prefix) || (t->suffix_len && !t->suffix) || t->split > PBL_SPLIT_CRDB)
     return PBL_INVALID_ARG;
   if (t->synthetic_seq_num >> 56) return PBL_INVALID_ARG;  // base.SeqNumMax

@@ -48,7 +48,7 @@ class TransformPlan:
         st = stream if stream is not None else torch.cuda.current_stream(dev)
         with torch.cuda.stream(st):
             out = DecodedBatch.allocate(d.n_blocks, cap, dev, entry_off=d.entry_off is not None,
-                                        restarts=d.restarts is not None)
+                                        restarts=d.restarts is not None, meta=d.tiering_span_id is not None)
             ws = int(N.lib().pbl_transform_workspace_bytes(d.n_blocks))
             if out.workspace.numel() < ws:
                 out.workspace = torch.empty(ws, dtype=torch.uint8, device=dev)

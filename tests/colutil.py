@@ -170,3 +170,39 @@ def embed_column(col: int, col_bytes: bytes, col_offset: int, rows: int, max_key
         if col == COL_PREFIX or start % 8 == col_offset % 8:
             return assemble_block(cols, rows, max(max_key_len, tail))
     raise AssertionError("unreachable")
+
+
+# ---- Pebblev8 tiering columns ------------------------------------------------------
+def random_metas(rng: random.Random, n: int):
+    """Random base.KVMeta per row (span, attribute), widths 0..8 bytes; about a
+    fifth unset (attribute 0: KVMeta.IsSet false, internal/base/internal.go:700)."""
+    out = []
+    big = rng.choice([1, 300, 70000, 1 << 40])
+    for _ in range(n):
+        if rng.random() < 0.2:
+            out.append((rng.randrange(big), 0))
+        else:
+            out.append((rng.randrange(big), 1 + rng.randrange(big)))
+    return out
+
+
+def build_block_meta(schema: int, rows, metas, bundle: int = 16, handles=None):
+    """A Pebblev8 block (tiering columns): returns (block bytes, expected decode
+    as build_block, expected KVMeta per row).  The writer stores a meta only
+    when its attribute is set (data_block.go:753-757), so an unset one reads
+    back as KVMeta{} whatever its span."""
+    w = DataBlockEncoder(schema, bundle, tiering=True)
+    exp = []
+    for i, ((k, tr, v, vk, obs), m) in enumerate(zip(rows, metas)):
+        h = handles[i] if handles else b""
+        pe = w.add(k, tr, v, vk, obs, meta=m, secondary_handle=h)
+        fl = 0 if pe else N.PBL_KV_PREFIX_CHANGED
+        if obs:
+            fl |= N.PBL_KV_OBSOLETE
+        val = v
+        if vk != VALUE_IN_PLACE:
+            vp = (0x80 if vk == VALUE_BLOCK_HANDLE else 0x40) | (0x20 if pe else 0)
+            val = bytes([vp]) + v
+            fl |= N.PBL_KV_VALBLK_HANDLE if vk == VALUE_BLOCK_HANDLE else N.PBL_KV_BLOB_HANDLE
+        exp.append((expected_key(schema, k), tr, val, fl, i))
+    return w.finish(), exp, [m if m[1] else (0, 0) for m in metas]

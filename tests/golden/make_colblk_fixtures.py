@@ -14,6 +14,8 @@ reference's test wrote into that block:
   cockroachkvs/testdata/block_encoding   cockroachkvs.KeySchema ("crdb1")
         writer input:  the `init` lines; expected decode: the `keys` output
         (cockroachkvs_test.go formatUserKey: `roachKey @ HEXVERSION #seq,KIND = value`)
+  sstable/testdata/writer_tiering_histogram   Pebblev8 blocks with the tiering columns
+        (`layout` dumps; tiering_cases below), plus the tiering KV/meta KATs
 
 The expected per-row output is derived from the writer input alone (never from
 the dump), so a decoder that reproduces it from the dumped bytes is pinned to
@@ -327,14 +329,120 @@ def transform_cases():
     return out
 
 
+TIER = re.compile(r";tiering:span=(\d+),attr=(\d+)$")
+
+
+def _tier_meta(value: str):
+    """testkeys.ExtractKVMeta (sstable/test_utils.go:182-186): a value ending in
+    ";tiering:span=S,attr=A" carries KVMeta{S, A}; the value keeps the text."""
+    m = TIER.search(value)
+    return (int(m.group(1)), int(m.group(2))) if m else (0, 0)
+
+
+def _layout_data_blocks(text: str):
+    """The `data` entries of a `layout` dump: (hex-dump text, KV lines) each."""
+    out, cur = [], None
+    for line in text.split("\n"):
+        if line.startswith(" ├── data ") or line.startswith(" └── data "):
+            cur = {"dump": [], "kvs": []}
+            out.append(cur)
+            continue
+        if line.startswith(" ├── ") or line.startswith(" └── "):
+            cur = None
+            continue
+        if cur is None:
+            continue
+        if LINE.search(line):
+            cur["dump"].append(line)
+        else:
+            m = re.match(r"^ │    [├└]── (\S.*)$", line)
+            if m and "#" in m.group(1) and not m.group(1).startswith("trailer"):
+                cur["kvs"].append(m.group(1))
+    return [("\n".join(b["dump"]), b["kvs"]) for b in out]
+
+
+def tiering_cases():
+    """Pebblev8 data blocks with the tiering columns (sstable/format.go:305-316;
+    data_block.go:514-525), recovered byte-for-byte from the only whole-block
+    dumps of that layout the reference holds: the `layout` outputs of
+    sstable/testdata/writer_tiering_histogram (DefaultKeySchema(testkeys, 16),
+    writer input from the preceding `build`).  Expected rows come from the
+    writer input: key and trailer, the value (in place: the input text; a
+    dual-tier blob value: the dumped column slice, isValueExternal), and the
+    KVMeta the writer stored (ExtractKVMeta; KVMeta{} without a tiering suffix).
+    Also the KV + meta KATs with no dump: colblk/data_block_meta_test.go:27-33
+    (TestDataBlockIterWithMeta) and the `build` / `scan-compaction` pair of
+    sstable/testdata/writer_v8:388-402 (NextWithMeta's output)."""
+    path = os.path.join(REF, "sstable/testdata/writer_tiering_histogram")
+    rel = os.path.relpath(path, REF)
+    blocks, build = [], None
+    for c in parse_datadriven(path):
+        verb = c["cmd"].split()[0]
+        if verb == "build":
+            build = c
+        elif verb == "layout" and "data for column" in c["expected"]:
+            lines = [l for l in build["input"].split("\n") if l]
+            for dump, kv_lines in _layout_data_blocks(c["expected"]):
+                blk = dump_to_bytes(dump)
+                rows, prev = [], None
+                exact = True
+                for i, line in enumerate(lines[: len(kv_lines)]):
+                    j = line.index(":")
+                    ukey, trailer = parse_ikey(line[:j])
+                    text = line[j + 1:]
+                    pl = testkeys_split(ukey)
+                    row = {"key": ukey.hex(), "trailer": trailer, "obsolete": False, "prefix_len": pl,
+                           "prefix_changed": prev is None or prev[:testkeys_split(prev)] != ukey[:pl]}
+                    if text.startswith("hot-blob{"):
+                        exact = False
+                        row.update(value=None, external=True, span=0, attr=0, dump_value=True)
+                    else:
+                        sp, at = _tier_meta(text)
+                        row.update(value=text.encode().hex(), external=False, span=sp, attr=at, vp=-1)
+                    rows.append(row)
+                    prev = ukey
+                blocks.append({"name": f"writer_tiering_histogram:{c['line']}", "source": f"{rel}:{build['line']}-{c['line']}",
+                               "schema": "default", "bundle_size": 16, "block": blk.hex(), "rows": rows,
+                               "encoder_exact": exact})
+    kats = [{"source": "sstable/colblk/data_block_meta_test.go:27-33", "schema": "default", "bundle_size": 16,
+             "kvs": [["a#1,SET", "value", 42, 100], ["b#2,SET", "value", 43, 200], ["c#3,SET", "value", 0, 0]]}]
+    path = os.path.join(REF, "sstable/testdata/writer_v8")
+    rel = os.path.relpath(path, REF)
+    build = None
+    for c in parse_datadriven(path):
+        verb = c["cmd"].split()[0]
+        if verb == "build":
+            build = c
+        elif verb == "scan-compaction":
+            kvs = []
+            for line in c["expected"].split("\n"):
+                if not line:
+                    continue
+                kv, _, meta = line.rpartition(" meta=")
+                j = kv.index(":")
+                if meta == "<no meta>":
+                    sp, at = 0, 0
+                else:
+                    m = re.fullmatch(r"tiering:span=(\d+),attr=(\d+)", meta)
+                    sp, at = int(m.group(1)), int(m.group(2))
+                kvs.append([kv[:j], kv[j + 1:], sp, at])
+            inp = [l for l in build["input"].split("\n") if l]
+            assert [k[0] + ":" + k[1] for k in kvs] == inp
+            kats.append({"source": f"{rel}:{build['line']}-{c['line']}", "schema": "default", "bundle_size": 16,
+                         "kvs": kvs})
+    return {"blocks": blocks, "kats": kats}
+
+
 def main():
     cases = data_block_cases() + crdb1_cases()
-    res = {"data_blocks": cases, "codecs": codec_cases(), "transforms": transform_cases()}
+    res = {"data_blocks": cases, "codecs": codec_cases(), "transforms": transform_cases(),
+           "tiering": tiering_cases()}
     p = os.path.join(HERE, "colblk_golden.json")
     with open(p, "w") as f:
         json.dump(res, f, indent=1)
     print("wrote", p, len(cases), "data blocks,", {k: len(v) for k, v in res["codecs"].items()}, "codec dumps,",
-          sum(len(t["iters"]) for t in res["transforms"]), "transform scans")
+          sum(len(t["iters"]) for t in res["transforms"]), "transform scans,",
+          len(res["tiering"]["blocks"]), "tiering blocks,", len(res["tiering"]["kats"]), "tiering KATs")
 
 
 if __name__ == "__main__":

@@ -57,7 +57,7 @@ def test_ctypes_struct_layouts_match_library():
     v = list(buf[:n])
     exp = []
     for S in (N.BlockBatchC, N.TotalsC, N.DecodeOutC, N.TransformsC, N.FooterC, N.IndexOutC, N.KvOutC,
-              N.ValueOutC, N.KvC):
+              N.ValueOutC, N.KvC, N.KvMetaC):
         exp.append(ctypes.sizeof(S))
         exp += [getattr(S, f).offset for f, _ in S._fields_]
     assert v == exp

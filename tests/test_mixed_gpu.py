@@ -15,7 +15,6 @@ from pebble_amd.rowblk import gen_row_blocks
 from test_rowblk_gpu import assert_same, pack
 
 pytestmark = pytest.mark.gpu
-KERNELS = {"default": 0}
 
 
 def gpu(buf, off, lens, bf, flags=0, cap=None, exact=False):
@@ -24,12 +23,12 @@ def gpu(buf, off, lens, bf, flags=0, cap=None, exact=False):
     return decode(b, cap=cap, exact=exact).to_host()
 
 
-def check(blocks, fmts, kernel, align=8, ctx="", **kw):
+def check(blocks, fmts, align=8, ctx="", **kw):
     buf, off, lens = pack(blocks, align)
     bf = np.array(fmts, np.uint8)
     o = oracle.decode_batch(buf, off, lens, N.PBL_FMT_ROW, bf)
-    g = gpu(buf, off, lens, bf, KERNELS[kernel], **kw)
-    assert_same(g, o, f"{ctx} kernel={kernel}")
+    g = gpu(buf, off, lens, bf, **kw)
+    assert_same(g, o, ctx)
     return g
 
 
@@ -41,8 +40,7 @@ def pool(seed, n_row, n_col, size=8192):
     return rows, cols
 
 
-@pytest.mark.parametrize("kernel", list(KERNELS))
-def test_mixed_shapes(kernel):
+def test_mixed_shapes():
     rows, cols = pool(1, 40, 40)
     rng = random.Random(2)
     dflt = build_block(SCHEMA_DEFAULT, random_rows(rng, SCHEMA_DEFAULT, 150))[0]
@@ -57,11 +55,10 @@ def test_mixed_shapes(kernel):
     }
     for name, (blocks, fmts) in cases.items():
         for align in (8, 1):
-            check(blocks, fmts, kernel, align, name)
+            check(blocks, fmts, align, name)
 
 
-@pytest.mark.parametrize("kernel", list(KERNELS))
-def test_mixed_random_across_split_chunks(kernel):
+def test_mixed_random_across_split_chunks():
     """> 4096 blocks: the format split spans several chunks."""
     rows, cols = pool(3, 64, 64, 4096)
     rng = random.Random(4)
@@ -71,12 +68,11 @@ def test_mixed_random_across_split_chunks(kernel):
             blocks.append(rng.choice(rows)); fmts.append(N.PBL_FMT_ROW)
         else:
             blocks.append(rng.choice(cols)); fmts.append(N.PBL_FMT_COL_CRDB1)
-    g = check(blocks, fmts, kernel, 8, "random9000")
+    g = check(blocks, fmts, 8, "random9000")
     assert g["status_mask"] == 0
 
 
-@pytest.mark.parametrize("kernel", list(KERNELS))
-def test_mixed_big_and_corrupt_blocks(kernel):
+def test_mixed_big_and_corrupt_blocks():
     """Row blocks past the LDS stage (the big-block passes must skip colblk
     blocks), colblk blocks past the head stage, corrupt blocks of both kinds."""
     rows, cols = pool(5, 8, 8)
@@ -89,13 +85,12 @@ def test_mixed_big_and_corrupt_blocks(kernel):
     blocks = rows[:4] + [big_row] + cols[:4] + [big_col, bad_row, bytes(bad_col)] + rows[4:] + cols[4:] + [big_row]
     R, C, D = N.PBL_FMT_ROW, N.PBL_FMT_COL_CRDB1, N.PBL_FMT_COL_DEFAULT
     fmts = [R] * 4 + [R] + [C] * 4 + [D, R, C] + [R] * 4 + [C] * 4 + [R]
-    g = check(blocks, fmts, kernel, 8, "big+corrupt")
+    g = check(blocks, fmts, 8, "big+corrupt")
     assert g["n_bad_blocks"] >= 1
 
 
 
-@pytest.mark.parametrize("kernel", list(KERNELS))
-def test_mixed_big_blocks_with_long_keys(kernel):
+def test_mixed_big_blocks_with_long_keys():
     """Big row blocks whose keys outgrow the big-block passes' 8 KiB key buffer
     in a mixed batch: the sizes pass lists them for its second tier (the redo
     list has its own workspace area, past the format split's ids, which the
@@ -114,12 +109,52 @@ def test_mixed_big_blocks_with_long_keys(kernel):
     R, C = N.PBL_FMT_ROW, N.PBL_FMT_COL_CRDB1
     blocks = rows[:6] + [big[0]] + cols[:6] + [big[1], big[2]] + rows[6:] + cols[6:] + [big[3]]
     fmts = [R] * 6 + [R] + [C] * 6 + [R, R] + [R] * 6 + [C] * 6 + [R]
-    check(blocks, fmts, kernel, 8, "big long keys")
+    check(blocks, fmts, 8, "big long keys")
 
 def test_mixed_overflow_retry_and_size_pass():
     from pebble_amd.batch import Capacity
     rows, cols = pool(8, 20, 20)
     blocks = [x for p in zip(rows, cols) for x in p]
     fmts = [N.PBL_FMT_ROW, N.PBL_FMT_COL_CRDB1] * 20
-    check(blocks, fmts, "default", 8, "overflow", cap=Capacity(kv=10, key=10, val=10, rst=10))
-    check(blocks, fmts, "default", 8, "exact", exact=True)
+    check(blocks, fmts, 8, "overflow", cap=Capacity(kv=10, key=10, val=10, rst=10))
+    check(blocks, fmts, 8, "exact", exact=True)
+
+
+def _big_row_block(rng, n=6, vlen=9000):
+    from pebble_amd.rowblk import Writer, make_trailer
+    w = Writer(rng.choice([1, 4, 16]))
+    for k in range(n):
+        w.add(b"key%06d" % k, make_trailer(10 + k, 1), bytes([k]) * vlen)
+    blk = w.finish()
+    assert len(blk) > 32768
+    return blk
+
+
+def test_big_row_blocks_failing_init_checks():
+    """Row blocks past the 32 KiB stage that fail rowblk.Iter.Init's checks
+    (rowblk_iter.go:248-256, readFirstKey :418-485): zero restarts, a restart
+    table larger than the block, a first entry with shared != 0, a first key
+    shorter than 8 bytes.  The sizes pass publishes their status and a zero
+    aggregate; every later block is placed after them.  Row and mixed batches."""
+    rng = random.Random(91)
+    rows, cols = pool(9, 6, 6)
+    good = [_big_row_block(rng) for _ in range(3)]
+    bad = []
+    b = bytearray(_big_row_block(rng)); b[-4:] = (0).to_bytes(4, "little"); bad.append(bytes(b))       # no restarts
+    b = bytearray(_big_row_block(rng)); b[-4:] = (1 << 20).to_bytes(4, "little"); bad.append(bytes(b))  # table > block
+    b = bytearray(_big_row_block(rng)); b[0] = 3; bad.append(bytes(b))                                  # shared != 0
+    b = bytearray(_big_row_block(rng)); b[1] = 4; bad.append(bytes(b))                                  # key < 8 bytes
+    b = bytearray(_big_row_block(rng)); b[-4:] = (0x80000001).to_bytes(4, "little"); bad.append(bytes(b))  # bit 31 count
+    R, C = N.PBL_FMT_ROW, N.PBL_FMT_COL_CRDB1
+    blocks = [good[0]] + bad[:2] + rows[:3] + [good[1]] + bad[2:] + rows[3:] + [good[2]]
+    buf, off, lens = pack(blocks)
+    o = oracle.decode_batch(buf, off, lens, N.PBL_FMT_ROW)
+    assert o["n_bad_blocks"] == len(bad)
+    for flags in (0, N.PBL_ROW_HIDE_OBSOLETE):
+        assert_same(gpu(buf, off, lens, None, flags), oracle.decode_batch(buf, off, lens, N.PBL_FMT_ROW, None, flags),
+                    f"row batch flags={flags}")
+    mixed = [good[0], cols[0]] + bad[:2] + [cols[1]] + rows[:3] + [good[1]] + bad[2:] + cols[2:] + [good[2]]
+    fm = [R, C, R, R, C] + [R] * 3 + [R] + [R] * len(bad[2:]) + [C] * 4 + [R]
+    g = check(mixed, fm, 8, "mixed big bad")
+    assert g["n_bad_blocks"] == len(bad)
+    check(mixed, fm, 8, "mixed big bad exact", exact=True)
