@@ -175,11 +175,14 @@ def plumbing(a, world, rank, dist) -> None:
     concat_step -- the same all-gather + rebase as the GPU step, the rebase as a
     CPU-tensor add of shard.exclusive_bases.  Rank 0 prints one JSON line with
     the concat checked against every rank's totals."""
-    from pebble_amd.rowblk import gen_row_blocks
+    import copy
+    from pebble_amd import _native as N
     from pebble_amd.shard import exclusive_bases
-    nb = a.blocks or 64
-    buf, off, lens, n_kv = gen_row_blocks(a.seed + 7919 * rank, nb, a.block_size, a.restart_interval, a.key_len,
-                                          a.val_len, a.value_prefix, n_threads=4)
+    ar = copy.copy(a)
+    ar.workload = "row" if a.workload not in ("row", "zipf") else a.workload
+    # this rank's byte-balanced shard of one global batch, as main() cuts it
+    (buf, off, lens, n_kv, _), shard, rank_bytes = global_shard(ar, world, rank, dist, None, a.blocks or 64, N)
+    nb = len(off)
     nres = np.array([int.from_bytes(buf[int(o) + int(l) - 4: int(o) + int(l)].tobytes(), "little")
                      for o, l in zip(off, lens)], np.int64)
     per = np.stack([nres, lens.astype(np.int64), lens.astype(np.int64) // 2, nres])  # [4, nb]
@@ -218,12 +221,129 @@ def plumbing(a, world, rank, dist) -> None:
                           "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4),
                           "plumbing": True, "dist_backend": a.dist_backend, "concat_ok": bool(ok),
                           "note": "no GPU: decode not run; rank, timing and offset-concat plumbing only",
-                          "config": {"workload": f"{nb} row blocks per rank (plumbing)",
+                          "config": {"workload": f"{ar.workload} blocks, byte-balanced shards of one global batch "
+                                                 f"(plumbing)",
+                                     "global_batch_blocks": int(shard[2]), "shard_blocks": [int(shard[0]), int(shard[1])],
+                                     "input_bytes_per_rank": [int(x) for x in rank_bytes],
                                      "parallelism": f"shard{world}" + ("+offset_concat" if world > 1 else "")}}),
               flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def workload_info(a, nb, N):
+    """(format, dominant kernel name, workload description) of a.workload."""
+    row_kernel = "rowblk_pool_kernel"
+    if a.workload in ("row", "transform"):
+        kernel = "tf_count_kernel+tf_scan_kernel+tf_scatter_kernel" if a.workload == "transform" else row_kernel
+        wl = ("transform pass (SyntheticSeqNum, HideObsoletePoints, 12 B SyntheticPrefix) over " if a.workload ==
+              "transform" else "") + (f"config2: {nb} x {a.block_size // 1024} KiB row-format blocks per GPU, restart interval "
+              f"{a.restart_interval}, {a.key_len} B keys / {a.val_len} B values" + (", value prefix" if a.value_prefix else "")
+              + (f", every {a.hide}th KV obsolete, HideObsoletePoints fused" if a.hide else ""))
+        return N.PBL_FMT_ROW, kernel, wl
+    if a.workload == "rowmix":
+        return N.PBL_FMT_ROW, row_kernel, (
+            f"row-shape mix: {nb} row blocks per GPU, config-2 blocks with " +
+            ("every 10th a config-5 Zipf block (restart interval 16)" if a.mix == "zipf10" else
+             "every 8th a short table-tail block (2 / 4 / 8 KiB)"))
+    if a.workload == "col":
+        kernel = "colblk_decode_kernel" if a.kernel == "single" and not a.hide else "colblk_pipe_kernel"
+        return N.PBL_FMT_COL_CRDB1, kernel, (
+            f"config3: {nb} x {a.block_size // 1024} KiB colblk blocks per GPU, cockroachkvs crdb1 schema "
+            f"(KeyGenConfig alphabet 26, RoachKeyLen 12, PrefixLenShared 4, 1 key/prefix), 128 B values"
+            + (f", every {a.hide}th row isObsolete, HideObsoletePoints fused" if a.hide else "")
+            + (f", Pebblev8 tiering columns (span ids 1..{a.tiering}) decoded to per-KV KVMeta" if a.tiering else ""))
+    if a.workload == "zipf":
+        fmt = N.PBL_FMT_ROW if a.zipf_format == "row" else N.PBL_FMT_COL_DEFAULT
+        # (a VARLEN colblk batch takes the one-block-per-workgroup kernel unless
+        # --kernel names another; row batches ignore the hint)
+        vl = a.kernel not in ("pipe", "single")
+        kernel = (row_kernel if fmt == N.PBL_FMT_ROW
+                  else "colblk_decode_kernel" if vl or a.kernel == "single" else "colblk_pipe_kernel")
+        return fmt, kernel, (f"config5: {nb} variable-length blocks per GPU targeting {a.block_size // 1024} KiB, "
+                             + (f"row format, restart interval {a.restart_interval}" if fmt == N.PBL_FMT_ROW
+                                else "colblk DefaultKeySchema")
+                             + ", Zipf(1.1) key lengths 8-1024 B / value lengths 0-64 KiB")
+    # (the sequential mixed path: split + colblk size pass + the row
+    # staging-pool kernel over the row ids + colblk pipeline, timed together)
+    return N.PBL_FMT_ROW, "mixed_col_size_kernel+rowblk_pool_kernel+mixed_col_kernel", (
+        f"config4 shard: {nb} x {a.block_size // 1024} KiB blocks per GPU, even ids row-format "
+        f"(config-2 shape), odd ids colblk crdb1 (config-3 shape)")
+
+
+def gen_range(a, first: int, n: int, N):
+    """Global blocks [first, first + n) of the workload's batch (seed a.seed):
+    (buf, off, lens, n_kv, block_fmt)."""
+    from pebble_amd.colblk import gen_col_blocks
+    from pebble_amd.rowblk import gen_row_blocks
+    if a.workload in ("row", "transform"):
+        return (*gen_row_blocks(a.seed, n, a.block_size, a.restart_interval, a.key_len, a.val_len, a.value_prefix,
+                                n_threads=16, obsolete_every=a.hide, first_block=first), None)
+    if a.workload == "rowmix":
+        from pebble_amd.batch import gen_row_mix
+        assert first == 0, "rowmix is a single-GPU workload"
+        return (*gen_row_mix(a.seed, n, a.mix, n_threads=16), None)
+    if a.workload == "col":
+        return (*gen_col_blocks(a.seed, n, a.block_size, n_threads=16, obsolete_every=a.hide, tiering=a.tiering,
+                                first_block=first), None)
+    if a.workload == "zipf":
+        from pebble_amd.batch import gen_zipf_blocks
+        fmt = N.PBL_FMT_ROW if a.zipf_format == "row" else N.PBL_FMT_COL_DEFAULT
+        return (*gen_zipf_blocks(a.seed, n, fmt, a.restart_interval, a.block_size, n_threads=16, first_block=first),
+                None)
+    # mixed (config 4): global block g is row block g // 2 (g even) or colblk
+    # block g // 2 (g odd), at a fixed stride
+    r0, r1 = (first + 1) // 2, (first + n + 1) // 2
+    c0, c1 = first // 2, (first + n) // 2
+    rb, ro, rl, rn = gen_row_blocks(a.seed, r1 - r0, a.block_size, a.restart_interval, a.key_len, a.val_len,
+                                    a.value_prefix, n_threads=16, first_block=r0)
+    cb, co, cl, cn = gen_col_blocks(a.seed, c1 - c0, a.block_size, n_threads=16, first_block=c0)
+    g = first + np.arange(n)
+    is_row = (g & 1) == 0
+    ri, ci = g // 2 - r0, g // 2 - c0
+    buf = np.zeros(n * a.block_size + 16, np.uint8)
+    v = buf[: n * a.block_size].reshape(n, a.block_size)
+    v[is_row] = rb[: (r1 - r0) * a.block_size].reshape(r1 - r0, a.block_size)[ri[is_row]]
+    v[~is_row] = cb[: (c1 - c0) * a.block_size].reshape(c1 - c0, a.block_size)[ci[~is_row]]
+    del rb, cb
+    off = np.arange(n, dtype=np.uint64) * a.block_size
+    lens = np.where(is_row, rl[np.clip(ri, 0, max(r1 - r0 - 1, 0))] if r1 > r0 else 0,
+                    cl[np.clip(ci, 0, max(c1 - c0 - 1, 0))] if c1 > c0 else 0).astype(np.uint32)
+    block_fmt = np.where(is_row, N.PBL_FMT_ROW, N.PBL_FMT_COL_CRDB1).astype(np.uint8)
+    return buf, off, lens, rn + cn, block_fmt
+
+
+def gather_ints(dist, dev, vals, world: int, backend: str) -> np.ndarray:
+    """All-gather an int64 vector of the same length from every rank -> [world, n]."""
+    t = torch.as_tensor(np.asarray(vals, np.int64))
+    if backend == "nccl":
+        t = t.to(dev)
+        out = torch.empty(world * t.numel(), dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(out, t)
+    else:
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        out = torch.cat(parts)
+    return out.cpu().numpy().reshape(world, -1)
+
+
+def global_shard(a, world, rank, dist, dev, nb, N):
+    """This rank's byte-balanced shard of the global batch of world x nb
+    blocks: ((buf, off, lens, n_kv, block_fmt), (start, end, global blocks),
+    input bytes of every rank)."""
+    if world == 1:
+        g = gen_range(a, 0, nb, N)
+        return g, (0, nb, nb), [int(g[2].astype(np.int64).sum())]
+    from pebble_amd.shard import partition_blocks
+    g = gen_range(a, rank * nb, nb, N)
+    lens_all = gather_ints(dist, dev, g[2].astype(np.int64), world, a.dist_backend).reshape(-1)
+    s, e = partition_blocks(lens_all, world)[rank]
+    if (s, e) != (rank * nb, (rank + 1) * nb):
+        del g
+        g = gen_range(a, s, e - s, N)
+    rank_bytes = gather_ints(dist, dev, [int(g[2].astype(np.int64).sum())], world, a.dist_backend).reshape(-1)
+    return g, (s, e, world * nb), [int(x) for x in rank_bytes]
 
 
 def main():
@@ -270,75 +390,16 @@ def main():
         assert a.workload == "col", "--tiering applies to the col workload"
         flags |= N.PBL_COL_TIERING
     flags |= {"auto": 0, "single": N.PBL_KERNEL_SINGLE, "pipe": N.PBL_KERNEL_PIPE, "pool": N.PBL_KERNEL_POOL}[a.kernel]
-    row_kernel = "rowblk_pool_kernel"
-    seed = a.seed + 7919 * rank
     t0 = time.time()
-    block_fmt = None
-    if a.workload in ("row", "transform"):
-        fmt = N.PBL_FMT_ROW
-        buf, off, lens, n_kv = gen_row_blocks(seed, nb, a.block_size, a.restart_interval, a.key_len, a.val_len,
-                                              a.value_prefix, n_threads=16, obsolete_every=a.hide)
-        kernel = row_kernel
-        if a.workload == "transform":
-            kernel = "tf_count_kernel+tf_scan_kernel+tf_scatter_kernel"
-        wl = ("transform pass (SyntheticSeqNum, HideObsoletePoints, 12 B SyntheticPrefix) over " if a.workload ==
-              "transform" else "") + (f"config2: {nb} x {a.block_size // 1024} KiB row-format blocks per GPU, restart interval "
-              f"{a.restart_interval}, {a.key_len} B keys / {a.val_len} B values" + (", value prefix" if a.value_prefix else "")
-              + (f", every {a.hide}th KV obsolete, HideObsoletePoints fused" if a.hide else ""))
-    elif a.workload == "rowmix":
-        from pebble_amd.batch import gen_row_mix
-        fmt = N.PBL_FMT_ROW
-        buf, off, lens, n_kv = gen_row_mix(seed, nb, a.mix, n_threads=16)
-        kernel = row_kernel
-        wl = (f"row-shape mix: {nb} row blocks per GPU, config-2 blocks with " +
-              ("every 10th a config-5 Zipf block (restart interval 16)" if a.mix == "zipf10" else
-               "every 8th a short table-tail block (2 / 4 / 8 KiB)"))
-    elif a.workload == "col":
-        fmt = N.PBL_FMT_COL_CRDB1
-        buf, off, lens, n_kv = gen_col_blocks(seed, nb, a.block_size, n_threads=16, obsolete_every=a.hide,
-                                              tiering=a.tiering)
-        kernel = "colblk_decode_kernel" if a.kernel == "single" and not a.hide else "colblk_pipe_kernel"
-        wl = (f"config3: {nb} x {a.block_size // 1024} KiB colblk blocks per GPU, cockroachkvs crdb1 schema "
-              f"(KeyGenConfig alphabet 26, RoachKeyLen 12, PrefixLenShared 4, 1 key/prefix), 128 B values"
-              + (f", every {a.hide}th row isObsolete, HideObsoletePoints fused" if a.hide else "")
-              + (f", Pebblev8 tiering columns (span ids 1..{a.tiering}) decoded to per-KV KVMeta" if meta else ""))
-    elif a.workload == "zipf":
-        from pebble_amd.batch import gen_zipf_blocks
-        fmt = N.PBL_FMT_ROW if a.zipf_format == "row" else N.PBL_FMT_COL_DEFAULT
-        buf, off, lens, n_kv = gen_zipf_blocks(seed, nb, fmt, a.restart_interval, a.block_size, n_threads=16)
-        from pebble_amd.batch import varlen_hint
-        # (a VARLEN colblk batch takes the one-block-per-workgroup kernel unless
-        # --kernel names another; row batches ignore the hint)
-        vl = varlen_hint(lens) and a.kernel not in ("pipe", "single")
-        kernel = (row_kernel if fmt == N.PBL_FMT_ROW
-                  else "colblk_decode_kernel" if vl or a.kernel == "single" else "colblk_pipe_kernel")
-        wl = (f"config5: {nb} variable-length blocks per GPU targeting {a.block_size // 1024} KiB, "
-              + (f"row format, restart interval {a.restart_interval}" if fmt == N.PBL_FMT_ROW
-                 else "colblk DefaultKeySchema")
-              + ", Zipf(1.1) key lengths 8-1024 B / value lengths 0-64 KiB")
-    else:
-        fmt = N.PBL_FMT_ROW
-        h = nb // 2
-        rb, ro, rl, rn = gen_row_blocks(seed, nb - h, a.block_size, a.restart_interval, a.key_len, a.val_len,
-                                        a.value_prefix, n_threads=16)
-        cb, co, cl, cn = gen_col_blocks(seed, h, a.block_size, n_threads=16)
-        # interleave: even block ids row, odd ids colblk, fixed stride
-        buf = np.zeros(nb * a.block_size + 16, np.uint8)
-        v = buf[: nb * a.block_size].reshape(nb, a.block_size)
-        v[0::2] = rb[: (nb - h) * a.block_size].reshape(nb - h, a.block_size)
-        v[1::2] = cb[: h * a.block_size].reshape(h, a.block_size)
-        del rb, cb
-        off = np.arange(nb, dtype=np.uint64) * a.block_size
-        lens = np.empty(nb, np.uint32)
-        lens[0::2], lens[1::2] = rl, cl
-        block_fmt = np.empty(nb, np.uint8)
-        block_fmt[0::2], block_fmt[1::2] = N.PBL_FMT_ROW, N.PBL_FMT_COL_CRDB1
-        n_kv = rn + cn
-        # (the sequential mixed path: split + colblk size pass + the row
-        # staging-pool kernel over the row ids + colblk pipeline, timed together)
-        kernel = "mixed_col_size_kernel+rowblk_pool_kernel+mixed_col_kernel"
-        wl = (f"config4 shard: {nb} x {a.block_size // 1024} KiB blocks per GPU, even ids row-format "
-              f"(config-2 shape), odd ids colblk crdb1 (config-3 shape)")
+    fmt, kernel, wl = workload_info(a, nb, N)
+    # ONE global batch of world x nb blocks (block content = f(seed, global
+    # index)), cut into contiguous byte-balanced ranges:
+    # every rank generates its nominal range, the ranges' lengths are
+    # all-gathered, shard.partition_blocks picks this rank's range, and the
+    # blocks it lacks are generated (configs 2-4: the nominal ranges; config 5:
+    # boundaries move to balance bytes)
+    (buf, off, lens, n_kv, block_fmt), shard_range, rank_bytes = global_shard(a, world, rank, dist, dev, nb, N)
+    nb = len(off)
     gen_s = time.time() - t0
     input_bytes = int(lens.astype(np.int64).sum())
     batch = BlockBatch.from_host(buf, off, lens, dev, fmt, flags, block_format=block_fmt)
@@ -418,7 +479,7 @@ def main():
         dist.all_reduce(km, op=dist.ReduceOp.MAX)
         kern_ms = float(km.item())
 
-    total_input = input_bytes * world
+    total_input = int(sum(rank_bytes))
     value = total_input * a.steps / elapsed / 2**30
     ab = alg_bytes(hres, nb, input_bytes)
     if plan is not None:  # the decoded arrays read once, the transformed ones written once
@@ -453,6 +514,8 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
         "config": {"workload": wl,
                    "blocks_per_gpu": nb, "input_bytes_per_gpu": input_bytes, "kvs_per_gpu": n_kv,
+                   "global_batch_blocks": int(shard_range[2]), "shard_blocks": [int(shard_range[0]), int(shard_range[1])],
+                   "input_bytes_per_rank": [int(x) for x in rank_bytes],
                    "parallelism": f"shard{world}" + (f"+{'rccl' if a.dist_backend == 'nccl' else 'gloo'}_offset_concat"
                                                       if world > 1 else "")},
         "roofline": {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1),

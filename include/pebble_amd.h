@@ -527,16 +527,19 @@ size_t pbl_rowblk_writer_finish(pbl_rowblk_writer* w, uint8_t* dst, size_t dst_c
  * value bytes from splitmix64(seed + r).  Each block is filled while
  * EstimatedSize()+entry <= block_size and is placed at a fixed `block_size`
  * stride in `dst` (dst must hold n_blocks*block_size bytes).  Fills
- * block_off/block_len (host arrays) and returns total KVs.
+ * block_off/block_len (host arrays) and returns total KVs.  Block content
+ * depends only on (seed, global block index).
  */
 uint64_t pbl_gen_row_blocks(uint64_t seed, uint32_t n_blocks, uint32_t block_size,
                             int restart_interval, uint32_t key_len, uint32_t val_len,
                             int value_prefix, uint8_t* dst, uint64_t* block_off,
                             uint32_t* block_len, int n_threads);
-/* The same with obsolete points (HideObsoletePoints measurements): key k of a
- * block carries the trailer's obsolete bit when obsolete_every > 0 and
- * k % obsolete_every == obsolete_every - 1 (rowblk_writer.go:30-42).        */
-uint64_t pbl_gen_row_blocks_obs(uint64_t seed, uint32_t n_blocks, uint32_t block_size,
+/* The same from global block `first_block` on (output block i = global block
+ * first_block + i: a rank's shard of one global batch), with obsolete points
+ * (HideObsoletePoints measurements): key k of a block carries the trailer's
+ * obsolete bit when obsolete_every > 0 and k % obsolete_every ==
+ * obsolete_every - 1 (rowblk_writer.go:30-42).                              */
+uint64_t pbl_gen_row_blocks_obs(uint64_t seed, uint32_t first_block, uint32_t n_blocks, uint32_t block_size,
                                 int restart_interval, uint32_t key_len, uint32_t val_len,
                                 int value_prefix, uint32_t obsolete_every, uint8_t* dst,
                                 uint64_t* block_off, uint32_t* block_len, int n_threads);
@@ -598,6 +601,11 @@ typedef struct pbl_colgen_config {
                                   attribute (base_wall_time / 1e9) + r % 3600,
                                   unset (KVMeta{}) for one row in ten, r drawn
                                   per row from the block's seed             */
+  uint32_t first_block;        /* global index of the first block generated:
+                                  block i of the output is global block
+                                  first_block + i (a rank's shard of one
+                                  global batch)                              */
+  uint32_t reserved;
 } pbl_colgen_config;
 
 /*
@@ -620,6 +628,8 @@ typedef struct pbl_zipf_config {
   uint32_t block_size;         /* target block size; a block always takes its
                                   first KV, so one large KV may exceed it         */
   int32_t restart_interval;    /* row format only (1, 16, 32)                     */
+  uint32_t first_block;        /* output block i = global block first_block + i   */
+  uint32_t reserved;
 } pbl_zipf_config;
 
 /*

@@ -87,6 +87,7 @@ class ColGenConfigC(ctypes.Structure):
         ("avg_keys_per_prefix", ctypes.c_uint32), ("base_wall_time", ctypes.c_uint64),
         ("pct_logical", ctypes.c_uint32), ("value_len", ctypes.c_uint32),
         ("obsolete_every", ctypes.c_uint32), ("tiering", ctypes.c_uint32),
+        ("first_block", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
     ]
 
 
@@ -95,6 +96,7 @@ class ZipfConfigC(ctypes.Structure):
         ("seed", ctypes.c_uint64), ("key_min", ctypes.c_uint32), ("key_max", ctypes.c_uint32),
         ("val_min", ctypes.c_uint32), ("val_max", ctypes.c_uint32), ("s", ctypes.c_double),
         ("block_size", ctypes.c_uint32), ("restart_interval", ctypes.c_int32),
+        ("first_block", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
     ]
 
 
@@ -241,7 +243,7 @@ SIGNATURES = {
     "pbl_gen_row_blocks": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                              ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                              _vp, _vp, _vp, ctypes.c_int]),
-    "pbl_gen_row_blocks_obs": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+    "pbl_gen_row_blocks_obs": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                  ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                                  ctypes.c_uint32, _vp, _vp, _vp, ctypes.c_int]),
     "pbl_colblk_writer_new": (_vp, [ctypes.c_uint32, ctypes.c_int]),

@@ -291,14 +291,15 @@ def offset_concat(out: DecodedBatch, rank_totals: torch.Tensor, rank: int, strea
 
 def gen_zipf_blocks(seed: int, n_blocks: int, fmt: int = 0, restart_interval: int = 16, block_size: int = 32768,
                     key_min: int = 8, key_max: int = 1024, val_min: int = 0, val_max: int = 65536, s: float = 1.1,
-                    n_threads: int = 0):
+                    n_threads: int = 0, first_block: int = 0):
     """Config 5 (BASELINE.json configs[4]): Zipf(s) key lengths in [key_min, key_max]
     and value lengths in [val_min, val_max], variable-length blocks packed at 8-B
     alignment (`pbl_gen_zipf_blocks`).  fmt is PBL_FMT_ROW or PBL_FMT_COL_DEFAULT.
+    Block i is global block first_block + i of the seed's batch (a rank's shard).
     Returns (buf, off, lens, n_kv) with buf padded by 16 zero bytes."""
     import ctypes
     import os
-    cfg = N.ZipfConfigC(seed, key_min, key_max, val_min, val_max, s, block_size, restart_interval)
+    cfg = N.ZipfConfigC(seed, key_min, key_max, val_min, val_max, s, block_size, restart_interval, first_block, 0)
     nt = n_threads or min(16, os.cpu_count() or 1)
     off = np.empty(n_blocks, np.uint64)
     lens = np.empty(n_blocks, np.uint32)

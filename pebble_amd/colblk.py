@@ -85,15 +85,16 @@ def gen_col_blocks(seed: int, n_blocks: int, block_size: int = 32768, schema: in
                    alphabet_len: int = 26, roach_key_len: int = 12, prefix_len_shared: int = 4,
                    avg_keys_per_prefix: int = 1, pct_logical: int = 0, value_len: int = 128,
                    base_wall_time: int = 1_700_000_000_000_000_000, n_threads: int = 0,
-                   obsolete_every: int = 0, tiering: int = 0):
+                   obsolete_every: int = 0, tiering: int = 0, first_block: int = 0):
     """Seeded synthetic colblk blocks at a fixed `block_size` stride (host numpy).
     Defaults are BASELINE config 3: cockroachkvs_bench_test.go:83-89 KeyGenConfig
     (alphabet 26, RoachKeyLen 12, PrefixLenShared 4, 1 key per prefix) with 128 B values.
     `tiering` > 0: Pebblev8 blocks with tiering columns and per-row KVMeta
-    (span ids 1..tiering; include/pebble_amd.h pbl_colgen_config)."""
+    (span ids 1..tiering; include/pebble_amd.h pbl_colgen_config).  Block i is
+    global block first_block + i of the seed's batch (a rank's shard)."""
     import os
     cfg = N.ColGenConfigC(seed, alphabet_len, prefix_len_shared, roach_key_len, avg_keys_per_prefix,
-                          base_wall_time, pct_logical, value_len, obsolete_every, tiering)
+                          base_wall_time, pct_logical, value_len, obsolete_every, tiering, first_block, 0)
     buf = np.zeros(n_blocks * block_size + 16, np.uint8)
     off = np.empty(n_blocks, np.uint64)
     lens = np.empty(n_blocks, np.uint32)

@@ -720,7 +720,8 @@ extern "C" uint64_t pbl_gen_col_blocks(const pbl_colgen_config* cfgp, uint32_t s
     w.tiering = cfg.tiering != 0;
     std::vector<std::string> keys;
     std::vector<uint8_t> val(cfg.value_len);
-    for (uint32_t b = t; b < n_blocks; b += n_threads) {
+    for (uint32_t bl = t; bl < n_blocks; bl += n_threads) {
+      const uint32_t b = cfg.first_block + bl;  // the block's global index: its content
       uint64_t s = cfg.seed ^ (0xC01B10C5ull * (b + 1));
       // Per-row estimate sizes the candidate set; refill if it runs out.
       uint32_t est = block_size / std::max<uint32_t>(1, cfg.value_len + cfg.roach_key_len / 2 + 12) + 64;
@@ -746,9 +747,9 @@ extern "C" uint64_t pbl_gen_col_blocks(const pbl_colgen_config* cfgp, uint32_t s
       }
       rows = uint32_t(w.rows);
       if (w.size_for(w.rows) > block_size) rows--;
-      size_t n = pbl_colblk_writer_finish(&w, rows, dst + uint64_t(b) * block_size, block_size);
-      block_off[b] = uint64_t(b) * block_size;
-      block_len[b] = uint32_t(n);
+      size_t n = pbl_colblk_writer_finish(&w, rows, dst + uint64_t(bl) * block_size, block_size);
+      block_off[bl] = uint64_t(bl) * block_size;
+      block_len[bl] = uint32_t(n);
       counts[t] += rows;
     }
   };

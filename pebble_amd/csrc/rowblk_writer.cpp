@@ -215,10 +215,10 @@ uint64_t gen_one_block(uint64_t seed, uint32_t b, uint32_t block_size, int ri, u
 
 }  // namespace
 
-extern "C" uint64_t pbl_gen_row_blocks_obs(uint64_t seed, uint32_t n_blocks, uint32_t block_size,
-                                           int restart_interval, uint32_t key_len, uint32_t val_len,
-                                           int value_prefix, uint32_t obsolete_every, uint8_t* dst,
-                                           uint64_t* block_off, uint32_t* block_len, int n_threads) {
+extern "C" uint64_t pbl_gen_row_blocks_obs(uint64_t seed, uint32_t first_block, uint32_t n_blocks,
+                                           uint32_t block_size, int restart_interval, uint32_t key_len,
+                                           uint32_t val_len, int value_prefix, uint32_t obsolete_every,
+                                           uint8_t* dst, uint64_t* block_off, uint32_t* block_len, int n_threads) {
   if (n_threads <= 0) n_threads = int(std::max(1u, std::thread::hardware_concurrency()));
   n_threads = std::min<int>(n_threads, 64);
   if (key_len < 8) key_len = 8;
@@ -227,7 +227,7 @@ extern "C" uint64_t pbl_gen_row_blocks_obs(uint64_t seed, uint32_t n_blocks, uin
     uint64_t c = 0;
     for (uint32_t b = uint32_t(t); b < n_blocks; b += uint32_t(n_threads)) {
       block_off[b] = uint64_t(b) * block_size;
-      c += gen_one_block(seed, b, block_size, restart_interval, key_len, val_len,
+      c += gen_one_block(seed, first_block + b, block_size, restart_interval, key_len, val_len,
                          value_prefix != 0, obsolete_every, dst + uint64_t(b) * block_size, &block_len[b]);
     }
     counts[size_t(t)] = c;
@@ -245,6 +245,6 @@ extern "C" uint64_t pbl_gen_row_blocks(uint64_t seed, uint32_t n_blocks, uint32_
                                        int restart_interval, uint32_t key_len, uint32_t val_len,
                                        int value_prefix, uint8_t* dst, uint64_t* block_off,
                                        uint32_t* block_len, int n_threads) {
-  return pbl_gen_row_blocks_obs(seed, n_blocks, block_size, restart_interval, key_len, val_len, value_prefix, 0,
+  return pbl_gen_row_blocks_obs(seed, 0, n_blocks, block_size, restart_interval, key_len, val_len, value_prefix, 0,
                                 dst, block_off, block_len, n_threads);
 }

@@ -125,7 +125,8 @@ extern "C" uint64_t pbl_gen_zipf_blocks(const pbl_zipf_config* cfgp, uint32_t fo
   std::vector<uint64_t> counts(size_t(n_threads), 0);
   auto gen = [&](int t) {
     for (uint32_t b = uint32_t(t); b < n_blocks; b += uint32_t(n_threads))
-      counts[size_t(t)] += format == PBL_FMT_ROW ? gen_row(c, zk, zv, b, blocks[b]) : gen_col(c, zk, zv, b, blocks[b]);
+      counts[size_t(t)] += format == PBL_FMT_ROW ? gen_row(c, zk, zv, c.first_block + b, blocks[b])
+                                                 : gen_col(c, zk, zv, c.first_block + b, blocks[b]);
   };
   std::vector<std::thread> th;
   for (int t = 1; t < n_threads; t++) th.emplace_back(gen, t);

@@ -111,15 +111,16 @@ class Writer:
 
 def gen_row_blocks(seed: int, n_blocks: int, block_size: int = 32768, restart_interval: int = 16,
                    key_len: int = 16, val_len: int = 100, value_prefix: bool = False, n_threads: int = 0,
-                   obsolete_every: int = 0):
+                   obsolete_every: int = 0, first_block: int = 0):
     """Seeded synthetic row blocks at a fixed `block_size` stride (host numpy).
     obsolete_every > 0: the k-th key of a block with k % obsolete_every ==
-    obsolete_every - 1 carries the trailer's obsolete bit."""
+    obsolete_every - 1 carries the trailer's obsolete bit.  Block i is global
+    block first_block + i of the seed's batch (a rank's shard)."""
     buf = np.empty(n_blocks * block_size + 16, np.uint8)
     buf[-16:] = 0
     off = np.empty(n_blocks, np.uint64)
     lens = np.empty(n_blocks, np.uint32)
-    n_kv = N.lib().pbl_gen_row_blocks_obs(seed, n_blocks, block_size, restart_interval, key_len, val_len,
+    n_kv = N.lib().pbl_gen_row_blocks_obs(seed, first_block, n_blocks, block_size, restart_interval, key_len, val_len,
                                           int(value_prefix), obsolete_every, buf.ctypes.data, off.ctypes.data,
                                           lens.ctypes.data, n_threads)
     return buf, off, lens, int(n_kv)
