@@ -267,6 +267,24 @@ SIGNATURES = {
 }
 
 _lib = None
+_gen_lib = None
+
+
+def gen_lib() -> ctypes.CDLL:
+    """The library for host-only work (synthetic generators, block writers):
+    always the in-tree build, so that an A/B run of an older decoder build
+    (PBL_LIB) generates exactly the same inputs."""
+    global _gen_lib
+    if not os.environ.get("PBL_LIB"):
+        return lib()
+    if _gen_lib is None:
+        L = ctypes.CDLL(os.path.join(_HERE, "libpebble_amd.so"))
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _gen_lib = L
+    return _gen_lib
 
 
 def lib() -> ctypes.CDLL:

@@ -307,7 +307,7 @@ def gen_zipf_blocks(seed: int, n_blocks: int, fmt: int = 0, restart_interval: in
     # worst case: every block is its target plus one maximal KV
     cap = n_blocks * (block_size + key_max + val_max + 64)
     buf = np.empty(cap + 16, np.uint8)
-    n = N.lib().pbl_gen_zipf_blocks(ctypes.byref(cfg), fmt, n_blocks, buf.ctypes.data, cap, off.ctypes.data,
+    n = N.gen_lib().pbl_gen_zipf_blocks(ctypes.byref(cfg), fmt, n_blocks, buf.ctypes.data, cap, off.ctypes.data,
                                     lens.ctypes.data, ctypes.byref(used), nt)
     if n == (1 << 64) - 1:
         raise ValueError(f"pbl_gen_zipf_blocks: bad config or capacity ({used.value} > {cap})")

@@ -36,7 +36,7 @@ class DataBlockEncoder:
     def __init__(self, schema: int = SCHEMA_CRDB1, bundle_size: int = 16, tiering: bool = False):
         """`tiering`: Init(schema, WithTieringColumns()) -- the Pebblev8 layout
         (sstable/format.go:305-316), whose add() also takes a base.KVMeta."""
-        self._lib = N.lib()
+        self._lib = N.gen_lib()
         self._w = self._lib.pbl_colblk_writer_new(schema, bundle_size)
         if not self._w:
             raise ValueError(f"bad schema {schema} / bundle size {bundle_size}")
@@ -99,7 +99,7 @@ def gen_col_blocks(seed: int, n_blocks: int, block_size: int = 32768, schema: in
     off = np.empty(n_blocks, np.uint64)
     lens = np.empty(n_blocks, np.uint32)
     nt = n_threads or min(16, os.cpu_count() or 1)
-    n = N.lib().pbl_gen_col_blocks(ctypes.byref(cfg), schema, n_blocks, block_size, buf.ctypes.data,
+    n = N.gen_lib().pbl_gen_col_blocks(ctypes.byref(cfg), schema, n_blocks, block_size, buf.ctypes.data,
                                    off.ctypes.data, lens.ctypes.data, nt)
     return buf, off, lens, int(n)
 

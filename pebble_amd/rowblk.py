@@ -66,7 +66,7 @@ class Writer:
     """rowblk.Writer backed by the native restatement."""
 
     def __init__(self, restart_interval: int = 16):
-        self._lib = N.lib()
+        self._lib = N.gen_lib()
         self._w = self._lib.pbl_rowblk_writer_new(restart_interval)
         self.restart_interval = restart_interval
 
@@ -120,7 +120,7 @@ def gen_row_blocks(seed: int, n_blocks: int, block_size: int = 32768, restart_in
     buf[-16:] = 0
     off = np.empty(n_blocks, np.uint64)
     lens = np.empty(n_blocks, np.uint32)
-    n_kv = N.lib().pbl_gen_row_blocks_obs(seed, first_block, n_blocks, block_size, restart_interval, key_len, val_len,
+    n_kv = N.gen_lib().pbl_gen_row_blocks_obs(seed, first_block, n_blocks, block_size, restart_interval, key_len, val_len,
                                           int(value_prefix), obsolete_every, buf.ctypes.data, off.ctypes.data,
                                           lens.ctypes.data, n_threads)
     return buf, off, lens, int(n_kv)
