@@ -4,6 +4,7 @@
 #include "common.hip.h"
 #include "colblk_block.hip.h"
 #include "colblk_pipe.hip.h"
+#include "colblk_wave.hip.h"
 
 namespace pbl {
 namespace col {
@@ -33,18 +34,21 @@ extern "C" int pbl_decode_batch_colblk(const pbl_block_batch* batch, pbl_decode_
   pbl::Args a;
   a.in = *batch;
   a.out = *out;
-  // default: the persistent lagged-look-back kernel (colblk_pipe.hip.h).  The
-  // one-block-per-workgroup kernel runs for PBL_KERNEL_SINGLE (A/B) and for
-  // PBL_BATCH_VARLEN batches unless PBL_KERNEL_PIPE forces the pipeline
-  // (config 5: 412 vs 245 GiB/s, the pipeline's one-iteration look-back lag
-  // convoys behind long blocks).
+  // default: the persistent lagged-look-back kernel (colblk_pipe.hip.h).
+  // PBL_BATCH_VARLEN batches take the wave-per-block kernel (colblk_wave.hip.h)
+  // unless PBL_KERNEL_PIPE forces the pipeline (its one-iteration look-back lag
+  // convoys behind long blocks); PBL_KERNEL_SINGLE (A/B) the one-block-per-
+  // workgroup kernel.
   const uint32_t f = batch->flags;
   // HideObsoletePoints (PBL_ROW_HIDE_OBSOLETE) is fused into the pipeline
   // (colblk_pipe_kernel<true>) whatever the other flags say.
   const bool hide = (f & PBL_ROW_HIDE_OBSOLETE) != 0;
-  const bool single = !hide && ((f & PBL_KERNEL_SINGLE) || ((f & PBL_BATCH_VARLEN) && !(f & PBL_KERNEL_PIPE)));
+  const bool single = !hide && (f & PBL_KERNEL_SINGLE);
+  const bool wave = !hide && !single && (f & PBL_BATCH_VARLEN) && !(f & PBL_KERNEL_PIPE);
   if (single) {
     hipLaunchKernelGGL(pbl::col::colblk_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
+  } else if (wave) {
+    hipLaunchKernelGGL(pbl::col::cwave::colblk_wave_kernel, dim3(batch->n_blocks), dim3(pbl::kWave), 0, st, a);
   } else {
     const void* fn = hide ? reinterpret_cast<const void*>(pbl::col::cpipe::colblk_pipe_kernel<true>)
                           : reinterpret_cast<const void*>(pbl::col::cpipe::colblk_pipe_kernel<false>);

@@ -1,0 +1,227 @@
+// colblk_wave.hip.h — one WAVE per colblk data block, many blocks in flight per
+// CU: the form for batches of variable-length blocks (PBL_BATCH_VARLEN, e.g.
+// config 5's Zipf key / value sizes), whose blocks hold few rows (config 5:
+// about 13) and are dominated by one contiguous values range.
+//
+// A 256-thread workgroup per block (colblk_block.hip.h) leaves most of its
+// threads idle on such blocks and serialises the block's round trips behind
+// barriers; the pipeline (colblk_pipe.hip.h) convoys behind long blocks.  Here
+// a wave owns its block from ticket to last store, with no barrier, and the
+// CU holds up to 16 such waves:
+//
+//   stage   the block's first kStage bytes (header, key columns, trailers,
+//           prefixChanged, the value offsets, and the first value bytes) by
+//           LDS-DMA, one round trip
+//   parse   DataBlockDecoder.Init + the KeySeeker init, lane per column
+//           (parse_block_wave, the same as every other colblk path)
+//   rows    lane per row, 64 rows at a time: key parts and bounds checks,
+//           aggregate PUBLISHED, then the exclusive prefix by the look-back
+//   emit    per-row arrays; keys built in the wave's LDS key buffer (16-B
+//           stores out); the values range copied in 16-B chunks, kValU per lane
+//           in flight, from the stage where it holds them, else global memory
+//
+// Semantics are those of colblk_block.hip.h (DataBlockDecoder.Init
+// sstable/colblk/data_block.go:1096-1109, DataBlockIter.Next :1662-1708,
+// decodeMeta :1633-1641).  Blocks whose key region passes the stage read it
+// through the global reader (same results).
+#pragma once
+
+namespace pbl {
+namespace col {
+namespace cwave {
+
+#ifndef PBL_CW_STAGE
+#define PBL_CW_STAGE 6144
+#endif
+#ifndef PBL_CW_KEYBUF
+#define PBL_CW_KEYBUF 1536
+#endif
+#ifndef PBL_CW_VALU
+#define PBL_CW_VALU 8  // 16-B value chunks per lane in flight
+#endif
+#ifndef PBL_CW_WAVES
+#define PBL_CW_WAVES 4  // waves per SIMD (one wave per workgroup)
+#endif
+constexpr uint32_t kStg = PBL_CW_STAGE;
+constexpr uint32_t kKb = PBL_CW_KEYBUF;
+constexpr int kVU = PBL_CW_VALU;
+
+template <class T>
+__device__ __forceinline__ void st_nt(gptr<T> p, T v) {  // outputs stream past the blocks' lines
+  __builtin_nontemporal_store(v, p);
+}
+
+struct WLds {
+  uint4 head4[(kStg + 48) / 16];  // block byte 0 at (boff & 15); 16 B of slack past the end for lds_bytes16
+  uint4 key4[(kKb + 2 * kKeyPad) / 16];
+  Desc d;
+};
+
+// 16 bytes of the block at block offset j ([j, j + 16) inside the block): from
+// the stage when it holds them, else global memory.
+__device__ __forceinline__ uint4 blk16(const WLds& L, uint32_t sh, uint32_t nst, gptr<const uint8_t> g, uint32_t j) {
+  if (j + 16 <= nst) return lds_bytes16((lds_cu32)to_lds(L.head4), sh + j);
+  typedef u32x4 u32x4_ua __attribute__((aligned(1)));
+  const u32x4 v = *(gptr<const u32x4_ua>)(g + j);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+template <bool F>
+__device__ __forceinline__ void cw_emit(WLds& L, const Args& A, uint32_t b, uint32_t schema, const Src& S,
+                                        uint32_t sh, uint32_t nst, const uint64_t excl[kNumComp]) {
+  const int l = lane_id();
+  const pbl_decode_out& O = A.out;
+  const Desc& d = L.d;
+  const uint32_t rows = d.rows;
+  const uint64_t kvb = excl[0], kbb = excl[1], vbb = excl[2];
+  const gptr<const uint8_t> g = to_glb(A.in.blocks + A.in.block_off[b]);
+
+  // ---- per-row arrays ----------------------------------------------------------
+  const UCol& vo = d.v_off;
+  for (uint32_t r = l; r <= rows; r += kWave) {
+    const uint32_t v = vo.w ? uint32_t(S.le(vo.at + r * vo.w, vo.w)) : 0;
+    st_nt(to_glb(O.val_off) + (kvb + b + r), v - d.v_lo);
+    if (r < rows) {
+      st_nt(to_glb(O.trailer) + (kvb + r), with_seq(u_at<F>(S, d.trailers, r), A.in.synthetic_seq_num, 0u));
+      if (O.kv_flags) {
+        uint8_t fl = 0;
+        if (d.pc_at && ((S.le(d.pc_at + 8 * (r >> 6), 8) >> (r & 63)) & 1)) fl |= PBL_KV_PREFIX_CHANGED;
+        if (d.obs_at && ((S.le(d.obs_at + 8 * (r >> 6), 8) >> (r & 63)) & 1)) fl |= PBL_KV_OBSOLETE;
+        if (d.ext_at && ((S.le(d.ext_at + 8 * (r >> 6), 8) >> (r & 63)) & 1)) {
+          const uint32_t v1 = vo.w ? uint32_t(S.le(vo.at + (r + 1) * vo.w, vo.w)) : 0;
+          const bool vb = v1 > v && (S.byte(d.v_data + v) & 0xC0) == 0x80;
+          fl |= vb ? PBL_KV_VALBLK_HANDLE : PBL_KV_BLOB_HANDLE;
+        }
+        st_nt(to_glb(O.kv_flags) + (kvb + r), fl);
+      }
+      if (O.entry_off) st_nt(to_glb(O.entry_off) + (kvb + r), r);
+      if (O.tiering_span_id) {  // decodeMeta (data_block.go:1633-1641)
+        st_nt(to_glb(O.tiering_span_id) + (kvb + r), u_at_any(S, d.span, r));
+        st_nt(to_glb(O.tiering_attr) + (kvb + r), u_at_any(S, d.attr, r));
+      }
+    }
+  }
+
+  // ---- keys: 64 rows at a time, built in the key buffer -------------------------
+  lds_u8 kb8 = (lds_u8)to_lds(L.key4);
+  const lds_cu32 KW = (lds_cu32)to_lds(L.key4);
+  uint32_t cbase = 0;
+  for (uint32_t r0 = 0; r0 < rows; r0 += kWave) {
+    const uint32_t r = r0 + l;
+    RowParts p;
+    p.klen = 0;
+    if (r < rows) p = row_parts<F>(S, d, schema, r);
+    const uint32_t incl = wave_incl_scan(p.klen);
+    const uint32_t tot = __shfl(incl, kWave - 1, kWave), ex = incl - p.klen;
+    if (r < rows) st_nt(to_glb(O.key_off) + (kvb + b + r), cbase + ex);
+    if (tot <= kKb) {
+      if (r < rows) build_key<F>(S, d, schema, p, kb8, kKeyPad + ex);
+      wave_sync();
+      const uint64_t lo = kbb + cbase, hi = lo + tot;
+      for (uint64_t ga = (lo & ~uint64_t(15)) + 16ull * l; ga < hi; ga += 16ull * kWave)
+        store16(O.key_bytes, ga, lo, hi, lds_bytes16(KW, uint32_t(kKeyPad + ga - lo)));
+      wave_sync();  // (the buffer is the next chunk's)
+    } else if (r < rows) {
+      build_key_global<F>(S, d, schema, p, O.key_bytes + kbb + cbase + ex);
+    }
+    cbase += tot;
+  }
+  if (l == 0) st_nt(to_glb(O.key_off) + (kvb + b + rows), cbase);
+
+  // ---- values: one contiguous range, 16-B chunks (the last ending at the end) --
+  const uint32_t j0 = d.v_data + d.v_lo, n = d.v_hi - d.v_lo;
+  const gptr<uint8_t> vout = to_glb(O.val_bytes) + vbb;
+  typedef u32x4 u32x4_ua __attribute__((aligned(1)));
+  if (n >= 16) {
+    const uint32_t nch = (n + 15) >> 4;
+    for (uint32_t k0 = l; k0 < nch; k0 += kWave * kVU) {
+      uint4 x[kVU];
+#pragma unroll
+      for (int u = 0; u < kVU; u++) {
+        const uint32_t k = k0 + kWave * u, q = 16 * k < n - 16 ? 16 * k : n - 16;
+        x[u] = k < nch ? blk16(L, sh, nst, g, j0 + q) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < kVU; u++) {
+        const uint32_t k = k0 + kWave * u, q = 16 * k < n - 16 ? 16 * k : n - 16;
+        if (k < nch) __builtin_nontemporal_store(u32x4_ua{x[u].x, x[u].y, x[u].z, x[u].w}, (gptr<u32x4_ua>)(vout + q));
+      }
+    }
+  } else {
+    for (uint32_t i = l; i < n; i += kWave) vout[i] = uint8_t(S.byte(j0 + i));
+  }
+}
+
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PBL_CW_WAVES)))
+colblk_wave_kernel(Args A) {
+  __shared__ WLds L;
+  const int l = lane_id();
+  const uint32_t nb = A.in.n_blocks;
+  const pbl_decode_out& O = A.out;
+  uint8_t* ws = reinterpret_cast<uint8_t*>(O.workspace);
+  uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
+  // a ticket only once resident: the look-back waits on smaller tickets only
+  uint32_t b = 0;
+  if (l == 0) b = g_atomic_add(reinterpret_cast<uint32_t*>(ws), 1u);
+  b = __builtin_amdgcn_readfirstlane(__shfl(b, 0, kWave));
+  if (b >= nb) return;
+  const uint32_t schema = A.in.block_format ? uint32_t(to_glb(A.in.block_format)[b]) : A.in.format;
+  const uint64_t boff = to_glb(A.in.block_off)[b];
+  const uint32_t blen = to_glb(A.in.block_len)[b];
+  // stage [0, nst) by LDS-DMA: granule i of the 16-B aligned range at head4[i]
+  const uint32_t sh = uint32_t(boff & 15);
+  const uint32_t nst = blen < kStg ? blen : kStg;
+  {
+    const gptr<const uint8_t> base = to_glb(A.in.blocks + (boff & ~uint64_t(15)));
+    const uint32_t n16 = (sh + nst + 15) >> 4;
+    for (uint32_t g0 = 0; g0 < n16; g0 += kWave)
+      if (g0 + l < n16)
+        __builtin_amdgcn_global_load_lds((gptr<const void>)(base + 16ull * (g0 + l)),
+                                         (lptr<void>)to_lds_ptr(reinterpret_cast<void*>(&L.head4[g0])), 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+  }
+  // (blocks are 8-B aligned for colblk, data_block.go:1097: the staged words
+  // keep every column's alignment; an unaligned block reads through global)
+  const bool staged = (boff & 7) == 0;
+  const Src S{(lds_cu8)to_lds(L.head4) + sh, (lds_cu8)to_lds(L.head4) + sh,
+              (glb_cu8)(A.in.blocks + boff), staged ? nst : 0u, 0xffffffffu, blen};
+  uint32_t st = parse_block_wave(S, schema, (A.in.flags & PBL_COL_TIERING) != 0, &L.d);
+  wave_sync();
+  const Desc& d = L.d;
+  const bool fast = st == PBL_OK && staged && d.key_end <= nst;
+  const uint32_t rows = st == PBL_OK ? d.rows : 0;
+  uint64_t kb = 0;
+  bool bad = false;
+  for (uint32_t r = l; r < rows; r += kWave) {
+    const RowParts p = fast ? row_parts<true>(S, d, schema, r) : row_parts<false>(S, d, schema, r);
+    bad |= !p.ok || !value_ok(S, d, r);
+    kb += p.klen;
+  }
+  kb = wave_sum(kb);
+  if (st == PBL_OK) {
+    if (__ballot(bad)) st = PBL_CORRUPT_BOUNDS;
+    else if (kb > 0xffffffffull || uint64_t(d.v_hi - d.v_lo) > 0xffffffffull) st = PBL_UNSUPPORTED;
+  }
+  const bool ok = st == PBL_OK;
+  const uint64_t agg[kNumComp] = {ok ? rows : 0u, ok ? kb : 0ull, ok ? uint64_t(d.v_hi - d.v_lo) : 0ull, 0ull};
+  lb_publish(lb_state, nb, b, agg);
+  uint64_t excl[kNumComp];
+  lb_resolve(lb_state, nb, b, agg, excl, &O.totals->status_mask);
+  uint32_t status = st;
+  if (ok && overflows(O, excl, agg)) status = PBL_OVERFLOW;
+  if (l == 0) {
+    if (status != PBL_OK && O.key_off && excl[0] + b < O.kv_cap + nb) {
+      to_glb(O.key_off)[excl[0] + b] = 0;
+      to_glb(O.val_off)[excl[0] + b] = 0;
+    }
+    write_block_meta(O, b, nb, status, excl, agg, !fast);
+  }
+  if (status != PBL_OK) return;
+  if (fast) cw_emit<true>(L, A, b, schema, S, sh, staged ? nst : 0u, excl);
+  else cw_emit<false>(L, A, b, schema, S, sh, staged ? nst : 0u, excl);
+}
+
+}  // namespace cwave
+}  // namespace col
+}  // namespace pbl
