@@ -44,7 +44,10 @@ extern "C" int pbl_decode_batch_colblk(const pbl_block_batch* batch, pbl_decode_
   // (colblk_pipe_kernel<true>) whatever the other flags say.
   const bool hide = (f & PBL_ROW_HIDE_OBSOLETE) != 0;
   const bool single = !hide && (f & PBL_KERNEL_SINGLE);
-  const bool wave = !hide && !single && (f & PBL_BATCH_VARLEN) && !(f & PBL_KERNEL_PIPE);
+#ifndef PBL_CW_ALWAYS
+#define PBL_CW_ALWAYS 0  // A/B: every colblk batch on the wave kernel
+#endif
+  const bool wave = !hide && !single && ((f & PBL_BATCH_VARLEN) || PBL_CW_ALWAYS) && !(f & PBL_KERNEL_PIPE);
   if (single) {
     hipLaunchKernelGGL(pbl::col::colblk_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
   } else if (wave) {
