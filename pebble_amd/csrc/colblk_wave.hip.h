@@ -102,6 +102,7 @@ __device__ __forceinline__ void cw_emit(WLds& L, const Args& A, uint32_t b, uint
     }
   }
 
+  CSTAMP(A, b, 5);
   // ---- keys: 64 rows at a time, built in the key buffer -------------------------
   lds_u8 kb8 = (lds_u8)to_lds(L.key4);
   const lds_cu32 KW = (lds_cu32)to_lds(L.key4);
@@ -128,6 +129,7 @@ __device__ __forceinline__ void cw_emit(WLds& L, const Args& A, uint32_t b, uint
   }
   if (l == 0) st_nt(to_glb(O.key_off) + (kvb + b + rows), cbase);
 
+  CSTAMP(A, b, 6);
   // ---- values: one contiguous range, 16-B chunks (the last ending at the end) --
   const uint32_t j0 = d.v_data + d.v_lo, n = d.v_hi - d.v_lo;
   const gptr<uint8_t> vout = to_glb(O.val_bytes) + vbb;
@@ -152,6 +154,7 @@ __device__ __forceinline__ void cw_emit(WLds& L, const Args& A, uint32_t b, uint
   }
 }
 
+#ifndef PBL_CW_SIZE_ONLY  // (rowblk_decode.hip uses the size pass only)
 __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PBL_CW_WAVES)))
 colblk_wave_kernel(Args A) {
   __shared__ WLds L;
@@ -165,6 +168,7 @@ colblk_wave_kernel(Args A) {
   if (l == 0) b = g_atomic_add(reinterpret_cast<uint32_t*>(ws), 1u);
   b = __builtin_amdgcn_readfirstlane(__shfl(b, 0, kWave));
   if (b >= nb) return;
+  CSTAMP(A, b, 0);
   const uint32_t schema = A.in.block_format ? uint32_t(to_glb(A.in.block_format)[b]) : A.in.format;
   const uint64_t boff = to_glb(A.in.block_off)[b];
   const uint32_t blen = to_glb(A.in.block_len)[b];
@@ -181,6 +185,7 @@ colblk_wave_kernel(Args A) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync();
   }
+  CSTAMP(A, b, 1);
   // (blocks are 8-B aligned for colblk, data_block.go:1097: the staged words
   // keep every column's alignment; an unaligned block reads through global)
   const bool staged = (boff & 7) == 0;
@@ -205,9 +210,11 @@ colblk_wave_kernel(Args A) {
   }
   const bool ok = st == PBL_OK;
   const uint64_t agg[kNumComp] = {ok ? rows : 0u, ok ? kb : 0ull, ok ? uint64_t(d.v_hi - d.v_lo) : 0ull, 0ull};
+  CSTAMP(A, b, 2);
   lb_publish(lb_state, nb, b, agg);
   uint64_t excl[kNumComp];
   lb_resolve(lb_state, nb, b, agg, excl, &O.totals->status_mask);
+  CSTAMP(A, b, 3);
   uint32_t status = st;
   if (ok && overflows(O, excl, agg)) status = PBL_OVERFLOW;
   if (l == 0) {
@@ -218,8 +225,80 @@ colblk_wave_kernel(Args A) {
     write_block_meta(O, b, nb, status, excl, agg, !fast);
   }
   if (status != PBL_OK) return;
+  CSTAMP(A, b, 4);
   if (fast) cw_emit<true>(L, A, b, schema, S, sh, staged ? nst : 0u, excl);
   else cw_emit<false>(L, A, b, schema, S, sh, staged ? nst : 0u, excl);
+  CSTAMP(A, b, 7);
+}
+#endif
+
+// The mixed batch's colblk size pass (rowblk_decode.hip launch_mixed step 3):
+// every colblk block of the list is staged and parsed as above and its
+// aggregate published (kHide: the visible rows, as col_emit_rows_hide counts
+// them), so the row kernel's look-back walks through them.  Resident waves
+// loop over the list; nothing waits.
+template <bool kHide>
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PBL_CW_WAVES)))
+colblk_wave_size_kernel(Args A, const uint32_t* ids) {
+  __shared__ WLds L;
+  const int l = lane_id();
+  const uint32_t nb = A.in.n_blocks;
+  uint8_t* ws = reinterpret_cast<uint8_t*>(A.out.workspace);
+  uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
+  const uint32_t n_row = __hip_atomic_load(to_glb(reinterpret_cast<uint32_t*>(ws)) + kWsRowCount, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+  for (uint32_t i = blockIdx.x; i < nb - n_row; i += gridDim.x) {
+    const uint32_t b = to_glb(ids)[n_row + i];
+    const uint32_t schema = uint32_t(to_glb(A.in.block_format)[b]);
+    const uint64_t boff = to_glb(A.in.block_off)[b];
+    const uint32_t blen = to_glb(A.in.block_len)[b];
+    const uint32_t sh = uint32_t(boff & 15), nst = blen < kStg ? blen : kStg;
+    const gptr<const uint8_t> base = to_glb(A.in.blocks + (boff & ~uint64_t(15)));
+    const uint32_t n16 = (sh + nst + 15) >> 4;
+    for (uint32_t g0 = 0; g0 < n16; g0 += kWave)
+      if (g0 + l < n16)
+        __builtin_amdgcn_global_load_lds((gptr<const void>)(base + 16ull * (g0 + l)),
+                                         (lptr<void>)to_lds_ptr(reinterpret_cast<void*>(&L.head4[g0])), 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+    const bool staged = (boff & 7) == 0;
+    const Src S{(lds_cu8)to_lds(L.head4) + sh, (lds_cu8)to_lds(L.head4) + sh,
+                (glb_cu8)(A.in.blocks + boff), staged ? nst : 0u, 0xffffffffu, blen};
+    uint32_t st = parse_block_wave(S, schema, (A.in.flags & PBL_COL_TIERING) != 0, &L.d);
+    wave_sync();
+    const Desc& d = L.d;
+    const bool fast = st == PBL_OK && staged && d.key_end <= nst;
+    const uint32_t rows = st == PBL_OK ? d.rows : 0;
+    uint64_t kb = 0, nv = 0, vb = 0;
+    bool bad = false;
+    for (uint32_t r = l; r < rows; r += kWave) {
+      const RowParts p = fast ? row_parts<true>(S, d, schema, r) : row_parts<false>(S, d, schema, r);
+      bad |= !p.ok || !value_ok(S, d, r);
+      if (!kHide || !row_obsolete(S, d, r)) {
+        kb += p.klen;
+        if (kHide) {
+          nv++;
+          vb += row_voff(S, d, r + 1) - row_voff(S, d, r);
+        }
+      }
+    }
+    kb = wave_sum(kb);
+    if (kHide) {
+      nv = wave_sum(nv);
+      vb = wave_sum(vb);
+    } else {
+      nv = rows;
+      vb = uint64_t(d.v_hi - d.v_lo);
+    }
+    if (st == PBL_OK) {
+      if (__ballot(bad)) st = PBL_CORRUPT_BOUNDS;
+      else if (kb > 0xffffffffull || vb > 0xffffffffull) st = PBL_UNSUPPORTED;
+    }
+    const bool ok = st == PBL_OK;
+    const uint64_t agg[kNumComp] = {ok ? nv : 0u, ok ? kb : 0ull, ok ? vb : 0ull, 0ull};
+    lb_publish(lb_state, nb, b, agg);
+    wave_sync();  // (the stage and the descriptor are the next block's)
+  }
 }
 
 }  // namespace cwave

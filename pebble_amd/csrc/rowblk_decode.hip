@@ -156,6 +156,8 @@ struct GlbRd {  // unstaged block in global memory
 
 #define PBL_COL_PIPE_BODY_ONLY
 #include "colblk_pipe.hip.h"
+#define PBL_CW_SIZE_ONLY
+#include "colblk_wave.hip.h"
 
 namespace pbl {
 namespace row {
@@ -463,14 +465,25 @@ int launch_mixed(const pbl_block_batch* batch, const pbl::Args& a, hipStream_t s
                          : reinterpret_cast<const void*>(pbl::row::mixed_col_kernel<false>);
   const uint64_t g_c = pbl::persistent_grid(st, hide ? pbl::kKMixedColHide : pbl::kKMixedCol, cfn, nb, &cus);
   if (!g_c) return PBL_DEVICE_ERROR;
-  const uint32_t g_cs = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 32));
   const uint32_t small = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4));
   const uint32_t* cids = static_cast<const uint32_t*>(ids);
   launch_big_sizes(a, st, small);
-  if (hide)
-    hipLaunchKernelGGL(pbl::row::mixed_col_size_kernel<true>, dim3(g_cs), dim3(pbl::kWave), 0, st, a, cids);
-  else
-    hipLaunchKernelGGL(pbl::row::mixed_col_size_kernel<false>, dim3(g_cs), dim3(pbl::kWave), 0, st, a, cids);
+#ifndef PBL_MIX_SIZE_WAVE
+#define PBL_MIX_SIZE_WAVE 1  // the colblk sizes by the staged wave form (colblk_wave.hip.h), else from global memory
+#endif
+  if (PBL_MIX_SIZE_WAVE) {
+    const uint32_t g_cs = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4 * PBL_CW_WAVES));
+    if (hide)
+      hipLaunchKernelGGL(pbl::col::cwave::colblk_wave_size_kernel<true>, dim3(g_cs), dim3(pbl::kWave), 0, st, a, cids);
+    else
+      hipLaunchKernelGGL(pbl::col::cwave::colblk_wave_size_kernel<false>, dim3(g_cs), dim3(pbl::kWave), 0, st, a, cids);
+  } else {
+    const uint32_t g_cs = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 32));
+    if (hide)
+      hipLaunchKernelGGL(pbl::row::mixed_col_size_kernel<true>, dim3(g_cs), dim3(pbl::kWave), 0, st, a, cids);
+    else
+      hipLaunchKernelGGL(pbl::row::mixed_col_size_kernel<false>, dim3(g_cs), dim3(pbl::kWave), 0, st, a, cids);
+  }
   // the row blocks on the staging-pool kernel, over the row id list
   const void* pfn = hide_rows ? reinterpret_cast<const void*>(pbl::row::pool::rowblk_pool_kernel<true>)
                               : reinterpret_cast<const void*>(pbl::row::pool::rowblk_pool_kernel<false>);
