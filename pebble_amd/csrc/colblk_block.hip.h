@@ -430,10 +430,70 @@ __device__ __forceinline__ bool value_ok(const Src& S, const Desc& d, uint32_t r
   return lo <= hi && hi <= d.v_hi;
 }
 
+// n LDS bytes src[0, n) to kb[dst, dst + n): 16 bytes per unaligned
+// ds_read_b128 / ds_write_b128 (gfx950 runs in unaligned mode), the tail by
+// the fewest narrower writes, nothing written past dst + n (the next key is
+// another lane's); reads may run up to 15 bytes past the source, inside the
+// workgroup's LDS.  Returns dst + n.
+__device__ __forceinline__ uint32_t lds_copy(lds_u8 kb, uint32_t dst, lds_cu8 src, uint32_t n) {
+  typedef u32x4 u32x4_l __attribute__((aligned(1)));
+  typedef uint64_t u64_l __attribute__((aligned(1)));
+  typedef uint32_t u32_l __attribute__((aligned(1)));
+  typedef uint16_t u16_l __attribute__((aligned(1)));
+  uint32_t c = 0;
+  for (; c + 16 <= n; c += 16)
+    *(__attribute__((address_space(3))) u32x4_l*)(kb + dst + c) =
+        *(__attribute__((address_space(3))) const u32x4_l*)(src + c);
+  if (c < n) {
+    const u32x4 w = *(__attribute__((address_space(3))) const u32x4_l*)(src + c);
+    uint64_t lo = uint64_t(w.x) | uint64_t(w.y) << 32;
+    const uint64_t hi = uint64_t(w.z) | uint64_t(w.w) << 32;
+    const uint32_t r = n - c;
+    lds_u8 o = kb + dst + c;
+    if (r & 8) { *(__attribute__((address_space(3))) u64_l*)o = lo; lo = hi; o += 8; }
+    if (r & 4) { *(__attribute__((address_space(3))) u32_l*)o = uint32_t(lo); lo >>= 32; o += 4; }
+    if (r & 2) { *(__attribute__((address_space(3))) u16_l*)o = uint16_t(lo); lo >>= 16; o += 2; }
+    if (r & 1) *o = uint8_t(lo);
+  }
+  return dst + n;
+}
+
+#ifndef PBL_COL_KEYCOPY16
+#define PBL_COL_KEYCOPY16 1  // staged keys: segment copies 16 B at a time (else byte by byte)
+#endif
+
 // MaterializeUserKey of row r into LDS bytes kb[dst ..).
 template <bool F>
 __device__ __forceinline__ void build_key(const Src& S, const Desc& d, uint32_t schema, const RowParts& p,
                                           lds_u8 kb, uint32_t dst) {
+  if (F && PBL_COL_KEYCOPY16) {  // every key byte is in the staged head
+    const lds_cu8 H = S.head;
+    dst = lds_copy(kb, dst, H + d.pb_data, d.shared_len);
+    dst = lds_copy(kb, dst, H + p.bl, p.bh - p.bl);
+    dst = lds_copy(kb, dst, H + p.sl, p.sh - p.sl);
+    if (schema == PBL_FMT_COL_CRDB1) {
+      kb[dst++] = 0;
+      if (p.wall == 0 && p.logical == 0) {
+        if (p.uh > p.ul) {
+          dst = lds_copy(kb, dst, H + p.ul, p.uh - p.ul);
+          kb[dst++] = uint8_t(p.uh - p.ul + 1);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; i++) kb[dst++] = uint8_t(p.wall >> (56 - 8 * i));
+        if (p.logical == 0) {
+          kb[dst++] = 9;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; i++) kb[dst++] = uint8_t(p.logical >> (24 - 8 * i));
+          kb[dst++] = 13;
+        }
+      }
+    } else {
+      lds_copy(kb, dst, H + p.ul, p.uh - p.ul);
+    }
+    return;
+  }
   for (uint32_t i = 0; i < d.shared_len; i++) kb[dst++] = uint8_t(key_byte<F>(S, d.pb_data + i));
   for (uint32_t o = p.bl; o < p.bh; o++) kb[dst++] = uint8_t(key_byte<F>(S, o));
   for (uint32_t o = p.sl; o < p.sh; o++) kb[dst++] = uint8_t(key_byte<F>(S, o));

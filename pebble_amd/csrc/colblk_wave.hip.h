@@ -42,6 +42,13 @@ namespace cwave {
 #ifndef PBL_CW_WAVES
 #define PBL_CW_WAVES 4  // waves per SIMD (one wave per workgroup)
 #endif
+// Look-back windows (of 64 predecessors) per round trip.  With 16 blocks in
+// flight per CU the nearest inclusive prefix sits far back, and a resolve
+// that covers less ticket time per round trip than the round trip lasts
+// never catches up (2 windows: look-back median 96 K cycles on config 5).
+#ifndef PBL_CW_LBWIN
+#define PBL_CW_LBWIN 8
+#endif
 constexpr uint32_t kStg = PBL_CW_STAGE;
 constexpr uint32_t kKb = PBL_CW_KEYBUF;
 constexpr int kVU = PBL_CW_VALU;
@@ -213,7 +220,7 @@ colblk_wave_kernel(Args A) {
   CSTAMP(A, b, 2);
   lb_publish(lb_state, nb, b, agg);
   uint64_t excl[kNumComp];
-  lb_resolve(lb_state, nb, b, agg, excl, &O.totals->status_mask);
+  lb_resolve<PBL_CW_LBWIN>(lb_state, nb, b, agg, excl, &O.totals->status_mask);
   CSTAMP(A, b, 3);
   uint32_t status = st;
   if (ok && overflows(O, excl, agg)) status = PBL_OVERFLOW;
