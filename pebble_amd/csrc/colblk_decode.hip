@@ -1,6 +1,8 @@
 // colblk_decode.hip — gfx950 decoder for batches of Pebble columnar (colblk)
 // data blocks (colblk.DefaultKeySchema / cockroachkvs "crdb1").  One 256-thread
 // workgroup per block in ticket order; per-block work in colblk_block.hip.h.
+#include <algorithm>
+
 #include "common.hip.h"
 #include "colblk_block.hip.h"
 #include "colblk_pipe.hip.h"
@@ -44,12 +46,29 @@ extern "C" int pbl_decode_batch_colblk(const pbl_block_batch* batch, pbl_decode_
   // (colblk_pipe_kernel<true>) whatever the other flags say.
   const bool hide = (f & PBL_ROW_HIDE_OBSOLETE) != 0;
   const bool single = !hide && (f & PBL_KERNEL_SINGLE);
+#ifndef PBL_CW_TWOPASS
+#define PBL_CW_TWOPASS 1  // the wave form in two passes (sizes + scan, then outputs) instead of one with a look-back
+#endif
 #ifndef PBL_CW_ALWAYS
 #define PBL_CW_ALWAYS 0  // A/B: every colblk batch on the wave kernel
 #endif
   const bool wave = !hide && !single && ((f & PBL_BATCH_VARLEN) || PBL_CW_ALWAYS) && !(f & PBL_KERNEL_PIPE);
   if (single) {
     hipLaunchKernelGGL(pbl::col::colblk_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
+  } else if (wave && PBL_CW_TWOPASS) {
+    // sizes (no waiting), the bases scan, then every block's outputs with no
+    // look-back (colblk_wave.hip.h)
+    int dev = 0, cus = 256;
+    if (hipStreamGetDevice(st, &dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return PBL_DEVICE_ERROR;
+    const uint32_t g_s = uint32_t(std::min<uint64_t>(batch->n_blocks, uint64_t(cus) * 4 * PBL_CW_WAVES));
+    const uint32_t nt = (batch->n_blocks + pbl::col::cwave::kScanTile - 1) / pbl::col::cwave::kScanTile;
+    hipLaunchKernelGGL((pbl::col::cwave::colblk_wave_size_kernel<false, false>), dim3(g_s), dim3(pbl::kWave), 0, st, a,
+                       static_cast<const uint32_t*>(nullptr));
+    hipLaunchKernelGGL(pbl::col::cwave::colblk_bases_scan_kernel, dim3(std::min<uint32_t>(nt, uint32_t(cus) * 2)),
+                       dim3(pbl::kTPB), 0, st, a);
+    hipLaunchKernelGGL(pbl::col::cwave::colblk_wave_emit_kernel, dim3(batch->n_blocks), dim3(pbl::kWave), 0, st, a);
   } else if (wave) {
     hipLaunchKernelGGL(pbl::col::cwave::colblk_wave_kernel, dim3(batch->n_blocks), dim3(pbl::kWave), 0, st, a);
   } else {

@@ -239,27 +239,36 @@ colblk_wave_kernel(Args A) {
 }
 #endif
 
-// The mixed batch's colblk size pass (rowblk_decode.hip launch_mixed step 3):
-// every colblk block of the list is staged and parsed as above and its
-// aggregate published (kHide: the visible rows, as col_emit_rows_hide counts
-// them), so the row kernel's look-back walks through them.  Resident waves
-// loop over the list; nothing waits.
-template <bool kHide>
+// Size pass of the wave form: stage (the first kSStg bytes: header and key
+// columns of config 5's blocks; anything past them is read through the global
+// reader), parse, count; kHide counts the visible rows, as col_emit_rows_hide
+// places them.  kList: the colblk blocks of a mixed batch (the id list past
+// its row ids; every aggregate is PUBLISHED to the look-back state, so the row
+// kernel walks through them); else every block of a colblk batch, whose
+// aggregate and status go to blk_{kv,key,val}_base[b] / blk_status[b] for
+// colblk_bases_scan_kernel.  Resident waves loop over the blocks; nothing waits.
+#ifndef PBL_CW_SSTAGE
+#define PBL_CW_SSTAGE 2048
+#endif
+template <bool kList, bool kHide>
 __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PBL_CW_WAVES)))
 colblk_wave_size_kernel(Args A, const uint32_t* ids) {
   __shared__ WLds L;
   const int l = lane_id();
   const uint32_t nb = A.in.n_blocks;
-  uint8_t* ws = reinterpret_cast<uint8_t*>(A.out.workspace);
+  const pbl_decode_out& O = A.out;
+  uint8_t* ws = reinterpret_cast<uint8_t*>(O.workspace);
   uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
-  const uint32_t n_row = __hip_atomic_load(to_glb(reinterpret_cast<uint32_t*>(ws)) + kWsRowCount, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t n_row = kList ? __hip_atomic_load(to_glb(reinterpret_cast<uint32_t*>(ws)) + kWsRowCount,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : 0u;
+  constexpr uint32_t kS = kList ? kStg : (PBL_CW_SSTAGE < kStg ? PBL_CW_SSTAGE : kStg);
   for (uint32_t i = blockIdx.x; i < nb - n_row; i += gridDim.x) {
-    const uint32_t b = to_glb(ids)[n_row + i];
-    const uint32_t schema = uint32_t(to_glb(A.in.block_format)[b]);
+    const uint32_t b = kList ? to_glb(ids)[n_row + i] : i;
+    const uint32_t schema = A.in.block_format ? uint32_t(to_glb(A.in.block_format)[b]) : A.in.format;
     const uint64_t boff = to_glb(A.in.block_off)[b];
     const uint32_t blen = to_glb(A.in.block_len)[b];
-    const uint32_t sh = uint32_t(boff & 15), nst = blen < kStg ? blen : kStg;
+    const uint32_t sh = uint32_t(boff & 15), nst = blen < kS ? blen : kS;
     const gptr<const uint8_t> base = to_glb(A.in.blocks + (boff & ~uint64_t(15)));
     const uint32_t n16 = (sh + nst + 15) >> 4;
     for (uint32_t g0 = 0; g0 < n16; g0 += kWave)
@@ -303,9 +312,146 @@ colblk_wave_size_kernel(Args A, const uint32_t* ids) {
     }
     const bool ok = st == PBL_OK;
     const uint64_t agg[kNumComp] = {ok ? nv : 0u, ok ? kb : 0ull, ok ? vb : 0ull, 0ull};
-    lb_publish(lb_state, nb, b, agg);
+    if (kList) {
+      lb_publish(lb_state, nb, b, agg);
+    } else if (l == 0) {
+      to_glb(O.blk_kv_base)[b] = agg[0];
+      to_glb(O.blk_key_base)[b] = agg[1];
+      to_glb(O.blk_val_base)[b] = agg[2];
+      to_glb(O.blk_status)[b] = st;
+    }
     wave_sync();  // (the stage and the descriptor are the next block's)
   }
+}
+
+// Exclusive scan, in place, of the per-block counts the size pass left in
+// blk_{kv,key,val}_base[0, n): tiles of 1024 blocks per 256-thread workgroup
+// in ticket order, each tile's aggregate published and its prefix resolved by
+// the decoupled look-back (tf_scan_kernel's form); [n] gets the batch totals,
+// blk_rst_base (colblk: no restarts) zeros.
+constexpr uint32_t kScanTile = 1024;
+__global__ void __launch_bounds__(kTPB) colblk_bases_scan_kernel(Args A) {
+  __shared__ uint32_t s_tile;
+  __shared__ uint64_t s_wsum[kTPB / kWave][3];
+  __shared__ uint64_t s_excl[3];
+  const pbl_decode_out& O = A.out;
+  uint8_t* ws = reinterpret_cast<uint8_t*>(O.workspace);
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(ws);
+  uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
+  const uint32_t nb = A.in.n_blocks, nt = (nb + kScanTile - 1) / kScanTile, t = threadIdx.x;
+  for (;;) {
+    if (t == 0) s_tile = g_atomic_add(hdr + 1, 1u);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    __syncthreads();  // (s_tile is rewritten next iteration)
+    if (tile >= nt) return;
+    const uint32_t b0 = tile * kScanTile + 4 * t;
+    uint64_t c[4][3], s3[3] = {0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const bool in = b0 + k < nb;
+      c[k][0] = in ? to_glb(O.blk_kv_base)[b0 + k] : 0;
+      c[k][1] = in ? to_glb(O.blk_key_base)[b0 + k] : 0;
+      c[k][2] = in ? to_glb(O.blk_val_base)[b0 + k] : 0;
+#pragma unroll
+      for (int q = 0; q < 3; q++) s3[q] += c[k][q];
+    }
+    uint64_t in3[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) in3[q] = wave_incl_scan(s3[q]);
+    if (lane_id() == kWave - 1)
+      for (int q = 0; q < 3; q++) s_wsum[wave_id()][q] = in3[q];
+    __syncthreads();
+    uint64_t before[3] = {0, 0, 0}, agg[kNumComp] = {0, 0, 0, 0};
+    for (int w = 0; w < kTPB / kWave; w++)
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        if (w < wave_id()) before[q] += s_wsum[w][q];
+        agg[q] += s_wsum[w][q];
+      }
+    if (wave_id() == 0) {
+      uint64_t excl[kNumComp];
+      lb_publish(lb_state, nt, tile, agg);
+      lb_resolve(lb_state, nt, tile, agg, excl, &O.totals->status_mask);
+      if (lane_id() == 0)
+        for (int q = 0; q < 3; q++) s_excl[q] = excl[q];
+    }
+    __syncthreads();
+    uint64_t e[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) e[q] = s_excl[q] + before[q] + in3[q] - s3[q];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t b = b0 + k;
+      if (b < nb) {
+        to_glb(O.blk_kv_base)[b] = e[0];
+        to_glb(O.blk_key_base)[b] = e[1];
+        to_glb(O.blk_val_base)[b] = e[2];
+        if (O.blk_rst_base) to_glb(O.blk_rst_base)[b] = 0;
+#pragma unroll
+        for (int q = 0; q < 3; q++) e[q] += c[k][q];
+      }
+    }
+    if (tile == nt - 1 && t == 0) {
+      to_glb(O.blk_kv_base)[nb] = s_excl[0] + agg[0];
+      to_glb(O.blk_key_base)[nb] = s_excl[1] + agg[1];
+      to_glb(O.blk_val_base)[nb] = s_excl[2] + agg[2];
+      if (O.blk_rst_base) to_glb(O.blk_rst_base)[nb] = 0;
+    }
+  }
+}
+
+// Emit pass of the two-pass wave form: block b's bases are final (the scan),
+// so there is no look-back and the waves never wait on one another.  The
+// block is staged and parsed again; its status and aggregate are the size
+// pass's.  Per-block results, totals and the overflow check as the one-pass
+// kernels (write_block_meta).
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PBL_CW_WAVES)))
+colblk_wave_emit_kernel(Args A) {
+  __shared__ WLds L;
+  const int l = lane_id();
+  const uint32_t nb = A.in.n_blocks, b = blockIdx.x;
+  const pbl_decode_out& O = A.out;
+  CSTAMP(A, b, 0);
+  const uint64_t excl[kNumComp] = {to_glb(O.blk_kv_base)[b], to_glb(O.blk_key_base)[b], to_glb(O.blk_val_base)[b], 0};
+  const uint64_t agg[kNumComp] = {to_glb(O.blk_kv_base)[b + 1] - excl[0], to_glb(O.blk_key_base)[b + 1] - excl[1],
+                                  to_glb(O.blk_val_base)[b + 1] - excl[2], 0};
+  const uint32_t st = to_glb(O.blk_status)[b];
+  uint32_t status = st;
+  if (st == PBL_OK && overflows(O, excl, agg)) status = PBL_OVERFLOW;
+  if (l == 0) {
+    if (status != PBL_OK && O.key_off && excl[0] + b < O.kv_cap + nb) {
+      to_glb(O.key_off)[excl[0] + b] = 0;
+      to_glb(O.val_off)[excl[0] + b] = 0;
+    }
+    write_block_meta(O, b, nb, status, excl, agg, false);
+  }
+  if (status != PBL_OK) return;
+  const uint32_t schema = A.in.block_format ? uint32_t(to_glb(A.in.block_format)[b]) : A.in.format;
+  const uint64_t boff = to_glb(A.in.block_off)[b];
+  const uint32_t blen = to_glb(A.in.block_len)[b];
+  const uint32_t sh = uint32_t(boff & 15);
+  const uint32_t nst = blen < kStg ? blen : kStg;
+  {
+    const gptr<const uint8_t> base = to_glb(A.in.blocks + (boff & ~uint64_t(15)));
+    const uint32_t n16 = (sh + nst + 15) >> 4;
+    for (uint32_t g0 = 0; g0 < n16; g0 += kWave)
+      if (g0 + l < n16)
+        __builtin_amdgcn_global_load_lds((gptr<const void>)(base + 16ull * (g0 + l)),
+                                         (lptr<void>)to_lds_ptr(reinterpret_cast<void*>(&L.head4[g0])), 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+  }
+  CSTAMP(A, b, 1);
+  const bool staged = (boff & 7) == 0;
+  const Src S{(lds_cu8)to_lds(L.head4) + sh, (lds_cu8)to_lds(L.head4) + sh,
+              (glb_cu8)(A.in.blocks + boff), staged ? nst : 0u, 0xffffffffu, blen};
+  parse_block_wave(S, schema, (A.in.flags & PBL_COL_TIERING) != 0, &L.d);  // (OK: the size pass parsed it)
+  wave_sync();
+  CSTAMP(A, b, 4);
+  if (staged && L.d.key_end <= nst) cw_emit<true>(L, A, b, schema, S, sh, nst, excl);
+  else cw_emit<false>(L, A, b, schema, S, sh, staged ? nst : 0u, excl);
+  CSTAMP(A, b, 7);
 }
 
 }  // namespace cwave
