@@ -474,10 +474,10 @@ int launch_mixed(const pbl_block_batch* batch, const pbl::Args& a, hipStream_t s
   if (PBL_MIX_SIZE_WAVE) {
     const uint32_t g_cs = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4 * PBL_CW_WAVES));
     if (hide)
-      hipLaunchKernelGGL(pbl::col::cwave::colblk_wave_size_kernel<true, true>, dim3(g_cs), dim3(pbl::kWave), 0, st, a,
+      hipLaunchKernelGGL((pbl::col::cwave::colblk_wave_size_kernel<true, true>), dim3(g_cs), dim3(pbl::kWave), 0, st, a,
                          cids);
     else
-      hipLaunchKernelGGL(pbl::col::cwave::colblk_wave_size_kernel<true, false>, dim3(g_cs), dim3(pbl::kWave), 0, st, a,
+      hipLaunchKernelGGL((pbl::col::cwave::colblk_wave_size_kernel<true, false>), dim3(g_cs), dim3(pbl::kWave), 0, st, a,
                          cids);
   } else {
     const uint32_t g_cs = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 32));
