@@ -324,6 +324,7 @@ colblk_wave_size_kernel(Args A, const uint32_t* ids) {
   }
 }
 
+#ifndef PBL_CW_SIZE_ONLY  // (rowblk_decode.hip uses the size pass only)
 // Exclusive scan, in place, of the per-block counts the size pass left in
 // blk_{kv,key,val}_base[0, n): tiles of 1024 blocks per 256-thread workgroup
 // in ticket order, each tile's aggregate published and its prefix resolved by
@@ -453,6 +454,7 @@ colblk_wave_emit_kernel(Args A) {
   else cw_emit<false>(L, A, b, schema, S, sh, staged ? nst : 0u, excl);
   CSTAMP(A, b, 7);
 }
+#endif
 
 }  // namespace cwave
 }  // namespace col
