@@ -248,7 +248,9 @@ def workload_info(a, nb, N):
             ("every 10th a config-5 Zipf block (restart interval 16)" if a.mix == "zipf10" else
              "every 8th a short table-tail block (2 / 4 / 8 KiB)"))
     if a.workload == "col":
-        kernel = "colblk_decode_kernel" if a.kernel == "single" and not a.hide else "colblk_pipe_kernel"
+        kernel = ("colblk_decode_kernel" if a.kernel == "single" and not a.hide else
+                  "colblk_pipe_kernel" if a.hide or a.kernel == "pipe" else
+                  "colblk_wave_size_kernel+colblk_bases_scan_kernel+colblk_wave_emit_kernel")
         return N.PBL_FMT_COL_CRDB1, kernel, (
             f"config3: {nb} x {a.block_size // 1024} KiB colblk blocks per GPU, cockroachkvs crdb1 schema "
             f"(KeyGenConfig alphabet 26, RoachKeyLen 12, PrefixLenShared 4, 1 key/prefix), 128 B values"
@@ -256,18 +258,17 @@ def workload_info(a, nb, N):
             + (f", Pebblev8 tiering columns (span ids 1..{a.tiering}) decoded to per-KV KVMeta" if a.tiering else ""))
     if a.workload == "zipf":
         fmt = N.PBL_FMT_ROW if a.zipf_format == "row" else N.PBL_FMT_COL_DEFAULT
-        # (a VARLEN colblk batch takes the one-block-per-workgroup kernel unless
-        # --kernel names another; row batches ignore the hint)
-        vl = a.kernel not in ("pipe", "single")
         kernel = (row_kernel if fmt == N.PBL_FMT_ROW
-                  else "colblk_decode_kernel" if vl or a.kernel == "single" else "colblk_pipe_kernel")
+                  else "colblk_decode_kernel" if a.kernel == "single" else "colblk_pipe_kernel" if a.kernel == "pipe"
+                  else "colblk_wave_size_kernel+colblk_bases_scan_kernel+colblk_wave_emit_kernel")
         return fmt, kernel, (f"config5: {nb} variable-length blocks per GPU targeting {a.block_size // 1024} KiB, "
                              + (f"row format, restart interval {a.restart_interval}" if fmt == N.PBL_FMT_ROW
                                 else "colblk DefaultKeySchema")
                              + ", Zipf(1.1) key lengths 8-1024 B / value lengths 0-64 KiB")
     # (the sequential mixed path: split + colblk size pass + the row
     # staging-pool kernel over the row ids + colblk pipeline, timed together)
-    return N.PBL_FMT_ROW, "mixed_col_size_kernel+rowblk_pool_kernel+mixed_col_kernel", (
+    return N.PBL_FMT_ROW, ("colblk_wave_size_kernel+rowblk_pool_kernel+" +
+                           ("mixed_col_kernel" if a.hide else "colblk_wave_emit_kernel")), (
         f"config4 shard: {nb} x {a.block_size // 1024} KiB blocks per GPU, even ids row-format "
         f"(config-2 shape), odd ids colblk crdb1 (config-3 shape)")
 

@@ -36,41 +36,35 @@ extern "C" int pbl_decode_batch_colblk(const pbl_block_batch* batch, pbl_decode_
   pbl::Args a;
   a.in = *batch;
   a.out = *out;
-  // default: the persistent lagged-look-back kernel (colblk_pipe.hip.h).
-  // PBL_BATCH_VARLEN batches take the wave-per-block kernel (colblk_wave.hip.h)
-  // unless PBL_KERNEL_PIPE forces the pipeline (its one-iteration look-back lag
-  // convoys behind long blocks); PBL_KERNEL_SINGLE (A/B) the one-block-per-
-  // workgroup kernel.
+  // default: the two-pass wave form (colblk_wave.hip.h): sizes, the bases
+  // scan, then every block's outputs with no look-back.  HideObsoletePoints
+  // (PBL_ROW_HIDE_OBSOLETE) is fused into the pipeline (colblk_pipe_kernel
+  // <true>); PBL_KERNEL_PIPE / PBL_KERNEL_SINGLE force the pipeline / the
+  // one-block-per-workgroup kernel (A/B).
   const uint32_t f = batch->flags;
-  // HideObsoletePoints (PBL_ROW_HIDE_OBSOLETE) is fused into the pipeline
-  // (colblk_pipe_kernel<true>) whatever the other flags say.
   const bool hide = (f & PBL_ROW_HIDE_OBSOLETE) != 0;
-  const bool single = !hide && (f & PBL_KERNEL_SINGLE);
-#ifndef PBL_CW_TWOPASS
-#define PBL_CW_TWOPASS 1  // the wave form in two passes (sizes + scan, then outputs) instead of one with a look-back
-#endif
-#ifndef PBL_CW_ALWAYS
-#define PBL_CW_ALWAYS 0  // A/B: every colblk batch on the wave kernel
-#endif
-  const bool wave = !hide && !single && ((f & PBL_BATCH_VARLEN) || PBL_CW_ALWAYS) && !(f & PBL_KERNEL_PIPE);
-  if (single) {
+  if (!hide && (f & PBL_KERNEL_SINGLE)) {
     hipLaunchKernelGGL(pbl::col::colblk_decode_kernel, dim3(batch->n_blocks), dim3(pbl::kTPB), 0, st, a);
-  } else if (wave && PBL_CW_TWOPASS) {
-    // sizes (no waiting), the bases scan, then every block's outputs with no
-    // look-back (colblk_wave.hip.h)
+  } else if (!hide && !(f & PBL_KERNEL_PIPE)) {
     int dev = 0, cus = 256;
     if (hipStreamGetDevice(st, &dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       return PBL_DEVICE_ERROR;
+    namespace cw = pbl::col::cwave;
     const uint32_t g_s = uint32_t(std::min<uint64_t>(batch->n_blocks, uint64_t(cus) * 4 * PBL_CW_WAVES));
-    const uint32_t nt = (batch->n_blocks + pbl::col::cwave::kScanTile - 1) / pbl::col::cwave::kScanTile;
-    hipLaunchKernelGGL((pbl::col::cwave::colblk_wave_size_kernel<false, false>), dim3(g_s), dim3(pbl::kWave), 0, st, a,
-                       static_cast<const uint32_t*>(nullptr));
-    hipLaunchKernelGGL(pbl::col::cwave::colblk_bases_scan_kernel, dim3(std::min<uint32_t>(nt, uint32_t(cus) * 2)),
-                       dim3(pbl::kTPB), 0, st, a);
-    hipLaunchKernelGGL(pbl::col::cwave::colblk_wave_emit_kernel, dim3(batch->n_blocks), dim3(pbl::kWave), 0, st, a);
-  } else if (wave) {
-    hipLaunchKernelGGL(pbl::col::cwave::colblk_wave_kernel, dim3(batch->n_blocks), dim3(pbl::kWave), 0, st, a);
+    const uint32_t nt = (batch->n_blocks + cw::kScanTile - 1) / cw::kScanTile;
+    const uint32_t* no_ids = nullptr;
+    hipLaunchKernelGGL((cw::colblk_wave_size_kernel<false, false>), dim3(g_s), dim3(pbl::kWave), 0, st, a, no_ids);
+    hipLaunchKernelGGL(cw::colblk_bases_scan_kernel, dim3(std::min<uint32_t>(nt, uint32_t(cus) * 2)), dim3(pbl::kTPB),
+                       0, st, a);
+    // variable-length blocks (config 5: one long values range each) read more
+    // of their values from a larger stage
+    if (f & PBL_BATCH_VARLEN)
+      hipLaunchKernelGGL((cw::colblk_wave_emit_kernel<PBL_CW_STAGE_VARLEN, false>), dim3(batch->n_blocks),
+                         dim3(pbl::kWave), 0, st, a, no_ids);
+    else
+      hipLaunchKernelGGL((cw::colblk_wave_emit_kernel<PBL_CW_STAGE, false>), dim3(batch->n_blocks), dim3(pbl::kWave),
+                         0, st, a, no_ids);
   } else {
     const void* fn = hide ? reinterpret_cast<const void*>(pbl::col::cpipe::colblk_pipe_kernel<true>)
                           : reinterpret_cast<const void*>(pbl::col::cpipe::colblk_pipe_kernel<false>);

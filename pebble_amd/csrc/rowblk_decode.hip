@@ -232,78 +232,19 @@ __global__ void __launch_bounds__(kTPB) mixed_split_scatter_kernel(Args A, const
   }
 }
 
-// Mixed batches: persistent launches over the split id lists.  (1)
-// mixed_col_size_kernel parses every colblk block and publishes its aggregate;
-// (2) the row kernel runs over the row list, its look-back walking through the
-// colblk aggregates; (3) mixed_col_kernel runs over
-// the colblk list (its predecessors' prefixes are all published: its look-back
-// ends at the row block before it).  Deadlock-free: (2) waits only on
-// aggregates published by (1) or by its own resident waves in ticket order,
-// (3) on aggregates published by (1) and its own workgroups.
+// Mixed batches: launches over the split id lists.  (1) the colblk sizes are
+// published (colblk_wave_size_kernel<true>, colblk_wave.hip.h); (2) the row
+// kernel runs over the row list, its look-back walking through the colblk
+// aggregates; (3) the colblk blocks' outputs (mixed_col_kernel below with
+// HideObsoletePoints, else the wave form's emit): every predecessor has
+// published, so their look-backs end at the row block before them.
+// Deadlock-free: (2) waits only on aggregates published by (1) or by its own
+// resident waves in ticket order, (3) never waits.
 constexpr int kWsColTick2 = 4;  // header u32 [4]: the colblk queue of launch (3)
 
-// (1): one wave per colblk block, straight from global memory (no staging: a
-// size needs the header, the key columns' offsets and the value bounds only),
-// many waves per CU to hide the latency (measured: a 256-thread workgroup per
-// block 0.73 ms, a wave per block 0.47 ms on config 4's 64 Ki colblk blocks).
-// Same parse_block_wave / row_parts / value_ok as the pipeline, so the
-// aggregate is the one the pipeline publishes again in (3).
-#ifndef PBL_COL_SIZE_WAVES
-#define PBL_COL_SIZE_WAVES 8  // waves per SIMD (64 VGPRs): config 4 951 at 4 (101 VGPRs), 975 at 8
-#endif
-// kHide (PBL_ROW_HIDE_OBSOLETE): the aggregate counts the visible rows, as
-// col_rows_hide publishes it again in (3).
-template <bool kHide>
-__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PBL_COL_SIZE_WAVES)))
-mixed_col_size_kernel(Args A, const uint32_t* ids) {
-  __shared__ col::Desc d;
-  const uint32_t nb = A.in.n_blocks;
-  uint32_t* hdr = reinterpret_cast<uint32_t*>(A.out.workspace);
-  uint64_t* lb_state = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(A.out.workspace) + kWsHeader);
-  const uint32_t n_row = __hip_atomic_load(to_glb(hdr) + kWsRowCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t n_col = nb - n_row;
-  for (uint32_t i = blockIdx.x; i < n_col; i += gridDim.x) {
-    const uint32_t b = to_glb(ids)[n_row + i];
-    const uint32_t blen = to_glb(A.in.block_len)[b];
-    const uint32_t schema = to_glb(A.in.block_format)[b];
-    const col::Src S{nullptr, nullptr, (col::glb_cu8)(A.in.blocks + to_glb(A.in.block_off)[b]), 0u, 0xffffffffu, blen};
-    uint32_t st = col::parse_block_wave(S, schema, (A.in.flags & PBL_COL_TIERING) != 0, &d);
-    const uint32_t rows = st == PBL_OK ? d.rows : 0;
-    uint64_t kb = 0, nv = 0, vb = 0;
-    bool bad = false;
-    // (not unrolled: 4 rows per lane in flight measured 0.89 against 0.47 ms)
-    for (uint32_t r = lane_id(); r < rows; r += kWave) {
-      const col::RowParts p = col::row_parts<false>(S, d, schema, r);
-      bad |= !p.ok || !col::value_ok(S, d, r);
-      if (!kHide || !col::row_obsolete(S, d, r)) {
-        kb += p.klen;
-        if (kHide) {
-          nv++;
-          vb += col::row_voff(S, d, r + 1) - col::row_voff(S, d, r);
-        }
-      }
-    }
-    kb = wave_sum(kb);
-    if (kHide) {
-      nv = wave_sum(nv);
-      vb = wave_sum(vb);
-    } else {
-      nv = rows;
-      vb = uint64_t(d.v_hi - d.v_lo);
-    }
-    if (st == PBL_OK) {
-      if (__ballot(bad)) st = PBL_CORRUPT_BOUNDS;
-      else if (kb > 0xffffffffull || vb > 0xffffffffull) st = PBL_UNSUPPORTED;
-    }
-    const bool ok = st == PBL_OK;
-    const uint64_t agg[kNumComp] = {ok ? nv : 0u, ok ? kb : 0ull, ok ? vb : 0ull, 0ull};
-    lb_publish(lb_state, nb, b, agg);
-    wave_sync();  // (d is rewritten by the next block's parse)
-  }
-}
-
-// (3): the colblk pipeline over the colblk list; kHide: HideObsoletePoints
-// fused (the visible rows, as mixed_col_size_kernel<true> counted them).
+// (3) with HideObsoletePoints: the colblk pipeline's fused form over the
+// colblk list (the visible rows, as colblk_wave_size_kernel<true, true>
+// counted them).
 template <bool kHide>
 __global__ void __launch_bounds__(kTPB, PBL_COL_PIPE_WG) mixed_col_kernel(Args A, const uint32_t* ids) {
   __shared__ col::cpipe::CLds L;
@@ -468,24 +409,14 @@ int launch_mixed(const pbl_block_batch* batch, const pbl::Args& a, hipStream_t s
   const uint32_t small = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4));
   const uint32_t* cids = static_cast<const uint32_t*>(ids);
   launch_big_sizes(a, st, small);
-#ifndef PBL_MIX_SIZE_WAVE
-#define PBL_MIX_SIZE_WAVE 1  // the colblk sizes by the staged wave form (colblk_wave.hip.h), else from global memory
-#endif
-  if (PBL_MIX_SIZE_WAVE) {
-    const uint32_t g_cs = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4 * PBL_CW_WAVES));
-    if (hide)
-      hipLaunchKernelGGL((pbl::col::cwave::colblk_wave_size_kernel<true, true>), dim3(g_cs), dim3(pbl::kWave), 0, st, a,
-                         cids);
-    else
-      hipLaunchKernelGGL((pbl::col::cwave::colblk_wave_size_kernel<true, false>), dim3(g_cs), dim3(pbl::kWave), 0, st, a,
-                         cids);
-  } else {
-    const uint32_t g_cs = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 32));
-    if (hide)
-      hipLaunchKernelGGL(pbl::row::mixed_col_size_kernel<true>, dim3(g_cs), dim3(pbl::kWave), 0, st, a, cids);
-    else
-      hipLaunchKernelGGL(pbl::row::mixed_col_size_kernel<false>, dim3(g_cs), dim3(pbl::kWave), 0, st, a, cids);
-  }
+  // (3) the colblk sizes, published (the staged wave form, colblk_wave.hip.h)
+  const uint32_t g_cs = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4 * PBL_CW_WAVES));
+  if (hide)
+    hipLaunchKernelGGL((pbl::col::cwave::colblk_wave_size_kernel<true, true>), dim3(g_cs), dim3(pbl::kWave), 0, st, a,
+                       cids);
+  else
+    hipLaunchKernelGGL((pbl::col::cwave::colblk_wave_size_kernel<true, false>), dim3(g_cs), dim3(pbl::kWave), 0, st,
+                       a, cids);
   // the row blocks on the staging-pool kernel, over the row id list
   const void* pfn = hide_rows ? reinterpret_cast<const void*>(pbl::row::pool::rowblk_pool_kernel<true>)
                               : reinterpret_cast<const void*>(pbl::row::pool::rowblk_pool_kernel<false>);
@@ -499,8 +430,17 @@ int launch_mixed(const pbl_block_batch* batch, const pbl::Args& a, hipStream_t s
   else
     hipLaunchKernelGGL(pbl::row::pool::rowblk_pool_kernel<false>, dim3(uint32_t(g_p)), dim3(pbl::row::pool::kTPBP), 0,
                        st, a, cids);
+  // (5) the colblk blocks: with HideObsoletePoints the pipeline's fused form;
+  // else the wave form's emit over the colblk list, whose look-back finds
+  // every predecessor published (the row kernel has finished)
+#ifndef PBL_MIX_COL_WAVE
+#define PBL_MIX_COL_WAVE 1
+#endif
   if (hide)
     hipLaunchKernelGGL(pbl::row::mixed_col_kernel<true>, dim3(uint32_t(g_c)), dim3(pbl::kTPB), 0, st, a, cids);
+  else if (PBL_MIX_COL_WAVE)
+    hipLaunchKernelGGL((pbl::col::cwave::colblk_wave_emit_kernel<PBL_CW_STAGE, true>), dim3(nb), dim3(pbl::kWave), 0,
+                       st, a, cids);
   else
     hipLaunchKernelGGL(pbl::row::mixed_col_kernel<false>, dim3(uint32_t(g_c)), dim3(pbl::kTPB), 0, st, a, cids);
   if (values) launch_big_values(a, st, small);

@@ -16,6 +16,9 @@ from pebble_amd.rowblk import CorruptionError, Transforms, gen_row_blocks, kvs_o
 from test_rowblk_gpu import ARRAYS, assert_same, pack
 
 pytestmark = pytest.mark.gpu
+# the colblk paths: the default two-pass wave form (colblk_wave.hip.h; fixed and
+# variable-length stages), the pipeline and the one-block-per-workgroup kernel
+KERNELS = {"wave": 0, "wave_varlen": N.PBL_BATCH_VARLEN, "pipe": N.PBL_KERNEL_PIPE, "single": N.PBL_KERNEL_SINGLE}
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "colblk_golden.json")
 
 
@@ -47,8 +50,9 @@ def test_reference_blocks_on_gpu():
             assert [kv.value for kv in kvs] == [bytes.fromhex(r["value"]) for r in c["rows"]], c["name"]
 
 
+@pytest.mark.parametrize("kernel", list(KERNELS))
 @pytest.mark.parametrize("schema", [SCHEMA_DEFAULT, SCHEMA_CRDB1])
-def test_random_blocks(schema):
+def test_random_blocks(schema, kernel):
     rng = random.Random(schema)
     blocks, exps = [], []
     for i in range(120):
@@ -58,13 +62,15 @@ def test_random_blocks(schema):
         blocks.append(blk)
         exps.append(exp)
     for align in (16, 8, 1):
-        g = check(*pack(blocks, align), schema, ctx=f"random schema={schema} align={align}")
+        g = check(*pack(blocks, align), schema, ctx=f"random schema={schema} align={align} {kernel}",
+                  flags=KERNELS[kernel])
         for b in (0, 7, 63, 119):
             kvs = kvs_of_block(g, b)
             assert [(kv.user_key, kv.trailer, kv.value, kv.flags) for kv in kvs] == [e[:4] for e in exps[b]]
 
 
-def test_large_key_regions_and_chunks():
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_large_key_regions_and_chunks(kernel):
     """Key columns past the LDS stage (global-read path), > 256 rows per block
     (chunked key placement) and chunks whose keys exceed the LDS key buffer."""
     rng = random.Random(77)
@@ -76,7 +82,7 @@ def test_large_key_regions_and_chunks():
         blocks.append((schema, build_block(schema, rows, 16)[0]))
     for schema in (SCHEMA_DEFAULT, SCHEMA_CRDB1):
         bl = [b for s, b in blocks if s == schema]
-        g = check(*pack(bl), schema, ctx=f"large schema={schema}")
+        g = check(*pack(bl), schema, ctx=f"large schema={schema} {kernel}", flags=KERNELS[kernel])
 
 
 def test_mixed_row_and_colblk_batch():
@@ -97,7 +103,8 @@ def test_mixed_row_and_colblk_batch():
     assert g["n_kv"] == rn + cn + 100
 
 
-def test_corrupt_and_fuzzed_colblk():
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_corrupt_and_fuzzed_colblk(kernel):
     rng = random.Random(11)
     rows = random_rows(rng, SCHEMA_CRDB1, 80)
     base, _ = build_block(SCHEMA_CRDB1, rows)
@@ -107,19 +114,22 @@ def test_corrupt_and_fuzzed_colblk():
         for _ in range(rng.randint(1, 3)):
             b[rng.randrange(len(b))] = rng.randrange(256)
         blocks.append(bytes(b))
-    g = check(*pack(blocks), SCHEMA_CRDB1, ctx="fuzz")
+    g = check(*pack(blocks), SCHEMA_CRDB1, ctx=f"fuzz {kernel}", flags=KERNELS[kernel])
     assert g["n_bad_blocks"] > 0
     # the wrong schema for the block is a header corruption
     g = check(*pack([base]), SCHEMA_DEFAULT, ctx="wrong schema")
     assert g["blk_status"][0] == N.PBL_CORRUPT_COLBLK_HEADER
 
 
-def test_colblk_overflow_retry():
-    from pebble_amd.batch import Capacity
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_colblk_overflow_retry(kernel):
+    from pebble_amd.batch import BlockBatch, Capacity, decode, size_batch
     buf, off, lens, n = gen_col_blocks(8, 32)
     o = oracle.decode_batch(buf, off, lens, SCHEMA_CRDB1)
-    g = gpu_decode(buf, off, lens, SCHEMA_CRDB1, cap=Capacity(kv=10, key=10, val=10, rst=10))
-    assert_same(g, o, "overflow retry")
+    g = gpu_decode(buf, off, lens, SCHEMA_CRDB1, cap=Capacity(kv=10, key=10, val=10, rst=10), flags=KERNELS[kernel])
+    assert_same(g, o, f"overflow retry {kernel}")
+    b = BlockBatch.from_host(buf, off, lens, "cuda", SCHEMA_CRDB1, KERNELS[kernel])
+    assert_same(decode(b, exact=True).to_host(), o, f"exact {kernel}")
 
 
 def test_new_data_block_iter():

@@ -35,7 +35,7 @@ def test_zipf_row(ri, vp):
 @pytest.mark.parametrize("seed", [7, 8, 9])
 @pytest.mark.parametrize("kernel", ["auto", "pipe"])
 def test_zipf_col(seed, kernel):
-    # auto: the batch carries PBL_BATCH_VARLEN -> one-block-per-workgroup kernel;
+    # auto: the batch carries PBL_BATCH_VARLEN -> the two-pass wave form (8 KiB stage);
     # pipe: the persistent pipeline forced on the same blocks (PBL_KERNEL_PIPE)
     buf, off, lens, n = gen_zipf_blocks(seed, 400, N.PBL_FMT_COL_DEFAULT)
     g = col_check(buf, off, lens, N.PBL_FMT_COL_DEFAULT, ctx="zipf col",
