@@ -250,7 +250,7 @@ def workload_info(a, nb, N):
     if a.workload == "col":
         kernel = ("colblk_decode_kernel" if a.kernel == "single" and not a.hide else
                   "colblk_pipe_kernel" if a.hide or a.kernel == "pipe" else
-                  "colblk_wave_size_kernel+colblk_bases_scan_kernel+colblk_wave_emit_kernel")
+                  "colblk_wave_size_kernel+bases_scan_kernel+colblk_wave_emit_kernel")
         return N.PBL_FMT_COL_CRDB1, kernel, (
             f"config3: {nb} x {a.block_size // 1024} KiB colblk blocks per GPU, cockroachkvs crdb1 schema "
             f"(KeyGenConfig alphabet 26, RoachKeyLen 12, PrefixLenShared 4, 1 key/prefix), 128 B values"
@@ -258,9 +258,9 @@ def workload_info(a, nb, N):
             + (f", Pebblev8 tiering columns (span ids 1..{a.tiering}) decoded to per-KV KVMeta" if a.tiering else ""))
     if a.workload == "zipf":
         fmt = N.PBL_FMT_ROW if a.zipf_format == "row" else N.PBL_FMT_COL_DEFAULT
-        kernel = (row_kernel if fmt == N.PBL_FMT_ROW
-                  else "colblk_decode_kernel" if a.kernel == "single" else "colblk_pipe_kernel" if a.kernel == "pipe"
-                  else "colblk_wave_size_kernel+colblk_bases_scan_kernel+colblk_wave_emit_kernel")
+        kernel = (("row_wave_size_kernel+bases_scan_kernel+row_wave_emit_kernel" if a.kernel != "pool" else row_kernel)
+                  if fmt == N.PBL_FMT_ROW else "colblk_decode_kernel" if a.kernel == "single" else "colblk_pipe_kernel" if a.kernel == "pipe"
+                  else "colblk_wave_size_kernel+bases_scan_kernel+colblk_wave_emit_kernel")
         return fmt, kernel, (f"config5: {nb} variable-length blocks per GPU targeting {a.block_size // 1024} KiB, "
                              + (f"row format, restart interval {a.restart_interval}" if fmt == N.PBL_FMT_ROW
                                 else "colblk DefaultKeySchema")

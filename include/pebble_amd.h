@@ -109,25 +109,30 @@ enum {
                                      NextWithMeta on the row iterator returns KVMeta{}).
                                      Keys and values decode identically either way.   */
 #define PBL_BATCH_VARLEN 0x100u   /* scheduling hint, no effect on results: block
-                                     lengths vary widely (e.g. Zipf value sizes), so a
-                                     colblk batch takes the one-block-per-workgroup
-                                     kernel, whose look-back does not convoy behind
-                                     long blocks.  Row batches ignore it: their
-                                     kernel picks a path per block.  The caller knows
-                                     the lengths on the host (block handles carry
-                                     them).                                        */
+                                     lengths vary widely (e.g. Zipf value sizes).
+                                     colblk batches read more of each block's
+                                     values from LDS; row batches take the
+                                     two-pass form (lane-per-block size walk, bases
+                                     scan, wave-per-block emit from LDS, no
+                                     look-back) unless HideObsoletePoints or value
+                                     prefixes need key bytes to size a block.  The
+                                     caller knows the lengths on the host (block
+                                     handles carry them).                          */
 #define PBL_KERNEL_SINGLE 0x200u  /* A/B measurement, no effect on results: colblk
                                      batches on the one-block-per-workgroup kernel
-                                     (row batches ignore it)                       */
+                                     instead of the two-pass wave form (row
+                                     batches ignore it)                            */
 #define PBL_KERNEL_PIPE 0x400u    /* A/B measurement, no effect on results: colblk
-                                     batches on the pipeline even with
-                                     PBL_BATCH_VARLEN (row batches ignore it)      */
+                                     batches on the persistent pipeline instead of
+                                     the two-pass wave form (row batches ignore
+                                     it)                                           */
 /* 0x800u, 0x1000u, 0x2000u, 0x8000u: retired A/B kernels (one-wave-per-block
    flat, run-major, HBM-walking and block-resident row kernels; removed, the
    bits are ignored)                                                            */
-#define PBL_KERNEL_POOL 0x4000u   /* row batches on the staging-pool kernel
-                                     (rowblk_pool.hip.h): the default; the bit is
-                                     accepted for older callers                    */
+#define PBL_KERNEL_POOL 0x4000u   /* A/B measurement, no effect on results: row
+                                     batches on the staging-pool kernel
+                                     (rowblk_pool.hip.h, the default without
+                                     PBL_BATCH_VARLEN) even with PBL_BATCH_VARLEN  */
 
 /* per-KV flag byte (kv_flags[]) */
 #define PBL_KV_RESTART 0x01u       /* entry offset is a restart point            */

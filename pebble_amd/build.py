@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libpebble_amd.so")
 SOURCES = ["rowblk_decode.hip", "colblk_decode.hip", "transforms.hip", "physical.hip", "zstd.hip", "sstable.hip", "rowblk_writer.cpp", "colblk_writer.cpp", "zipf_gen.cpp", "data_iter.cpp"]
-HEADERS = ["common.hip.h", "rowblk_general.hip.h", "rowblk_big.hip.h", "rowblk_pool.hip.h", "colblk_pipe.hip.h", "colblk_block.hip.h", "colblk_wave.hip.h", "zstd_dec.hip.h", "snappy_dec.hip.h", "minlz_dec.hip.h", os.path.join("..", "..", "include", "pebble_amd.h")]
+HEADERS = ["common.hip.h", "rowblk_general.hip.h", "rowblk_big.hip.h", "rowblk_pool.hip.h", "rowblk_wave.hip.h", "colblk_pipe.hip.h", "colblk_block.hip.h", "colblk_wave.hip.h", "zstd_dec.hip.h", "snappy_dec.hip.h", "minlz_dec.hip.h", os.path.join("..", "..", "include", "pebble_amd.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-pthread"]
 

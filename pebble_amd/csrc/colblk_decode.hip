@@ -55,7 +55,7 @@ extern "C" int pbl_decode_batch_colblk(const pbl_block_batch* batch, pbl_decode_
     const uint32_t nt = (batch->n_blocks + cw::kScanTile - 1) / cw::kScanTile;
     const uint32_t* no_ids = nullptr;
     hipLaunchKernelGGL((cw::colblk_wave_size_kernel<false, false>), dim3(g_s), dim3(pbl::kWave), 0, st, a, no_ids);
-    hipLaunchKernelGGL(cw::colblk_bases_scan_kernel, dim3(std::min<uint32_t>(nt, uint32_t(cus) * 2)), dim3(pbl::kTPB),
+    hipLaunchKernelGGL(cw::bases_scan_kernel<false>, dim3(std::min<uint32_t>(nt, uint32_t(cus) * 2)), dim3(pbl::kTPB),
                        0, st, a);
     // variable-length blocks (config 5: one long values range each) read more
     // of their values from a larger stage

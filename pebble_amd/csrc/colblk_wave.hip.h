@@ -15,7 +15,7 @@
 //           row the key length and the bounds checks; the aggregate and
 //           status go to blk_{kv,key,val}_base[b] / blk_status[b].  Nothing
 //           waits.
-//   scan    colblk_bases_scan_kernel: the exclusive scan of those counts in
+//   scan    bases_scan_kernel<false>: the exclusive scan of those counts in
 //           place (tiles of 1024 blocks, decoupled look-back across tiles),
 //           totals at [n].
 //   emit    colblk_wave_emit_kernel: per block, its final bases; the first
@@ -250,7 +250,7 @@ __device__ __forceinline__ void cw_emit(L_& L, const Args& A, uint32_t b, uint32
 // kList: the colblk blocks of a mixed batch (the id list past its row ids;
 // each aggregate is PUBLISHED to the look-back state); else every block of a
 // colblk batch (aggregate and status to blk_{kv,key,val}_base[b] / blk_status[b]
-// for colblk_bases_scan_kernel).  kHide: the visible rows, as
+// for bases_scan_kernel).  kHide: the visible rows, as
 // col_emit_rows_hide places them.  Resident waves loop over the blocks.
 struct SLds {
   uint4 head4[(kSizeStg + 48) / 16];
@@ -368,22 +368,28 @@ colblk_wave_emit_kernel(Args A, const uint32_t* ids) {
   CSTAMP(A, b, 7);
 }
 
-#ifndef PBL_CW_SIZE_ONLY  // (rowblk_decode.hip needs the templates only)
-// Exclusive scan, in place, of the per-block counts the size pass left in
+// Exclusive scan, in place, of the per-block counts a size pass left in
 // blk_{kv,key,val}_base[0, n): tiles of 1024 blocks per 256-thread workgroup
 // in ticket order, each tile's aggregate published and its prefix resolved by
-// the decoupled look-back (tf_scan_kernel's form); [n] gets the batch totals,
-// blk_rst_base (colblk: no restarts) zeros.
+// the decoupled look-back (tf_scan_kernel's form); [n] gets the batch totals.
+// kRst (row batches, rowblk_wave.hip.h): the restart counts at
+// ws_rcnt_offset are scanned the same way (and copied to blk_rst_base when
+// given); else (colblk: no restarts) blk_rst_base gets zeros.  (Each
+// instantiation is launched from one translation unit only.)
 constexpr uint32_t kScanTile = 1024;
-__global__ void __launch_bounds__(kTPB) colblk_bases_scan_kernel(Args A) {
+template <bool kRst>
+__global__ void __launch_bounds__(kTPB) bases_scan_kernel(Args A) {
+  constexpr int kC = kRst ? 4 : 3;
   __shared__ uint32_t s_tile;
-  __shared__ uint64_t s_wsum[kTPB / kWave][3];
-  __shared__ uint64_t s_excl[3];
+  __shared__ uint64_t s_wsum[kTPB / kWave][kC];
+  __shared__ uint64_t s_excl[kC];
   const pbl_decode_out& O = A.out;
   uint8_t* ws = reinterpret_cast<uint8_t*>(O.workspace);
   uint32_t* hdr = reinterpret_cast<uint32_t*>(ws);
   uint64_t* lb_state = reinterpret_cast<uint64_t*>(ws + kWsHeader);
   const uint32_t nb = A.in.n_blocks, nt = (nb + kScanTile - 1) / kScanTile, t = threadIdx.x;
+  uint64_t* const arr[4] = {O.blk_kv_base, O.blk_key_base, O.blk_val_base,
+                            reinterpret_cast<uint64_t*>(ws + ws_rcnt_offset(nb))};
   for (;;) {
     if (t == 0) s_tile = g_atomic_add(hdr + 1, 1u);
     __syncthreads();
@@ -391,26 +397,30 @@ __global__ void __launch_bounds__(kTPB) colblk_bases_scan_kernel(Args A) {
     __syncthreads();  // (s_tile is rewritten next iteration)
     if (tile >= nt) return;
     const uint32_t b0 = tile * kScanTile + 4 * t;
-    uint64_t c[4][3], s3[3] = {0, 0, 0};
+    uint64_t c[4][kC], s3[kC];
+#pragma unroll
+    for (int q = 0; q < kC; q++) s3[q] = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const bool in = b0 + k < nb;
-      c[k][0] = in ? to_glb(O.blk_kv_base)[b0 + k] : 0;
-      c[k][1] = in ? to_glb(O.blk_key_base)[b0 + k] : 0;
-      c[k][2] = in ? to_glb(O.blk_val_base)[b0 + k] : 0;
 #pragma unroll
-      for (int q = 0; q < 3; q++) s3[q] += c[k][q];
+      for (int q = 0; q < kC; q++) {
+        c[k][q] = in ? to_glb(arr[q])[b0 + k] : 0;
+        s3[q] += c[k][q];
+      }
     }
-    uint64_t in3[3];
+    uint64_t in3[kC];
 #pragma unroll
-    for (int q = 0; q < 3; q++) in3[q] = wave_incl_scan(s3[q]);
+    for (int q = 0; q < kC; q++) in3[q] = wave_incl_scan(s3[q]);
     if (lane_id() == kWave - 1)
-      for (int q = 0; q < 3; q++) s_wsum[wave_id()][q] = in3[q];
+      for (int q = 0; q < kC; q++) s_wsum[wave_id()][q] = in3[q];
     __syncthreads();
-    uint64_t before[3] = {0, 0, 0}, agg[kNumComp] = {0, 0, 0, 0};
+    uint64_t before[kC], agg[kNumComp] = {0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < kC; q++) before[q] = 0;
     for (int w = 0; w < kTPB / kWave; w++)
 #pragma unroll
-      for (int q = 0; q < 3; q++) {
+      for (int q = 0; q < kC; q++) {
         if (w < wave_id()) before[q] += s_wsum[w][q];
         agg[q] += s_wsum[w][q];
       }
@@ -419,33 +429,30 @@ __global__ void __launch_bounds__(kTPB) colblk_bases_scan_kernel(Args A) {
       lb_publish(lb_state, nt, tile, agg);
       lb_resolve(lb_state, nt, tile, agg, excl, &O.totals->status_mask);
       if (lane_id() == 0)
-        for (int q = 0; q < 3; q++) s_excl[q] = excl[q];
+        for (int q = 0; q < kC; q++) s_excl[q] = excl[q];
     }
     __syncthreads();
-    uint64_t e[3];
+    uint64_t e[kC];
 #pragma unroll
-    for (int q = 0; q < 3; q++) e[q] = s_excl[q] + before[q] + in3[q] - s3[q];
+    for (int q = 0; q < kC; q++) e[q] = s_excl[q] + before[q] + in3[q] - s3[q];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const uint32_t b = b0 + k;
       if (b < nb) {
-        to_glb(O.blk_kv_base)[b] = e[0];
-        to_glb(O.blk_key_base)[b] = e[1];
-        to_glb(O.blk_val_base)[b] = e[2];
-        if (O.blk_rst_base) to_glb(O.blk_rst_base)[b] = 0;
 #pragma unroll
-        for (int q = 0; q < 3; q++) e[q] += c[k][q];
+        for (int q = 0; q < kC; q++) to_glb(arr[q])[b] = e[q];
+        if (O.blk_rst_base) to_glb(O.blk_rst_base)[b] = kRst ? e[kC - 1] : 0;
+#pragma unroll
+        for (int q = 0; q < kC; q++) e[q] += c[k][q];
       }
     }
     if (tile == nt - 1 && t == 0) {
-      to_glb(O.blk_kv_base)[nb] = s_excl[0] + agg[0];
-      to_glb(O.blk_key_base)[nb] = s_excl[1] + agg[1];
-      to_glb(O.blk_val_base)[nb] = s_excl[2] + agg[2];
-      if (O.blk_rst_base) to_glb(O.blk_rst_base)[nb] = 0;
+#pragma unroll
+      for (int q = 0; q < kC; q++) to_glb(arr[q])[nb] = s_excl[q] + agg[q];
+      if (O.blk_rst_base) to_glb(O.blk_rst_base)[nb] = kRst ? s_excl[kC - 1] + agg[kC - 1] : 0;
     }
   }
 }
-#endif
 
 }  // namespace cwave
 }  // namespace col

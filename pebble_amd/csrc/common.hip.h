@@ -73,6 +73,13 @@ constexpr int kPfBits[kNumComp] = {31, 30, 37, 24};
 __host__ __device__ inline uint64_t ws_bytes(uint32_t n_blocks) {
   return kWsHeader + uint64_t(2 + 2 * kNumComp) * n_blocks * 8ull;
 }
+// Two-pass forms (a size pass, the bases scan, then the outputs): per-block
+// restart counts, scanned in place into restart bases ([n_blocks] = total).
+// The last n_blocks + 1 words of the look-back area, which the scan's own
+// per-tile look-back (n_blocks / 1024 records) never reaches.
+__host__ __device__ inline uint64_t ws_rcnt_offset(uint32_t n_blocks) {
+  return ws_bytes(n_blocks) - 8ull * (n_blocks + 1);
+}
 #ifdef PBL_STAMPS
 constexpr uint64_t kStampWords = 16;  // diagnostic build: per-block phase stamps
 #else
@@ -91,7 +98,15 @@ __host__ __device__ inline uint64_t ws_redo_offset(uint32_t n_blocks) {
   return ws_ids_offset(n_blocks) + 4ull * n_blocks + 4ull * (n_blocks / kSplitChunk + 1) + 8;
 }
 __host__ __device__ inline uint64_t ws_pend_offset(uint32_t n_blocks) { return ws_redo_offset(n_blocks) + 4ull * n_blocks; }
-__host__ __device__ inline uint64_t ws_alloc_bytes(uint32_t n_blocks) { return ws_pend_offset(n_blocks) + 4ull * n_blocks; }
+// Then the entry offsets of the two-pass row form (rowblk_wave.hip.h): the
+// first kEntRec entries' block offsets per block, u16 (blocks <= 32 KiB).
+constexpr uint32_t kEntRec = 64;
+__host__ __device__ inline uint64_t ws_ent_offset(uint32_t n_blocks) {
+  return (ws_pend_offset(n_blocks) + 4ull * n_blocks + 15) & ~uint64_t(15);
+}
+__host__ __device__ inline uint64_t ws_alloc_bytes(uint32_t n_blocks) {
+  return ws_ent_offset(n_blocks) + 2ull * kEntRec * n_blocks;
+}
 
 
 // Address-space-typed pointers.  A generic pointer compiles to FLAT

@@ -5,6 +5,8 @@
 // Kernels:
 //   rowblk_pool_kernel   (rowblk_pool.hip.h) the staging-pool kernel
 //   big_block_*_kernel   (rowblk_big.hip.h) blocks past the 32 KiB LDS stage
+//   row_wave_*_kernel    (rowblk_wave.hip.h) PBL_BATCH_VARLEN batches in two
+//                        passes (sizes, bases_scan_kernel<true>, outputs)
 //   mixed_*              row + colblk batches (config 4): the ids split by
 //                        format, the colblk sizes, the row kernel over the row
 //                        ids, the colblk pipeline over the colblk ids
@@ -150,13 +152,13 @@ struct GlbRd {  // unstaged block in global memory
 
 #include "rowblk_big.hip.h"
 #include "rowblk_pool.hip.h"
+#include "rowblk_wave.hip.h"
 
 }  // namespace row
 }  // namespace pbl
 
 #define PBL_COL_PIPE_BODY_ONLY
 #include "colblk_pipe.hip.h"
-#define PBL_CW_SIZE_ONLY
 #include "colblk_wave.hip.h"
 
 namespace pbl {
@@ -447,8 +449,31 @@ int launch_mixed(const pbl_block_batch* batch, const pbl::Args& a, hipStream_t s
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }
 
-// A single-format row batch: the staging-pool kernel.
-int launch_row(const pbl::Args& a, hipStream_t st, bool values) { return launch_row_pool(a, st, values); }
+// Variable-length row batches: the two-pass form (rowblk_wave.hip.h).
+int launch_row_wave(const pbl::Args& a, hipStream_t st) {
+  const uint32_t nb = a.in.n_blocks;
+  int dev = 0, cus = 256;
+  if (hipStreamGetDevice(st, &dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return PBL_DEVICE_ERROR;
+  namespace cw = pbl::col::cwave;
+  const uint32_t nt = (nb + cw::kScanTile - 1) / cw::kScanTile;
+  hipLaunchKernelGGL(pbl::row::rwave::row_wave_size_kernel, dim3((nb + pbl::kWave - 1) / pbl::kWave),
+                     dim3(pbl::kWave), 0, st, a);
+  hipLaunchKernelGGL(cw::bases_scan_kernel<true>, dim3(std::min<uint32_t>(nt, uint32_t(cus) * 2)), dim3(pbl::kTPB), 0,
+                     st, a);
+  hipLaunchKernelGGL(pbl::row::rwave::row_wave_emit_kernel, dim3(nb), dim3(pbl::kWave), 0, st, a);
+  return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
+}
+
+// A single-format row batch: the staging-pool kernel, or with
+// PBL_BATCH_VARLEN the two-pass form (PBL_KERNEL_POOL forces the pool).
+int launch_row(const pbl::Args& a, hipStream_t st, bool values) {
+  const uint32_t f = a.in.flags;
+  if ((f & PBL_BATCH_VARLEN) && !(f & PBL_KERNEL_POOL) && pbl::row::rwave::sizes_without_keys(f))
+    return launch_row_wave(a, st);
+  return launch_row_pool(a, st, values);
+}
 }  // namespace
 
 extern "C" {

@@ -1,0 +1,385 @@
+// rowblk_wave.hip.h — row batches of variable-length blocks (PBL_BATCH_VARLEN:
+// config 5's Zipf-sized KVs) in two passes, no look-back:
+//
+//   sizes   row_wave_size_kernel: LANE per block.  Each lane walks its block's
+//           entry headers in global memory (one 16-B window per entry, the
+//           three varints from registers) and leaves {status, KVs, user-key
+//           bytes, value bytes} in blk_status / blk_{kv,key,val}_base[b] and
+//           the restart count at ws_rcnt_offset.  A Zipf block holds ~8-13
+//           entries, so a wave sizes 64 blocks in ~13 dependent round trips
+//           and touches only the header lines (about 1/10 of the bytes).
+//   scan    bases_scan_kernel<true> (colblk_wave.hip.h): the four components'
+//           exclusive scan in place, totals at [n].
+//   emit    row_wave_emit_kernel: one wave per block (four per CU), its bases
+//           final.  The block by LDS-DMA into the wave's stage, the pool
+//           kernel's lane-per-run walk and metadata pass into the wave's slot,
+//           then every output from LDS: keys lane per KV, the values (97 % of
+//           a Zipf block's bytes) LDS -> HBM in 16-B chunks, so a block is read
+//           once.  Blocks off that form take the general walk (below).
+//
+// Against the staging-pool kernel (rowblk_pool.hip.h) on config 5: no look-back
+// (16 K of its 95 K cycles per block), no second read of the values from
+// L2 / HBM after the stage is released (1.56x traffic), no per-value round
+// trips of the global->global copies.  Fixed-size batches (config 2: 271 KVs
+// per block) stay on the pool kernel: there the lane walk would be 271 round
+// trips deep and the wave-serial emit 271 entries long.
+//
+// Results are the general walk's: the size walk applies slow_walk_t's checks
+// in slow_walk_t's order (rowblk_general.hip.h; Iter.Init rowblk_iter.go:
+// 241-276, readEntry :333-416, the key-buffer limit of the general path); the
+// emit's lane-parallel form is taken only where its walk agrees with those
+// sizes, else the emit IS slow_walk_t.  (The wave-serial walk alone measured
+// 2.87 ms on config 5 RI 16: ~6.9 K cycles per entry of dependent LDS steps.)  Flags that need a key's bytes
+// to size it (HideObsoletePoints, value prefixes, on internal keys) take the
+// pool kernel.
+#pragma once
+
+namespace rwave {
+
+#ifndef PBL_RW_VALU
+#define PBL_RW_VALU 4  // value granules per lane in flight, LDS -> HBM
+#endif
+
+// the general walk's key limit with the whole stage as its key buffer
+constexpr uint64_t kKeyCapMax = uint64_t(kLdsBlkBytes) - kKeyBufSlack;
+
+// Whether a batch's flags let the size pass count without key bytes.
+__host__ __device__ inline bool sizes_without_keys(uint32_t flags) {
+  return (flags & PBL_ROW_RAW_KEYS) || !(flags & (PBL_ROW_HIDE_OBSOLETE | PBL_ROW_VALUE_PREFIX));
+}
+
+// ---- the size pass: lane per block -------------------------------------------
+__global__ void __launch_bounds__(kWave) row_wave_size_kernel(Args A) {
+  const uint32_t nb = A.in.n_blocks, flags = A.in.flags;
+  const pbl_decode_out& O = A.out;
+  const bool raw = (flags & PBL_ROW_RAW_KEYS) != 0;
+  const gptr<uint64_t> rcnt =
+      to_glb(reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(O.workspace) + ws_rcnt_offset(nb)));
+  const gptr<uint16_t> rec =
+      to_glb(reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(O.workspace) + ws_ent_offset(nb)));
+  for (uint64_t b = uint64_t(blockIdx.x) * kWave + lane_id(); b < nb; b += uint64_t(gridDim.x) * kWave) {
+    const uint32_t blen = to_glb(A.in.block_len)[b];
+    const uint8_t* g = A.in.blocks + to_glb(A.in.block_off)[b];
+    uint32_t roff, nres;
+    uint32_t status = rowc::init_checks(GlbRd{g}, blen, flags, &roff, &nres);
+    uint64_t nkv = 0, kb = 0, vb = 0;
+    if (status == PBL_OK) {
+      const SlowGlb S{to_glb(g), blen};
+      uint64_t off = 0, full = 0;
+      // slow_walk_t's loop, its checks in its order, without the key bytes
+      while (off < roff) {
+        const uint4 hw = S.ld16(int64_t(off));
+        const uint32_t hn = uint32_t(min<uint64_t>(15, uint64_t(blen) - off));
+        uint32_t shared, unshared, vlen;
+        const uint32_t a = w_varint(hw, 0, hn, &shared);
+        const uint32_t bb = a ? w_varint(hw, a, hn, &unshared) : 0;
+        const uint32_t c = bb ? w_varint(hw, a + bb, hn, &vlen) : 0;
+        if (!c) { status = PBL_CORRUPT_BOUNDS; break; }
+        const uint64_t kp = off + a + bb + c;
+        if (blen - kp < unshared) { status = PBL_CORRUPT_BOUNDS; break; }
+        const uint64_t vp = kp + unshared;
+        if (blen - vp < vlen) { status = PBL_CORRUPT_BOUNDS; break; }
+        if (shared > full) { status = PBL_CORRUPT_BOUNDS; break; }
+        const uint64_t klen = uint64_t(shared) + unshared;
+        if (klen > kKeyCapMax) { status = PBL_UNSUPPORTED; break; }
+        full = klen;
+        if (nkv < kEntRec && blen <= kMaxFastLen) rec[b * kEntRec + nkv] = uint16_t(off);  // (for the emit)
+        nkv++;
+        kb += raw ? klen : (klen >= 8 ? klen - 8 : 0);
+        vb += vlen;
+        off = vp + vlen;
+      }
+      if (status == PBL_OK && (kb >> 32 || vb >> 32)) status = PBL_UNSUPPORTED;
+    }
+    const bool ok = status == PBL_OK;
+    to_glb(O.blk_kv_base)[b] = ok ? nkv : 0;
+    to_glb(O.blk_key_base)[b] = ok ? kb : 0;
+    to_glb(O.blk_val_base)[b] = ok ? vb : 0;
+    rcnt[b] = ok ? nres : 0;
+    to_glb(O.blk_status)[b] = status;
+  }
+}
+
+// ---- the emit pass: wave per block -------------------------------------------
+// The block staged, then the staging-pool kernel's lane-per-run walk and its
+// metadata pass (rowblk_pool.hip.h: run_walk / count_span, park_meta /
+// span_meta into the wave's slot), then the outputs: keys and per-KV arrays
+// lane per KV (key_load / key_store with the stage as the key source), values
+// from the stage.  A block off that form (not walkable per run, more entries
+// than a slot holds, an empty or failing block, sizes that disagree with the
+// size pass) takes the wave-serial general walk on the stage with the slot as
+// its key buffer; a key past the slot, or a block past the stage, walks global
+// memory with the stage as the key buffer (as block_slow does).
+#ifndef PBL_RW_FAST
+#define PBL_RW_FAST 1  // 0: every block on the general walk (A/B)
+#endif
+#ifndef PBL_RW_PAR
+#define PBL_RW_PAR 1  // 0: every block through the serial per-run walk (A/B)
+#endif
+struct ELds {
+  pool::Stage st;
+  pool::Slot<false> sl;
+};
+static_assert(4 * sizeof(ELds) <= 163840, "four emit waves per CU");
+
+// Walk and describe the staged block into slot W; false if the block is off
+// the lane-parallel form.
+__device__ __forceinline__ bool front_fast(const View& V, uint32_t blen, uint32_t flags, pool::Slot<false>& W,
+                                           const uint64_t agg[kNumComp], uint32_t* roff_o) {
+  using namespace pool;
+  const int l = lane_id();
+  constexpr uint32_t kKv = uint32_t(Slot<false>::kKv);
+  const bool vprefix = (flags & PBL_ROW_VALUE_PREFIX) && !(flags & PBL_ROW_RAW_KEYS);
+  uint32_t roff, nres;
+  if (rowc::init_checks(LdsRd{V}, blen, flags, &roff, &nres) != PBL_OK || roff == 0 || nres > kKv) return false;
+  // lane l owns runs [r0, r1)
+  const uint32_t R = (nres + kWave - 1) / kWave;
+  const uint32_t r0 = min(uint32_t(l) * R, nres), r1 = min(r0 + R, nres);
+  PAcc acc{0, 0, 0, 0};
+  bool ok = true, bad = false, vbad = false, over = false;
+  PRun RB;
+  RB.n = 0;
+  RB.pos = RB.e0 = RB.prev_kl = RB.prev_kind = RB.rw = 0;
+  const bool single = R == 1;
+  if (single) {
+    if (r0 < nres) run_walk<false>(V, r0, nres, roff, flags, vprefix, RB, acc, ok, bad, vbad, over);
+    if (over && ok)
+      count_span<false>(V, RB.pos, RB.e0, RB.n, RB.prev_kl, RB.prev_kind, flags, vprefix, acc, ok, bad, vbad);
+  } else {
+    for (uint32_t r = r0; r < r1 && ok; r++) {
+      uint32_t rw, e0;
+      if (!run_bounds(V, r, nres, roff, &rw, &e0)) ok = false;
+      else count_span<false>(V, rw & kRestartMask, e0, 0, 0, 0, flags, vprefix, acc, ok, bad, vbad);
+    }
+  }
+  const uint32_t ic = dpp_incl_scan(acc.cnt), ik = dpp_incl_scan(acc.kb), iv = dpp_incl_scan(acc.vb);
+  const uint32_t nkv = last_lane(ic), tkb = last_lane(ik), tvb = last_lane(iv);
+  if (__ballot(bad || vbad || !ok) || nkv > kKv) return false;
+  if (nkv != agg[0] || tkb != agg[1] || tvb != agg[2] || nres != agg[3]) return false;
+  MState M{ic - acc.cnt, ic - acc.cnt, iv - acc.vb, 0, 0, 0};
+  if (single) {
+    if (r0 < nres) {
+      park_meta<false>(W, V, RB, flags, M);
+      if (over) span_meta<false>(W, V, RB.pos, RB.e0, RB.rw, RB.n, RB.prev_kl, RB.prev_kind, flags, vprefix, M);
+    }
+  } else {
+    for (uint32_t r = r0; r < r1; r++) {
+      uint32_t rw, e0;
+      run_bounds(V, r, nres, roff, &rw, &e0);
+      M.prev_sh = M.pp = M.ppsh = 0;
+      span_meta<false>(W, V, rw & kRestartMask, e0, rw, 0, 0, 0, flags, vprefix, M);
+    }
+  }
+  if (l < 5) W.vp[nkv + l] = tvb;
+  *roff_o = roff;
+  return true;
+}
+
+// The same description without the serial walk, for a block of at most
+// kEntRec KVs: lane i takes entry i at the offset the size pass recorded
+// (pos), decodes its header from the stage, and the wave derives the rest --
+// value output offsets by a scan, the prefix parent (nearest earlier entry
+// with a smaller shared length, entry_meta's chain) by one pass over the
+// lanes, restart flags by a binary search of the restart table.  That search
+// is slow_walk_t's restart pointer only for a strictly increasing table, so
+// any other table (and any entry off the fast form's limits) returns false.
+__device__ __forceinline__ bool front_par(const View& V, uint32_t blen, uint32_t flags, pool::Slot<false>& W,
+                                          const uint64_t agg[kNumComp], uint32_t pos, uint32_t* roff_o) {
+  using namespace pool;
+  const int l = lane_id();
+  const uint32_t nkv = uint32_t(agg[0]), nres = uint32_t(agg[3]);
+  const uint32_t roff = blen - 4u * (1u + nres);  // (the size pass checked the table)
+  const bool raw = (flags & PBL_ROW_RAW_KEYS) != 0;
+  const bool me = uint32_t(l) < nkv;
+  uint32_t sh = 0, un = 0, vl = 0, h = 0;
+  bool ok = true;
+  if (me) {
+    ok = rowc::hdr2(V.ld8(pos), &sh, &un, &vl, &h) && sh + un <= kMaxKl && h <= 15;
+    const uint32_t nxt = __shfl(pos, l + 1 < kWave ? l + 1 : l, kWave);
+    ok = ok && pos + h + un + vl == (uint32_t(l) + 1 < nkv ? nxt : roff);
+  }
+  // the restart table strictly increasing (masked words)
+  bool inc = true;
+  for (uint32_t r = l; r + 1 < nres; r += kWave)
+    inc = inc && (V.le32(roff + 4 * r) & kRestartMask) < (V.le32(roff + 4 * r + 4) & kRestartMask);
+  if (__ballot(!ok || !inc)) return false;
+  const uint32_t kl = sh + un;
+  // prefix parent: the last lane t < l with sh_t < sh (itself when sh == 0)
+  uint32_t par = uint32_t(l);
+  for (uint32_t t = 0; t + 1 < nkv; t++) {
+    const uint32_t sht = __builtin_amdgcn_readlane(sh, t);
+    if (sh != 0 && t < uint32_t(l) && sht < sh) par = t;
+  }
+  // restart flags: offset pos in the table
+  uint32_t fl = 0;
+  if (me) {
+    uint32_t lo = 0, hi = nres;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if ((V.le32(roff + 4 * mid) & kRestartMask) < pos) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo < nres) {
+      const uint32_t rw = V.le32(roff + 4 * lo);
+      if ((rw & kRestartMask) == pos) fl = PBL_KV_RESTART | ((rw >> 31) ? PBL_KV_RESTART_SAMEPFX : 0u);
+    }
+    if (!raw && kl < 8) fl |= PBL_KV_INVALID_KEY;
+  }
+  const uint32_t incl = dpp_incl_scan(me ? vl : 0u);
+  if (me) {
+    W.m0[l] = m_pack(pos + h, sh, kl, par, h, fl);
+    W.vp[l] = (incl - vl) | ((pos + h + un) << 16);
+  }
+  if (l < 5) W.vp[nkv + l] = uint32_t(agg[2]);
+  *roff_o = roff;
+  return true;
+}
+
+// Values of the slot's KVs from the stage: values of at most 128 B 8 lanes per
+// KV (8 KVs per pass), longer ones by the whole wave, four 16-B chunks per lane
+// in flight; a value's last chunk ENDS at its end (overlapping the one before),
+// so every store is a whole unaligned 16-B store of its own value's bytes.
+__device__ __forceinline__ void values_from_stage(const uint32_t* vp, const View& V, uint32_t nkv,
+                                                  gptr<uint8_t> vbytes) {
+  using pool::st_out;
+  const int l = lane_id();
+  const uint32_t c = uint32_t(l) & 7u;
+  for (uint32_t j0 = 0; j0 < nkv; j0 += 8) {
+    const uint32_t j = j0 + (uint32_t(l) >> 3);
+    const uint32_t a = j < nkv ? vp[j] : 0u, z = j < nkv ? vp[j + 1] : 0u;
+    const uint32_t vo = a & 0xffffu, vl = (z & 0xffffu) - vo, vs = a >> 16;
+    if (j >= nkv || vl > 128) continue;
+    if (vl >= 16) {
+      if (16 * c < vl) {
+        const uint32_t q = 16 * c < vl - 16 ? 16 * c : vl - 16;
+        const uint4 w = V.ld16(int32_t(vs + q));
+        st_out((gptr<pool::u32x4_ug>)(vbytes + vo + q), pool::u32x4_ug{w.x, w.y, w.z, w.w});
+      }
+    } else {
+      for (uint32_t o = c; o < vl; o += 8) vbytes[vo + o] = uint8_t(V.byte(vs + o));
+    }
+  }
+  for (uint32_t j0 = 0; j0 < nkv; j0 += kWave) {
+    const uint32_t j = j0 + uint32_t(l);
+    const uint32_t a = j < nkv ? vp[j] : 0u, z = j < nkv ? vp[j + 1] : 0u;
+    const uint32_t len = (z & 0xffffu) - (a & 0xffffu);
+    for (uint64_t lm = __ballot(j < nkv && len > 128); lm; lm &= lm - 1) {
+      const int sl = __builtin_ctzll(lm);
+      const uint32_t vs = __shfl(a >> 16, sl, kWave), vl = __shfl(len, sl, kWave), vo = __shfl(a & 0xffffu, sl, kWave);
+      for (uint32_t o0 = 16u * l; o0 < vl; o0 += 64u * kWave) {
+        uint4 y[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t o = o0 + 16u * kWave * k, q = o < vl - 16 ? o : vl - 16;
+          y[k] = V.ld16(int32_t(vs + (o < vl ? q : 0u)));
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t o = o0 + 16u * kWave * k, q = o < vl - 16 ? o : vl - 16;
+          if (o < vl) st_out((gptr<pool::u32x4_ug>)(vbytes + vo + q), pool::u32x4_ug{y[k].x, y[k].y, y[k].z, y[k].w});
+        }
+      }
+    }
+  }
+}
+
+// The outputs of a block front_fast described, at bases excl.
+__device__ __forceinline__ void emit_fast(const Args& A, uint32_t b, const View& V, const pool::Slot<false>& W,
+                                          uint32_t roff, const uint64_t excl[kNumComp], const uint64_t agg[kNumComp]) {
+  const int l = lane_id();
+  const pbl_decode_out& O = A.out;
+  const bool raw = (A.in.flags & PBL_ROW_RAW_KEYS) != 0;
+  const uint32_t nkv = uint32_t(agg[0]), nres = uint32_t(agg[3]);
+  if (O.restarts)
+    for (uint32_t r = l; r < nres; r += kWave) to_glb(O.restarts)[excl[3] + r] = V.le32(roff + 4 * r);
+  uint32_t kcar = 0;
+  for (uint32_t j0 = 0; j0 <= nkv; j0 += kWave) {
+    pool::KBatch K;
+    pool::key_load<false, View>(W, V, raw, j0, nkv, K);
+    pool::key_store<false, View>(W, V, A, b, j0, nkv, excl[0], excl[1], K, kcar);
+  }
+  values_from_stage(W.vp, V, nkv, to_glb(O.val_bytes) + excl[2]);
+}
+
+__global__ void __launch_bounds__(kWave) row_wave_emit_kernel(Args A) {
+  __shared__ ELds L;
+  const int l = lane_id();
+  const uint32_t nb = A.in.n_blocks, b = blockIdx.x, flags = A.in.flags;
+  const pbl_decode_out& O = A.out;
+  PSTAMP(A, b, 0, l == 0);
+  const gptr<const uint64_t> rcnt = to_glb(
+      reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(O.workspace) + ws_rcnt_offset(nb)));
+  uint64_t excl[kNumComp], agg[kNumComp];
+  excl[0] = to_glb(O.blk_kv_base)[b];
+  excl[1] = to_glb(O.blk_key_base)[b];
+  excl[2] = to_glb(O.blk_val_base)[b];
+  excl[3] = rcnt[b];
+  agg[0] = to_glb(O.blk_kv_base)[b + 1] - excl[0];
+  agg[1] = to_glb(O.blk_key_base)[b + 1] - excl[1];
+  agg[2] = to_glb(O.blk_val_base)[b + 1] - excl[2];
+  agg[3] = rcnt[b + 1] - excl[3];
+  uint32_t status = to_glb(O.blk_status)[b];
+  if (status == PBL_OK && overflows(O, excl, agg)) status = PBL_OVERFLOW;
+  const uint64_t boff = to_glb(A.in.block_off)[b];
+  const uint32_t blen = to_glb(A.in.block_len)[b];
+  const bool staged = status == PBL_OK && blen <= kMaxFastLen;
+  const bool par = staged && agg[0] > 0 && agg[0] <= kEntRec;
+  uint32_t pos = 0;
+  if (staged) {  // (in flight under the metadata stores)
+    pool::stage_dma(L.st, A.in.blocks, boff, blen);
+    if (par && uint32_t(l) < agg[0])
+      pos = to_glb(reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(O.workspace) +
+                                                     ws_ent_offset(nb)))[uint64_t(b) * kEntRec + l];
+  }
+  if (l == 0) {
+    if (status != PBL_OK && O.key_off && excl[0] + b < O.kv_cap + nb) {
+      to_glb(O.key_off)[excl[0] + b] = 0;
+      to_glb(O.val_off)[excl[0] + b] = 0;
+    }
+    write_block_meta(O, b, nb, status, excl, agg, false);
+  }
+  PSTAMP(A, b, 1, l == 0);
+  if (status != PBL_OK) return;
+  const uint8_t* g = A.in.blocks + boff;
+  const uint64_t seq = A.in.synthetic_seq_num;
+  SlowState ss;
+  ss.status = PBL_UNSUPPORTED;
+  if (staged) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+    PSTAMP(A, b, 2, l == 0);
+    const View V = lds_view(L.st.x, uint32_t(kPad + (boff & 15)));
+    uint32_t roff = 0;
+    if (PBL_RW_FAST && ((PBL_RW_PAR && par && front_par(V, blen, flags, L.sl, agg, pos, &roff)) ||
+                        front_fast(V, blen, flags, L.sl, agg, &roff))) {
+      wave_sync();
+      PSTAMP(A, b, 3, l == 0);
+      emit_fast(A, b, V, L.sl, roff, excl, agg);
+      PSTAMP(A, b, 4, l == 0);
+      return;
+    }
+    if (l == 0) g_atomic_add(&O.totals->n_slow_blocks, 1u);
+    wave_sync();
+    slow_walk_t<SlowLds, PBL_RW_VALU>(SlowLds{V}, blen, flags, seq, to_lds_ptr(reinterpret_cast<uint8_t*>(&L.sl)),
+                                      uint32_t(sizeof(L.sl)), kPassAll, O, b, excl, &ss);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wave_sync();  // (the stage may become the key buffer below)
+    PSTAMP(A, b, 3, l == 0);
+  } else if (l == 0) {
+    g_atomic_add(&O.totals->n_slow_blocks, 1u);
+  }
+  if (ss.status == PBL_UNSUPPORTED)  // past the stage, or a key past the slot
+    slow_walk_t<SlowGlb, PBL_BIG_U>(SlowGlb{to_glb(g), blen}, blen, flags, seq,
+                                    to_lds_ptr(reinterpret_cast<uint8_t*>(L.st.x)), uint32_t(sizeof(L.st)), kPassAll,
+                                    O, b, excl, &ss);
+  PSTAMP(A, b, 4, l == 0);
+  if (ss.status != PBL_OK && l == 0) {
+    // the walk the size pass restated cannot disagree with it; if it ever
+    // did, the block reports the walk's status
+    to_glb(O.blk_status)[b] = ss.status;
+    g_atomic_or(&O.totals->status_mask, 1u << ss.status);
+    g_atomic_add(&O.totals->n_bad_blocks, 1u);
+  }
+}
+
+}  // namespace rwave

@@ -1,8 +1,12 @@
-"""The row kernel -- the staging-pool kernel (rowblk_pool.hip.h, with its
-general walk and the big-block passes) -- against the oracle: bit-exact on every
+"""The row kernels -- the staging-pool kernel (rowblk_pool.hip.h, with its
+general walk and the big-block passes; PBL_KERNEL_POOL) and the two-pass form
+of PBL_BATCH_VARLEN batches (rowblk_wave.hip.h: lane-per-block size walk,
+bases scan, wave-per-block emit) -- against the oracle: bit-exact on every
 output array, over reference blocks, synthetic configs, random and fuzzed
-blocks, value prefixes, blocks past the LDS limits, the general-path fallbacks
-and batches whose block shapes vary."""
+blocks, value prefixes, blocks past the LDS limits, the general-path fallbacks,
+batches whose block shapes vary, overflowing capacities and the size pass.
+(Batches whose flags need key bytes to size a block -- value prefixes --
+take the pool kernel under either flag.)"""
 import os
 import random
 
@@ -15,7 +19,7 @@ from pebble_amd.rowblk import Writer, gen_row_blocks
 from test_rowblk_gpu import GOLDEN, assert_same, pack, random_block
 
 pytestmark = pytest.mark.gpu
-KERNELS = {"pool": N.PBL_KERNEL_POOL}
+KERNELS = {"pool": N.PBL_KERNEL_POOL, "wave": N.PBL_BATCH_VARLEN}
 
 
 @pytest.fixture(params=sorted(KERNELS))
@@ -148,3 +152,47 @@ def test_big_blocks_with_keys_near_the_slot():
     blocks += [bytes(small[0][o:o + l]) for o, l in zip(small[1], small[2])]
     rng.shuffle(blocks)
     check(*pack(blocks), 0, "big blocks, keys near the slot")
+
+
+def test_keys_past_the_wave_key_buffer(kern):
+    """Blocks inside the 32 KiB stage whose keys outgrow the two-pass emit's
+    4 KiB LDS key buffer (re-walked from global memory with the stage as the
+    key buffer), shared prefixes reaching into the long keys, next to ordinary
+    blocks."""
+    from rowutil import make_trailer
+    rng = random.Random(81)
+    blocks = []
+    for i, kl in enumerate([1000, 4000, 4047, 4048, 4100, 6000, 9000]):
+        w = Writer(rng.choice([1, 2, 16]))
+        base = bytes(rng.randrange(256) for _ in range(kl - 16))
+        for k in range(3):
+            w.add(base + b"%08d" % (10 * i + k), make_trailer(3 + k, 1), bytes([k + i]) * rng.choice([0, 50, 3000]))
+        blocks.append(w.finish())
+    small = gen_row_blocks(13, 12, 32768, 16, 16, 100)
+    blocks += [bytes(small[0][o:o + l]) for o, l in zip(small[1], small[2])]
+    rng.shuffle(blocks)
+    check(*pack(blocks), 0, "keys past the key buffer", kern)
+    check(*pack(blocks), N.PBL_ROW_RAW_KEYS, "keys past the key buffer, raw", kern)
+
+
+def test_overflow_and_size_pass(kern):
+    """Capacities too small: every block reports PBL_OVERFLOW with exact sizes,
+    the retry decodes; the size pass alone gives the same bases and totals."""
+    import torch
+    from pebble_amd.batch import BlockBatch, Capacity, DecodedBatch, decode_into, decode, gen_zipf_blocks, size_batch
+    buf, off, lens, n = gen_zipf_blocks(21, 64, N.PBL_FMT_ROW, 16)
+    b = BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, kern)
+    out = DecodedBatch.allocate(64, Capacity(kv=10, key=10, val=10, rst=10), "cuda")
+    decode_into(b, out)
+    torch.cuda.synchronize()
+    t = out.read_totals()
+    assert t.status_mask & (1 << N.PBL_OVERFLOW) and t.n_kv == n
+    h = decode(b, cap=Capacity(kv=10, key=10, val=10, rst=10)).to_host()
+    assert h["n_kv"] == n and h["status_mask"] == 0
+    s = size_batch(b)
+    torch.cuda.synchronize()
+    ts = s.read_totals()
+    assert (ts.n_kv, ts.key_bytes, ts.val_bytes, ts.n_restarts, ts.status_mask) == \
+        (h["n_kv"], h["key_bytes_total"], h["val_bytes_total"], h["n_restarts"], 0)
+    assert np.array_equal(s.blk_kv_base.cpu().numpy(), h["blk_kv_base"])
+    assert np.array_equal(s.blk_val_base.cpu().numpy(), h["blk_val_base"])
