@@ -462,7 +462,8 @@ int launch_row_wave(const pbl::Args& a, hipStream_t st) {
                      dim3(pbl::kWave), 0, st, a);
   hipLaunchKernelGGL(cw::bases_scan_kernel<true>, dim3(std::min<uint32_t>(nt, uint32_t(cus) * 2)), dim3(pbl::kTPB), 0,
                      st, a);
-  hipLaunchKernelGGL(pbl::row::rwave::row_wave_emit_kernel, dim3(nb), dim3(pbl::kWave), 0, st, a);
+  hipLaunchKernelGGL(pbl::row::rwave::row_wave_emit_kernel, dim3(nb), dim3(pbl::row::rwave::kRwWaves * pbl::kWave), 0,
+                     st, a);
   return hipGetLastError() == hipSuccess ? PBL_OK : PBL_DEVICE_ERROR;
 }
 

@@ -283,8 +283,9 @@ __device__ __forceinline__ void values_from_stage(const uint32_t* vp, const View
   }
 }
 
-// The outputs of a block front_fast described, at bases excl.
-__device__ __forceinline__ void emit_fast(const Args& A, uint32_t b, const View& V, const pool::Slot<false>& W,
+// The keys, per-KV arrays and restart words of a block front_par / front_fast
+// described, at bases excl.
+__device__ __forceinline__ void emit_keys(const Args& A, uint32_t b, const View& V, const pool::Slot<false>& W,
                                           uint32_t roff, const uint64_t excl[kNumComp], const uint64_t agg[kNumComp]) {
   const int l = lane_id();
   const pbl_decode_out& O = A.out;
@@ -298,88 +299,158 @@ __device__ __forceinline__ void emit_fast(const Args& A, uint32_t b, const View&
     pool::key_load<false, View>(W, V, raw, j0, nkv, K);
     pool::key_store<false, View>(W, V, A, b, j0, nkv, excl[0], excl[1], K, kcar);
   }
-  values_from_stage(W.vp, V, nkv, to_glb(O.val_bytes) + excl[2]);
 }
 
-__global__ void __launch_bounds__(kWave) row_wave_emit_kernel(Args A) {
-  __shared__ ELds L;
-  const int l = lane_id();
-  const uint32_t nb = A.in.n_blocks, b = blockIdx.x, flags = A.in.flags;
+// PBL_RW_WAVES 2: a workgroup of two waves per block -- wave 0 stages,
+// describes, then writes the keys and per-KV arrays while wave 1 writes the
+// values (each phase a chain of LDS / issue latencies at one wave per SIMD;
+// side by side they overlap).  1: one wave does both in turn (A/B).
+#ifndef PBL_RW_WAVES
+#define PBL_RW_WAVES 2
+#endif
+constexpr int kRwWaves = PBL_RW_WAVES;
+static_assert(kRwWaves == 1 || kRwWaves == 2, "emit waves per block: 1 or 2");
+
+// One block's bases, status and extent: SCALAR loads (the constant address
+// space: nothing in this kernel writes them).
+template <class T>
+using cptr = __attribute__((address_space(4))) const T*;
+struct RDesc {
+  uint64_t kv0, kv1, k0, k1, v0, v1, r0, r1, boff;
+  uint32_t status, blen;
+};
+__device__ __forceinline__ RDesc load_desc(const Args& A, uint32_t b) {
   const pbl_decode_out& O = A.out;
-  PSTAMP(A, b, 0, l == 0);
-  const gptr<const uint64_t> rcnt = to_glb(
-      reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(O.workspace) + ws_rcnt_offset(nb)));
-  uint64_t excl[kNumComp], agg[kNumComp];
-  excl[0] = to_glb(O.blk_kv_base)[b];
-  excl[1] = to_glb(O.blk_key_base)[b];
-  excl[2] = to_glb(O.blk_val_base)[b];
-  excl[3] = rcnt[b];
-  agg[0] = to_glb(O.blk_kv_base)[b + 1] - excl[0];
-  agg[1] = to_glb(O.blk_key_base)[b + 1] - excl[1];
-  agg[2] = to_glb(O.blk_val_base)[b + 1] - excl[2];
-  agg[3] = rcnt[b + 1] - excl[3];
-  uint32_t status = to_glb(O.blk_status)[b];
+  const uint32_t nb = A.in.n_blocks;
+  const uint8_t* ws = reinterpret_cast<const uint8_t*>(O.workspace);
+  RDesc d;
+  d.kv0 = ((cptr<uint64_t>)O.blk_kv_base)[b];
+  d.kv1 = ((cptr<uint64_t>)O.blk_kv_base)[b + 1];
+  d.k0 = ((cptr<uint64_t>)O.blk_key_base)[b];
+  d.k1 = ((cptr<uint64_t>)O.blk_key_base)[b + 1];
+  d.v0 = ((cptr<uint64_t>)O.blk_val_base)[b];
+  d.v1 = ((cptr<uint64_t>)O.blk_val_base)[b + 1];
+  const cptr<uint64_t> rc = (cptr<uint64_t>)(ws + ws_rcnt_offset(nb));
+  d.r0 = rc[b];
+  d.r1 = rc[b + 1];
+  d.status = ((cptr<uint32_t>)O.blk_status)[b];
+  d.boff = ((cptr<uint64_t>)A.in.block_off)[b];
+  d.blen = ((cptr<uint32_t>)A.in.block_len)[b];
+  return d;
+}
+
+// One block of the emit (both waves).
+__device__ __forceinline__ void emit_block(ELds& L, uint32_t* s_fast, const Args& A, uint32_t b, const RDesc& d) {
+  const int l = lane_id();
+  const bool w0 = kRwWaves == 1 || wave_id() == 0;
+  const uint32_t nb = A.in.n_blocks, flags = A.in.flags;
+  const pbl_decode_out& O = A.out;
+  PSTAMP(A, b, 0, l == 0 && w0);
+  const uint64_t excl[kNumComp] = {d.kv0, d.k0, d.v0, d.r0};
+  const uint64_t agg[kNumComp] = {d.kv1 - d.kv0, d.k1 - d.k0, d.v1 - d.v0, d.r1 - d.r0};
+  uint32_t status = d.status;
   if (status == PBL_OK && overflows(O, excl, agg)) status = PBL_OVERFLOW;
-  const uint64_t boff = to_glb(A.in.block_off)[b];
-  const uint32_t blen = to_glb(A.in.block_len)[b];
+  const uint64_t boff = d.boff;
+  const uint32_t blen = d.blen;
   const bool staged = status == PBL_OK && blen <= kMaxFastLen;
-  const bool par = staged && agg[0] > 0 && agg[0] <= kEntRec;
-  uint32_t pos = 0;
-  if (staged) {  // (in flight under the metadata stores)
-    pool::stage_dma(L.st, A.in.blocks, boff, blen);
-    if (par && uint32_t(l) < agg[0])
-      pos = to_glb(reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(O.workspace) +
-                                                     ws_ent_offset(nb)))[uint64_t(b) * kEntRec + l];
-  }
-  if (l == 0) {
-    if (status != PBL_OK && O.key_off && excl[0] + b < O.kv_cap + nb) {
-      to_glb(O.key_off)[excl[0] + b] = 0;
-      to_glb(O.val_off)[excl[0] + b] = 0;
+  const View V = lds_view(L.st.x, uint32_t(kPad + (boff & 15)));
+  uint32_t fast = 0;
+  if (w0) {
+    const bool par = staged && agg[0] > 0 && agg[0] <= kEntRec;
+    uint32_t pos = 0;
+    if (staged) {  // (in flight under the metadata stores)
+      pool::stage_dma(L.st, A.in.blocks, boff, blen);
+      if (par && uint32_t(l) < agg[0])
+        pos = to_glb(reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(O.workspace) +
+                                                       ws_ent_offset(nb)))[uint64_t(b) * kEntRec + l];
     }
-    write_block_meta(O, b, nb, status, excl, agg, false);
-  }
-  PSTAMP(A, b, 1, l == 0);
-  if (status != PBL_OK) return;
-  const uint8_t* g = A.in.blocks + boff;
-  const uint64_t seq = A.in.synthetic_seq_num;
-  SlowState ss;
-  ss.status = PBL_UNSUPPORTED;
-  if (staged) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    wave_sync();
-    PSTAMP(A, b, 2, l == 0);
-    const View V = lds_view(L.st.x, uint32_t(kPad + (boff & 15)));
-    uint32_t roff = 0;
-    if (PBL_RW_FAST && ((PBL_RW_PAR && par && front_par(V, blen, flags, L.sl, agg, pos, &roff)) ||
-                        front_fast(V, blen, flags, L.sl, agg, &roff))) {
+    if (l == 0) {
+      if (status != PBL_OK && O.key_off && excl[0] + b < O.kv_cap + nb) {
+        to_glb(O.key_off)[excl[0] + b] = 0;
+        to_glb(O.val_off)[excl[0] + b] = 0;
+      }
+      // (the bases are the scan's; the status, the counters and the totals)
+      to_glb(O.blk_status)[b] = status;
+      if (status != PBL_OK) {
+        g_atomic_or(&O.totals->status_mask, 1u << status);
+        g_atomic_add(&O.totals->n_bad_blocks, 1u);
+      }
+      if (b == nb - 1) {
+        gptr<pbl_totals> T = to_glb(O.totals);
+        T->n_kv = d.kv1;
+        T->key_bytes = d.k1;
+        T->val_bytes = d.v1;
+        T->n_restarts = d.r1;
+      }
+    }
+    PSTAMP(A, b, 1, l == 0);
+    if (staged) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       wave_sync();
-      PSTAMP(A, b, 3, l == 0);
-      emit_fast(A, b, V, L.sl, roff, excl, agg);
-      PSTAMP(A, b, 4, l == 0);
-      return;
+      PSTAMP(A, b, 2, l == 0);
+      uint32_t roff = 0;
+      if (PBL_RW_FAST && ((PBL_RW_PAR && par && front_par(V, blen, flags, L.sl, agg, pos, &roff)) ||
+                          front_fast(V, blen, flags, L.sl, agg, &roff)))
+        fast = roff + 1;
     }
+    if (kRwWaves > 1 && l == 0) *s_fast = fast;
+  }
+  if (kRwWaves > 1) {
+    __syncthreads();
+    fast = *s_fast;
+  }
+  if (fast) {
+    PSTAMP(A, b, 3, l == 0 && w0);
+    if (w0) {
+      emit_keys(A, b, V, L.sl, fast - 1, excl, agg);
+      PSTAMP(A, b, 5, l == 0);
+    }
+    if (kRwWaves == 1 || !w0) {
+      values_from_stage(L.sl.vp, V, uint32_t(agg[0]), to_glb(O.val_bytes) + excl[2]);
+      PSTAMP(A, b, 6, l == 0);
+    }
+    PSTAMP(A, b, 4, l == 0 && w0);
+  } else if (w0 && status == PBL_OK) {
+    // the general walk: on the stage with the slot as its key buffer; a key
+    // past the slot, or a block past the stage, from global memory with the
+    // stage as the key buffer
+    const uint8_t* g = A.in.blocks + boff;
+    const uint64_t seq = A.in.synthetic_seq_num;
     if (l == 0) g_atomic_add(&O.totals->n_slow_blocks, 1u);
-    wave_sync();
-    slow_walk_t<SlowLds, PBL_RW_VALU>(SlowLds{V}, blen, flags, seq, to_lds_ptr(reinterpret_cast<uint8_t*>(&L.sl)),
-                                      uint32_t(sizeof(L.sl)), kPassAll, O, b, excl, &ss);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    wave_sync();  // (the stage may become the key buffer below)
-    PSTAMP(A, b, 3, l == 0);
-  } else if (l == 0) {
-    g_atomic_add(&O.totals->n_slow_blocks, 1u);
+    SlowState ss;
+    ss.status = PBL_UNSUPPORTED;
+    if (staged) {
+      wave_sync();
+      slow_walk_t<SlowLds, PBL_RW_VALU>(SlowLds{V}, blen, flags, seq, to_lds_ptr(reinterpret_cast<uint8_t*>(&L.sl)),
+                                        uint32_t(sizeof(L.sl)), kPassAll, O, b, excl, &ss);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      wave_sync();  // (the stage may become the key buffer below)
+      PSTAMP(A, b, 3, l == 0);
+    }
+    if (ss.status == PBL_UNSUPPORTED)
+      slow_walk_t<SlowGlb, PBL_BIG_U>(SlowGlb{to_glb(g), blen}, blen, flags, seq,
+                                      to_lds_ptr(reinterpret_cast<uint8_t*>(L.st.x)), uint32_t(sizeof(L.st)),
+                                      kPassAll, O, b, excl, &ss);
+    PSTAMP(A, b, 4, l == 0);
+    if (ss.status != PBL_OK && l == 0) {
+      // the walk the size pass restated cannot disagree with it; if it ever
+      // did, the block reports the walk's status
+      to_glb(O.blk_status)[b] = ss.status;
+      g_atomic_or(&O.totals->status_mask, 1u << ss.status);
+      g_atomic_add(&O.totals->n_bad_blocks, 1u);
+    }
   }
-  if (ss.status == PBL_UNSUPPORTED)  // past the stage, or a key past the slot
-    slow_walk_t<SlowGlb, PBL_BIG_U>(SlowGlb{to_glb(g), blen}, blen, flags, seq,
-                                    to_lds_ptr(reinterpret_cast<uint8_t*>(L.st.x)), uint32_t(sizeof(L.st)), kPassAll,
-                                    O, b, excl, &ss);
-  PSTAMP(A, b, 4, l == 0);
-  if (ss.status != PBL_OK && l == 0) {
-    // the walk the size pass restated cannot disagree with it; if it ever
-    // did, the block reports the walk's status
-    to_glb(O.blk_status)[b] = ss.status;
-    g_atomic_or(&O.totals->status_mask, 1u << ss.status);
-    g_atomic_add(&O.totals->n_bad_blocks, 1u);
-  }
+}
+
+// One workgroup per block, in block order.  (Resident workgroups looping over
+// blocks with the next block's descriptor prefetched measured slower: 1408 /
+// 1310 GiB/s with static / ticketed assignment against 1475 on config 5 RI
+// 16; the dispatcher's own refill hides a new workgroup's first round trip.)
+__global__ void __launch_bounds__(kRwWaves * kWave) row_wave_emit_kernel(Args A) {
+  __shared__ ELds L;
+  __shared__ uint32_t s_fast;  // the block took the lane-parallel form (roff + 1), else 0
+  const uint32_t b = blockIdx.x;
+  emit_block(L, &s_fast, A, b, load_desc(A, b));
 }
 
 }  // namespace rwave

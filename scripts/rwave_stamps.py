@@ -2,7 +2,9 @@
 """Diagnostic: per-phase cycles of the two-pass row emit kernel
 (rowblk_wave.hip.h, PBL_STAMPS build) on config 5's row batch.
 Stamps: 0 start, 1 bases read + block metadata written, 2 staged,
-3 LDS walk done, 4 end (after a global-memory walk, if any)."""
+3 LDS walk done (the metadata pass on the lane-parallel form), 5 keys and
+per-KV arrays written (lane-parallel form, wave 0), 6 values written (wave 1
+of a two-wave workgroup), 4 end (wave 0)."""
 import os
 import sys
 
@@ -27,7 +29,7 @@ torch.cuda.synchronize()
 ws_state = 256 + 10 * nb * 8
 st = out.workspace[ws_state: ws_state + nb * 16 * 8].view(torch.int64).view(nb, 16).cpu().numpy()
 nkv = np.diff(out.blk_kv_base.cpu().numpy())[:nb]
-for nm, a, z in [("bases + meta", 0, 1), ("stage (DMA)", 1, 2), ("LDS walk", 2, 3), ("global walk", 3, 4),
+for nm, a, z in [("bases + meta", 0, 1), ("stage (DMA)", 1, 2), ("LDS walk", 2, 3), ("global walk", 3, 4), ("keys (wave 0)", 3, 5), ("values (wave 1)", 3, 6),
                  ("total", 0, 4)]:
     m = (st[:, a] > 0) & (st[:, z] > 0)
     d = (st[m, z] - st[m, a]).astype(np.float64)
