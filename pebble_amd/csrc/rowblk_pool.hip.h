@@ -584,7 +584,9 @@ __device__ __forceinline__ void store_key_general(const uint64_t* M0, const Src&
 
 // The batch's stores.  Key output offsets: an exclusive wave scan of the user-
 // key lengths per u, `kcar` carrying the running total (KV nkv gets the total).
-template <bool kHide, class Src>
+// kPart (the two-pass row emit splits the stores over two waves): 0 all, 1 all
+// but the long keys' own bytes, 2 only those (K unused).
+template <bool kHide, class Src, int kPart = 0>
 __device__ __forceinline__ void key_store(const Slot<kHide>& W, const Src& V, const Args& A, uint32_t b, uint32_t j0,
                                           uint32_t nkv, uint64_t kvb, uint64_t kbb, const KBatch& K, uint32_t& kcar) {
   const int l = lane_id();
@@ -597,11 +599,13 @@ __device__ __forceinline__ void key_store(const Slot<kHide>& W, const Src& V, co
 #pragma unroll
   for (int u = 0; u < kKU; u++) {
 #if PBL_POOL_KMETA
-    Km[u] = K.m[u];
-    Kmp[u] = K.mp[u];
-#else
-    kv_meta<kHide>(W, j0 + kWave * u + l, nkv, &Km[u], &Kmp[u]);
+    if (kPart != 2) {
+      Km[u] = K.m[u];
+      Kmp[u] = K.mp[u];
+      continue;
+    }
 #endif
+    kv_meta<kHide>(W, j0 + kWave * u + l, nkv, &Km[u], &Kmp[u]);
   }
 #pragma unroll
   for (int u = 0; u < kKU; u++) {
@@ -612,7 +616,7 @@ __device__ __forceinline__ void key_store(const Slot<kHide>& W, const Src& V, co
     kc0[u] = kcar;
     const uint32_t ko = kcar + incl - ukl;
     kcar += last_lane(incl);
-    if (j > nkv) continue;
+    if (kPart == 2 || j > nkv) continue;
     st_out(to_glb(O.key_off) + (kvb + b + j), ko);
     st_out(to_glb(O.val_off) + (kvb + b + j), uint32_t(W.vp[j] & 0xffffu));
     if (j == nkv) continue;
@@ -645,6 +649,7 @@ __device__ __forceinline__ void key_store(const Slot<kHide>& W, const Src& V, co
     if (O.kv_flags) st_out(to_glb(O.kv_flags) + (kvb + j), uint8_t(f));
     if (O.entry_off) st_out(to_glb(O.entry_off) + (kvb + j), uint32_t(m_ksrc(m) - m_hl(m)));
   }
+  if (kPart == 1) return;
   // the own bytes [shared, ukl) of long keys: one contiguous range of the
   // entry each, copied by the whole wave (16-B chunks, the last one ending at
   // the key's end, four per lane in flight)

@@ -284,32 +284,38 @@ __device__ __forceinline__ void values_from_stage(const uint32_t* vp, const View
 }
 
 // The keys, per-KV arrays and restart words of a block front_par / front_fast
-// described, at bases excl.
+// described, at bases excl.  kPart: key_store's (0 all; 1 all but the long
+// keys' own bytes; 2 those and the restart words).
+template <int kPart>
 __device__ __forceinline__ void emit_keys(const Args& A, uint32_t b, const View& V, const pool::Slot<false>& W,
                                           uint32_t roff, const uint64_t excl[kNumComp], const uint64_t agg[kNumComp]) {
   const int l = lane_id();
   const pbl_decode_out& O = A.out;
   const bool raw = (A.in.flags & PBL_ROW_RAW_KEYS) != 0;
   const uint32_t nkv = uint32_t(agg[0]), nres = uint32_t(agg[3]);
-  if (O.restarts)
+  if (O.restarts && kPart != 1)
     for (uint32_t r = l; r < nres; r += kWave) to_glb(O.restarts)[excl[3] + r] = V.le32(roff + 4 * r);
   uint32_t kcar = 0;
   for (uint32_t j0 = 0; j0 <= nkv; j0 += kWave) {
     pool::KBatch K;
-    pool::key_load<false, View>(W, V, raw, j0, nkv, K);
-    pool::key_store<false, View>(W, V, A, b, j0, nkv, excl[0], excl[1], K, kcar);
+    if (kPart != 2) pool::key_load<false, View>(W, V, raw, j0, nkv, K);
+    pool::key_store<false, View, kPart>(W, V, A, b, j0, nkv, excl[0], excl[1], K, kcar);
   }
 }
 
 // PBL_RW_WAVES 2: a workgroup of two waves per block -- wave 0 stages,
 // describes, then writes the keys and per-KV arrays while wave 1 writes the
 // values (each phase a chain of LDS / issue latencies at one wave per SIMD;
-// side by side they overlap).  1: one wave does both in turn (A/B).
+// side by side they overlap).  3: a third wave takes the long keys' own bytes
+// and the restart words from wave 0 (config 5 RI 16: a block's latency 18.8 K
+// -> 16.9 K cycles, the rate unchanged, 1540 vs 1537 GiB/s).  1: one wave does
+// all in turn (A/B: 1314 GiB/s).  Without the value stores the rate is 1752
+// (diagnostic build): the value writes cost 11 %.
 #ifndef PBL_RW_WAVES
 #define PBL_RW_WAVES 2
 #endif
 constexpr int kRwWaves = PBL_RW_WAVES;
-static_assert(kRwWaves == 1 || kRwWaves == 2, "emit waves per block: 1 or 2");
+static_assert(kRwWaves >= 1 && kRwWaves <= 3, "emit waves per block: 1 to 3");
 
 // One block's bases, status and extent: SCALAR loads (the constant address
 // space: nothing in this kernel writes them).
@@ -402,10 +408,15 @@ __device__ __forceinline__ void emit_block(ELds& L, uint32_t* s_fast, const Args
   if (fast) {
     PSTAMP(A, b, 3, l == 0 && w0);
     if (w0) {
-      emit_keys(A, b, V, L.sl, fast - 1, excl, agg);
+      if (kRwWaves == 3) emit_keys<1>(A, b, V, L.sl, fast - 1, excl, agg);
+      else emit_keys<0>(A, b, V, L.sl, fast - 1, excl, agg);
       PSTAMP(A, b, 5, l == 0);
     }
-    if (kRwWaves == 1 || !w0) {
+    if (kRwWaves == 3 && wave_id() == 2) {
+      emit_keys<2>(A, b, V, L.sl, fast - 1, excl, agg);
+      PSTAMP(A, b, 7, l == 0);
+    }
+    if (kRwWaves == 1 || wave_id() == 1) {
       values_from_stage(L.sl.vp, V, uint32_t(agg[0]), to_glb(O.val_bytes) + excl[2]);
       PSTAMP(A, b, 6, l == 0);
     }

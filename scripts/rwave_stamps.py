@@ -4,7 +4,8 @@
 Stamps: 0 start, 1 bases read + block metadata written, 2 staged,
 3 LDS walk done (the metadata pass on the lane-parallel form), 5 keys and
 per-KV arrays written (lane-parallel form, wave 0), 6 values written (wave 1
-of a two-wave workgroup), 4 end (wave 0)."""
+of a two-wave workgroup), 7 long keys' own bytes and restarts (wave 2 of a
+three-wave workgroup), 4 end (wave 0)."""
 import os
 import sys
 
@@ -15,7 +16,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from pebble_amd import _native as N  # noqa: E402
-from pebble_amd.batch import BlockBatch, decode, gen_zipf_blocks  # noqa: E402
+from pebble_amd.batch import BlockBatch, decode, decode_into, gen_zipf_blocks  # noqa: E402
 
 nb = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 ri = int(sys.argv[2]) if len(sys.argv) > 2 else 16
@@ -26,10 +27,20 @@ print("blocks: len median", np.median(lens), "p90", np.percentile(lens, 90), "ma
 for _ in range(3):
     out = decode(b)
 torch.cuda.synchronize()
+# one more launch with the stamp words cleared, timed by HIP events (the
+# s_memtime clock against wall time)
+ws_stamps = 256 + 10 * nb * 8
+out.workspace[ws_stamps: ws_stamps + nb * 16 * 8].zero_()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+decode_into(b, out)
+e1.record()
+torch.cuda.synchronize()
+ms = e0.elapsed_time(e1)
 ws_state = 256 + 10 * nb * 8
 st = out.workspace[ws_state: ws_state + nb * 16 * 8].view(torch.int64).view(nb, 16).cpu().numpy()
 nkv = np.diff(out.blk_kv_base.cpu().numpy())[:nb]
-for nm, a, z in [("bases + meta", 0, 1), ("stage (DMA)", 1, 2), ("LDS walk", 2, 3), ("global walk", 3, 4), ("keys (wave 0)", 3, 5), ("values (wave 1)", 3, 6),
+for nm, a, z in [("bases + meta", 0, 1), ("stage (DMA)", 1, 2), ("LDS walk", 2, 3), ("global walk", 3, 4), ("keys (wave 0)", 3, 5), ("values (wave 1)", 3, 6), ("long keys (wave 2)", 3, 7),
                  ("total", 0, 4)]:
     m = (st[:, a] > 0) & (st[:, z] > 0)
     d = (st[m, z] - st[m, a]).astype(np.float64)
@@ -39,5 +50,4 @@ m = (st[:, 2] > 0) & (st[:, 3] > 0)
 d = (st[m, 3] - st[m, 2]).astype(np.float64)
 k = nkv[m].astype(np.float64)
 print("LDS walk per entry: median", np.median(d / np.maximum(k, 1)), "KVs per block mean", k.mean())
-t0 = st[st[:, 0] > 0, 0]
-print("kernel span", t0.max() - t0.min())
+print(f"whole decode {ms:.3f} ms (size + scan + emit)")
