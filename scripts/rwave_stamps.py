@@ -20,8 +20,12 @@ from pebble_amd.batch import BlockBatch, decode, decode_into, gen_zipf_blocks  #
 
 nb = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 ri = int(sys.argv[2]) if len(sys.argv) > 2 else 16
-buf, off, lens, n = gen_zipf_blocks(42, nb, N.PBL_FMT_ROW, ri, 32768, n_threads=16)
-b = BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, 0)
+if len(sys.argv) > 3 and sys.argv[3] == "row":  # config 2's blocks, the two-pass form forced
+    from pebble_amd.rowblk import gen_row_blocks
+    buf, off, lens, n = gen_row_blocks(42, nb, 32768, ri, 16, 100, n_threads=16)
+else:
+    buf, off, lens, n = gen_zipf_blocks(42, nb, N.PBL_FMT_ROW, ri, 32768, n_threads=16)
+b = BlockBatch.from_host(buf, off, lens, "cuda", N.PBL_FMT_ROW, N.PBL_BATCH_VARLEN)
 print("blocks: len median", np.median(lens), "p90", np.percentile(lens, 90), "max", lens.max(), "kvs", n,
       "flags", hex(b.flags))
 for _ in range(3):
