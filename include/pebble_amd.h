@@ -115,9 +115,13 @@ enum {
                                      two-pass form (lane-per-block size walk, bases
                                      scan, wave-per-block emit from LDS, no
                                      look-back) unless HideObsoletePoints or value
-                                     prefixes need key bytes to size a block.  The
-                                     caller knows the lengths on the host (block
-                                     handles carry them).                          */
+                                     prefixes need key bytes to size a block.  Set
+                                     it for row batches of value-dominated blocks
+                                     (few entries per block); blocks of many small
+                                     KVs decode faster without it.  The caller
+                                     knows the lengths on the host (block handles
+                                     carry them); the Python layer also samples
+                                     entry counts (batch.varlen_hint).             */
 #define PBL_KERNEL_SINGLE 0x200u  /* A/B measurement, no effect on results: colblk
                                      batches on the one-block-per-workgroup kernel
                                      instead of the two-pass wave form (row

@@ -460,6 +460,8 @@ int launch_row_wave(const pbl::Args& a, hipStream_t st) {
   const uint32_t nt = (nb + cw::kScanTile - 1) / cw::kScanTile;
   hipLaunchKernelGGL(pbl::row::rwave::row_wave_size_kernel, dim3((nb + pbl::kWave - 1) / pbl::kWave),
                      dim3(pbl::kWave), 0, st, a);
+  hipLaunchKernelGGL(pbl::row::rwave::row_wave_dense_kernel, dim3(std::min<uint32_t>(nb, uint32_t(cus) * 8)),
+                     dim3(pbl::kWave), 0, st, a);
   hipLaunchKernelGGL(cw::bases_scan_kernel<true>, dim3(std::min<uint32_t>(nt, uint32_t(cus) * 2)), dim3(pbl::kTPB), 0,
                      st, a);
   hipLaunchKernelGGL(pbl::row::rwave::row_wave_emit_kernel, dim3(nb), dim3(pbl::row::rwave::kRwWaves * pbl::kWave), 0,

@@ -49,54 +49,169 @@ __host__ __device__ inline bool sizes_without_keys(uint32_t flags) {
 }
 
 // ---- the size pass: lane per block -------------------------------------------
+// A lane walks its block's first kDenseProbe entries; a block that, at that
+// pace, would hold more than 2 kEntRec entries in at least eight restart runs is
+// DENSE (config-2-shaped: 271 entries, a 271-deep chain of round trips for one
+// lane): it is listed for
+// row_wave_dense_kernel, which sizes it lane per restart run, and its entry
+// records are marked absent (entry 0 recorded as 0xffff).  Which kernel sizes
+// a block changes only the speed: both give the general walk's sizes.
+constexpr uint32_t kDenseProbe = 16;
+__device__ __forceinline__ void put_sizes(const pbl_decode_out& O, gptr<uint64_t> rcnt, uint64_t b, uint32_t status,
+                                          uint64_t nkv, uint64_t kb, uint64_t vb, uint32_t nres) {
+  const bool ok = status == PBL_OK;
+  to_glb(O.blk_kv_base)[b] = ok ? nkv : 0;
+  to_glb(O.blk_key_base)[b] = ok ? kb : 0;
+  to_glb(O.blk_val_base)[b] = ok ? vb : 0;
+  rcnt[b] = ok ? nres : 0;
+  to_glb(O.blk_status)[b] = status;
+}
+
+// slow_walk_t's loop from block offset `off` (entries before it counted into
+// nkv / kb / vb, `full` the last key's length), its checks in its order,
+// without the key bytes; at most `limit` entries (then *more is set).
+__device__ __forceinline__ uint32_t seq_count(const SlowGlb& S, uint32_t blen, uint32_t roff, bool raw, uint64_t& off,
+                                              uint64_t& full, uint64_t& nkv, uint64_t& kb, uint64_t& vb,
+                                              uint32_t limit, bool* more, gptr<uint16_t> rec) {
+  uint32_t n = 0;
+  *more = false;
+  while (off < roff) {
+    if (n == limit) { *more = true; return PBL_OK; }
+    const uint4 hw = S.ld16(int64_t(off));
+    const uint32_t hn = uint32_t(min<uint64_t>(15, uint64_t(blen) - off));
+    uint32_t shared, unshared, vlen;
+    const uint32_t a = w_varint(hw, 0, hn, &shared);
+    const uint32_t bb = a ? w_varint(hw, a, hn, &unshared) : 0;
+    const uint32_t c = bb ? w_varint(hw, a + bb, hn, &vlen) : 0;
+    if (!c) return PBL_CORRUPT_BOUNDS;
+    const uint64_t kp = off + a + bb + c;
+    if (blen - kp < unshared) return PBL_CORRUPT_BOUNDS;
+    const uint64_t vp = kp + unshared;
+    if (blen - vp < vlen) return PBL_CORRUPT_BOUNDS;
+    if (shared > full) return PBL_CORRUPT_BOUNDS;
+    const uint64_t klen = uint64_t(shared) + unshared;
+    if (klen > kKeyCapMax) return PBL_UNSUPPORTED;
+    full = klen;
+    if (rec && nkv < kEntRec) rec[nkv] = uint16_t(off);  // (for the emit)
+    nkv++;
+    n++;
+    kb += raw ? klen : (klen >= 8 ? klen - 8 : 0);
+    vb += vlen;
+    off = vp + vlen;
+  }
+  return (kb >> 32 || vb >> 32) ? PBL_UNSUPPORTED : PBL_OK;
+}
+
 __global__ void __launch_bounds__(kWave) row_wave_size_kernel(Args A) {
   const uint32_t nb = A.in.n_blocks, flags = A.in.flags;
   const pbl_decode_out& O = A.out;
   const bool raw = (flags & PBL_ROW_RAW_KEYS) != 0;
-  const gptr<uint64_t> rcnt =
-      to_glb(reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(O.workspace) + ws_rcnt_offset(nb)));
-  const gptr<uint16_t> rec =
-      to_glb(reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(O.workspace) + ws_ent_offset(nb)));
-  for (uint64_t b = uint64_t(blockIdx.x) * kWave + lane_id(); b < nb; b += uint64_t(gridDim.x) * kWave) {
+  uint8_t* ws = reinterpret_cast<uint8_t*>(O.workspace);
+  const gptr<uint64_t> rcnt = to_glb(reinterpret_cast<uint64_t*>(ws + ws_rcnt_offset(nb)));
+  const gptr<uint16_t> rec = to_glb(reinterpret_cast<uint16_t*>(ws + ws_ent_offset(nb)));
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(ws);
+  const gptr<uint32_t> dense_ids = to_glb(reinterpret_cast<uint32_t*>(ws + ws_redo_offset(nb)));
+  for (uint64_t b0 = uint64_t(blockIdx.x) * kWave; b0 < nb; b0 += uint64_t(gridDim.x) * kWave) {
+    const uint64_t b = b0 + lane_id();
+    bool dense = false;
+    if (b < nb) {
+      const uint32_t blen = to_glb(A.in.block_len)[b];
+      const uint8_t* g = A.in.blocks + to_glb(A.in.block_off)[b];
+      uint32_t roff, nres;
+      uint32_t status = rowc::init_checks(GlbRd{g}, blen, flags, &roff, &nres);
+      uint64_t nkv = 0, kb = 0, vb = 0;
+      if (status == PBL_OK) {
+        const SlowGlb S{to_glb(g), blen};
+        const gptr<uint16_t> r = blen <= kMaxFastLen ? rec + b * kEntRec : gptr<uint16_t>(nullptr);
+        uint64_t off = 0, full = 0;
+        bool more = false;
+        status = seq_count(S, blen, roff, raw, off, full, nkv, kb, vb, kDenseProbe, &more, r);
+        if (status == PBL_OK && more) {
+          // at this pace more than 2 kEntRec entries, in at least eight
+          // restart runs to walk side by side (config 5 RI 16 with the
+          // threshold at kEntRec entries and four runs: 1558 -> 1480 GiB/s,
+          // its long-run blocks walked lane per run and emitted without
+          // their entry records)
+          dense = nres >= 8 && uint64_t(roff) * kDenseProbe > off * (2 * kEntRec);
+          if (dense) {
+            if (r) r[0] = 0xffffu;
+          } else {
+            status = seq_count(S, blen, roff, raw, off, full, nkv, kb, vb, ~0u, &more, r);
+          }
+        }
+      }
+      if (!dense) put_sizes(O, rcnt, b, status, nkv, kb, vb, nres);
+    }
+    // the dense blocks' ids, one atomic per wave
+    const uint64_t m = __ballot(dense);
+    if (m) {
+      uint32_t base = 0;
+      if (lane_id() == 0) base = g_atomic_add(hdr + rowc::kWsBigRedo, uint32_t(__popcll(m)));
+      base = __shfl(base, 0, kWave);
+      if (dense) dense_ids[base + __popcll(m & ((1ull << lane_id()) - 1))] = uint32_t(b);
+    }
+  }
+}
+
+// Dense blocks: a wave per block, lane per restart run, each run walked from
+// global memory (the pool kernel's per-run rules: runs_bounds, a restart entry
+// with shared 0, each run ending at the next run's start).  Where the runs tile
+// the entries exactly and every entry is clean, the per-run sums ARE the
+// sequential walk's; any other block is counted by seq_count (lane 0).
+__global__ void __launch_bounds__(kWave) row_wave_dense_kernel(Args A) {
+  const uint32_t nb = A.in.n_blocks, flags = A.in.flags;
+  const pbl_decode_out& O = A.out;
+  const bool raw = (flags & PBL_ROW_RAW_KEYS) != 0;
+  const int l = lane_id();
+  uint8_t* ws = reinterpret_cast<uint8_t*>(O.workspace);
+  const gptr<uint64_t> rcnt = to_glb(reinterpret_cast<uint64_t*>(ws + ws_rcnt_offset(nb)));
+  const uint32_t* hdr = reinterpret_cast<const uint32_t*>(ws);
+  const uint32_t n = __hip_atomic_load(to_glb(hdr) + rowc::kWsBigRedo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const gptr<const uint32_t> dense_ids = to_glb(reinterpret_cast<const uint32_t*>(ws + ws_redo_offset(nb)));
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint32_t b = dense_ids[i];
     const uint32_t blen = to_glb(A.in.block_len)[b];
     const uint8_t* g = A.in.blocks + to_glb(A.in.block_off)[b];
-    uint32_t roff, nres;
-    uint32_t status = rowc::init_checks(GlbRd{g}, blen, flags, &roff, &nres);
+    const SlowGlb S{to_glb(g), blen};
+    const uint32_t nres = S.le32(blen - 4), roff = blen - 4u * (1u + nres);  // (the size pass checked them)
     uint64_t nkv = 0, kb = 0, vb = 0;
-    if (status == PBL_OK) {
-      const SlowGlb S{to_glb(g), blen};
-      uint64_t off = 0, full = 0;
-      // slow_walk_t's loop, its checks in its order, without the key bytes
-      while (off < roff) {
+    bool ok = true;
+    for (uint32_t r = l; r < nres && ok; r += kWave) {
+      const uint32_t s0 = S.le32(roff + 4ull * r) & kRestartMask;
+      const uint32_t e0 = r + 1 < nres ? (S.le32(roff + 4ull * r + 4) & kRestartMask) : roff;
+      if (!((r != 0 || s0 == 0) && s0 < e0 && e0 <= roff)) { ok = false; break; }
+      uint64_t off = s0, prev = 0;
+      bool first = true;
+      while (off < e0) {
         const uint4 hw = S.ld16(int64_t(off));
         const uint32_t hn = uint32_t(min<uint64_t>(15, uint64_t(blen) - off));
         uint32_t shared, unshared, vlen;
         const uint32_t a = w_varint(hw, 0, hn, &shared);
         const uint32_t bb = a ? w_varint(hw, a, hn, &unshared) : 0;
         const uint32_t c = bb ? w_varint(hw, a + bb, hn, &vlen) : 0;
-        if (!c) { status = PBL_CORRUPT_BOUNDS; break; }
-        const uint64_t kp = off + a + bb + c;
-        if (blen - kp < unshared) { status = PBL_CORRUPT_BOUNDS; break; }
-        const uint64_t vp = kp + unshared;
-        if (blen - vp < vlen) { status = PBL_CORRUPT_BOUNDS; break; }
-        if (shared > full) { status = PBL_CORRUPT_BOUNDS; break; }
+        const uint64_t np = off + a + bb + c + unshared + vlen;
         const uint64_t klen = uint64_t(shared) + unshared;
-        if (klen > kKeyCapMax) { status = PBL_UNSUPPORTED; break; }
-        full = klen;
-        if (nkv < kEntRec && blen <= kMaxFastLen) rec[b * kEntRec + nkv] = uint16_t(off);  // (for the emit)
+        if (!c || np > e0 || (first ? shared != 0 : shared > prev) || klen > kKeyCapMax) { ok = false; break; }
         nkv++;
         kb += raw ? klen : (klen >= 8 ? klen - 8 : 0);
         vb += vlen;
-        off = vp + vlen;
+        prev = klen;
+        first = false;
+        off = np;
       }
-      if (status == PBL_OK && (kb >> 32 || vb >> 32)) status = PBL_UNSUPPORTED;
     }
-    const bool ok = status == PBL_OK;
-    to_glb(O.blk_kv_base)[b] = ok ? nkv : 0;
-    to_glb(O.blk_key_base)[b] = ok ? kb : 0;
-    to_glb(O.blk_val_base)[b] = ok ? vb : 0;
-    rcnt[b] = ok ? nres : 0;
-    to_glb(O.blk_status)[b] = status;
+    ok = !__ballot(!ok);
+    nkv = wave_sum(nkv);
+    kb = wave_sum(kb);
+    vb = wave_sum(vb);
+    uint32_t status = PBL_OK;
+    if (!ok || kb >> 32 || vb >> 32) {
+      uint64_t off = 0, full = 0;
+      bool more;
+      nkv = kb = vb = 0;
+      status = seq_count(S, blen, roff, raw, off, full, nkv, kb, vb, ~0u, &more, gptr<uint16_t>(nullptr));
+    }
+    if (l == 0) put_sizes(O, rcnt, b, status, nkv, kb, vb, nres);
   }
 }
 
@@ -194,7 +309,7 @@ __device__ __forceinline__ bool front_par(const View& V, uint32_t blen, uint32_t
   uint32_t sh = 0, un = 0, vl = 0, h = 0;
   bool ok = true;
   if (me) {
-    ok = rowc::hdr2(V.ld8(pos), &sh, &un, &vl, &h) && sh + un <= kMaxKl && h <= 15;
+    ok = (l != 0 || pos == 0) && rowc::hdr2(V.ld8(pos), &sh, &un, &vl, &h) && sh + un <= kMaxKl && h <= 15;
     const uint32_t nxt = __shfl(pos, l + 1 < kWave ? l + 1 : l, kWave);
     ok = ok && pos + h + un + vl == (uint32_t(l) + 1 < nkv ? nxt : roff);
   }

@@ -48,3 +48,22 @@ def test_varlen_hint():
     assert varlen_hint(np.r_[np.full(50, 8000), np.full(50, 60000)]) == N.PBL_BATCH_VARLEN
     _, _, lens, _ = gen_zipf_blocks(7, 200, N.PBL_FMT_COL_DEFAULT)
     assert varlen_hint(lens) == N.PBL_BATCH_VARLEN
+
+
+def test_varlen_hint_row_density():
+    """With the host bytes of a row batch the hint also samples the blocks'
+    entry counts: value-dominated Zipf blocks keep PBL_BATCH_VARLEN (the
+    two-pass row form), a mix of config-2 blocks and short table tails (many
+    small KVs per block) does not (the pool kernel)."""
+    from pebble_amd.batch import _row_entries, gen_row_mix, varlen_hint
+    from pebble_amd.rowblk import gen_row_blocks
+    buf, off, lens, n = gen_zipf_blocks(8, 200, N.PBL_FMT_ROW, 16)
+    assert varlen_hint(lens, buf, off, N.PBL_FMT_ROW) == N.PBL_BATCH_VARLEN
+    assert varlen_hint(lens, buf, off, N.PBL_FMT_COL_DEFAULT) == N.PBL_BATCH_VARLEN  # (only row batches sample)
+    assert sum(_row_entries(bytes(buf[o:o + l])) for o, l in zip(off, lens)) == n
+    buf, off, lens, n = gen_row_mix(9, 200, "tail8")
+    assert varlen_hint(lens) == N.PBL_BATCH_VARLEN
+    assert varlen_hint(lens, buf, off, N.PBL_FMT_ROW) == 0
+    b2, o2, l2, n2 = gen_row_blocks(3, 4, 32768, 16, 16, 100)
+    assert _row_entries(bytes(b2[o2[0]:o2[0] + l2[0]])) == n2 // 4
+    assert _row_entries(b"\x00\x01") == -1
