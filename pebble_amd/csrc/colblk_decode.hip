@@ -51,7 +51,7 @@ extern "C" int pbl_decode_batch_colblk(const pbl_block_batch* batch, pbl_decode_
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       return PBL_DEVICE_ERROR;
     namespace cw = pbl::col::cwave;
-    const uint32_t g_s = uint32_t(std::min<uint64_t>(batch->n_blocks, uint64_t(cus) * 4 * PBL_CW_WAVES));
+    const uint32_t g_s = uint32_t(std::min<uint64_t>(batch->n_blocks, uint64_t(cus) * 4 * PBL_CW_SWAVES));
     const uint32_t nt = (batch->n_blocks + cw::kScanTile - 1) / cw::kScanTile;
     const uint32_t* no_ids = nullptr;
     hipLaunchKernelGGL((cw::colblk_wave_size_kernel<false, false>), dim3(g_s), dim3(pbl::kWave), 0, st, a, no_ids);

@@ -63,6 +63,9 @@ namespace cwave {
 #ifndef PBL_CW_WAVES
 #define PBL_CW_WAVES 4  // waves per SIMD (one wave per workgroup; 5: within noise)
 #endif
+#ifndef PBL_CW_SWAVES
+#define PBL_CW_SWAVES 5  // the size pass: 5 waves per SIMD (96 VGPRs, no scratch): config 3 / 5 colblk / 4 +1 %; 6 spills 36 B/lane
+#endif
 constexpr uint32_t kSizeStg = PBL_CW_SSTAGE;
 constexpr uint32_t kKb = PBL_CW_KEYBUF;
 constexpr int kVU = PBL_CW_VALU;
@@ -257,7 +260,7 @@ struct SLds {
   Desc d;
 };
 template <bool kList, bool kHide>
-__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PBL_CW_WAVES)))
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PBL_CW_SWAVES)))
 colblk_wave_size_kernel(Args A, const uint32_t* ids) {
   __shared__ SLds L;
   const int l = lane_id();

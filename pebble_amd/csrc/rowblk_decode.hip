@@ -412,7 +412,7 @@ int launch_mixed(const pbl_block_batch* batch, const pbl::Args& a, hipStream_t s
   const uint32_t* cids = static_cast<const uint32_t*>(ids);
   launch_big_sizes(a, st, small);
   // (3) the colblk sizes, published (the staged wave form, colblk_wave.hip.h)
-  const uint32_t g_cs = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4 * PBL_CW_WAVES));
+  const uint32_t g_cs = uint32_t(std::min<uint64_t>(nb, uint64_t(cus > 0 ? cus : 1) * 4 * PBL_CW_SWAVES));
   if (hide)
     hipLaunchKernelGGL((pbl::col::cwave::colblk_wave_size_kernel<true, true>), dim3(g_cs), dim3(pbl::kWave), 0, st, a,
                        cids);
