@@ -28,7 +28,7 @@ if [ "${PART:-check}" = check ]; then
   run transform --workload transform
   timeout -k 10 200 python bench.py --workload cfg1 --no-e2e > $O/bench_cfg1.json 2> $O/bench_cfg1.err && cat $O/bench_cfg1.json || exit 1
 else
-  for w in ${PROF:-row col mixed zipf:16 zipf:1 zipf:32 zipf:col}; do
+  for w in ${PROF:-row col mixed zipf:16 zipf:1 zipf:32 zipf:col transform}; do
     nbp=65536; [ $w = mixed ] && nbp=131072  # (bench.py's config-4 shard)
     PROF_BLOCKS=$nbp PROF_WORKLOAD=$w PROF_OUT=$O/prof_${w/:/_} bash scripts/gpu_prof.sh > $O/prof_${w/:/_}.log 2>&1 || { tail -5 $O/prof_${w/:/_}.log; exit 1; }
     echo "prof $w done"
